@@ -1,0 +1,146 @@
+"""ctypes binding of libgpk.so (the C ABI declared in include/gpk.h).
+
+The shared library is built in-tree (gopacket_amd/libgpk.so, see
+csrc/Makefile) so the GPU box loads exactly the code in this repository.
+There is no fallback: if the library is missing or a call fails, an
+exception is raised.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libgpk.so")
+SYNTH_PATH = os.path.join(_HERE, "libgpk_synth.so")
+
+# include/gpk.h constants
+GPK_OK = 0
+OUT_IP4_CSUM, OUT_L4_CSUM, OUT_FLOWS, OUT_ALL = 1, 2, 4, 7
+DEC_NONE, DEC_ETHERNET, DEC_DOT1Q, DEC_IPV4, DEC_IPV6, DEC_IPV6_EXT, DEC_TCP, DEC_UDP, DEC_PAYLOAD, \
+    DEC_FRAGMENT = range(10)
+ST_ERR_MASK = 0x7F
+ST_TRUNCATED = 1 << 7
+ST_NLAYERS_SHIFT = 8
+ST_NLAYERS_MASK = 0xFFF
+ST_IP4_CSUM = 1 << 20
+ST_IP4_VALID = 1 << 21
+ST_L4_CSUM = 1 << 22
+ST_L4_VALID = 1 << 23
+ST_L4_UDP = 1 << 24
+ST_LINK_FLOW = 1 << 25
+ST_NET_FLOW = 1 << 26
+ST_NET_IPV6 = 1 << 27
+ST_TRANSPORT_FLOW = 1 << 28
+LAYOUT_ABSENT = 0xFFFFFFFF
+MAX_INLINE_LAYERS = 16
+
+RECORD_DTYPE = np.dtype([("layers", "<u8"), ("status", "<u4"), ("ip4_csum", "<u2"), ("l4_csum", "<u2")])
+LAYOUT_DTYPE = np.dtype([("start", "<u4", (8,)), ("end", "<u4", (8,))])
+# gpk_layout slot -> decoder kind (slot 7: Payload or Fragment)
+LAYOUT_SLOTS = (DEC_ETHERNET, DEC_DOT1Q, DEC_IPV4, DEC_IPV6, DEC_IPV6_EXT, DEC_TCP, DEC_UDP, DEC_PAYLOAD)
+
+# exported symbols, in include/gpk.h order
+EXPORTS = (
+    "gpk_parser_create", "gpk_parser_destroy", "gpk_parser_add_decoder", "gpk_parser_set_options",
+    "gpk_parser_set_outputs", "gpk_parser_decoder_for", "gpk_parser_set_ethertype",
+    "gpk_parser_set_ipprotocol", "gpk_parser_set_tcp_port", "gpk_parser_set_udp_port", "gpk_ctx_create",
+    "gpk_ctx_destroy", "gpk_decode_batch", "gpk_decode_batch_host", "gpk_decoded_list", "gpk_decoded_list_host",
+    "gpk_host_alloc",
+    "gpk_host_free", "gpk_format_error", "gpk_layer_type_name", "gpk_code_layer_type", "gpk_strerror",
+    "gpk_last_hip_error", "gpk_abi_version",
+)
+
+
+class GpkError(RuntimeError):
+    """A negative status from the C ABI."""
+
+
+class Batch(ctypes.Structure):
+    _fields_ = [("data", ctypes.c_void_p), ("offsets", ctypes.c_void_p), ("caplens", ctypes.c_void_p),
+                ("n", ctypes.c_uint64), ("data_bytes", ctypes.c_uint64)]
+
+
+class Results(ctypes.Structure):
+    _fields_ = [("records", ctypes.c_void_p), ("err_args", ctypes.c_void_p), ("flows", ctypes.c_void_p),
+                ("layouts", ctypes.c_void_p)]
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError("gopacket_amd: %s is not built (run __graft_entry__.build() or make -C "
+                          "gopacket_amd/csrc)" % LIB_PATH)
+    L = ctypes.CDLL(LIB_PATH)
+    vp, i64, u32, u64, c_int = ctypes.c_void_p, ctypes.c_int64, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int
+    P = ctypes.POINTER
+    sig = {
+        "gpk_parser_create": ([P(vp), i64], c_int),
+        "gpk_parser_destroy": ([vp], c_int),
+        "gpk_parser_add_decoder": ([vp, c_int], c_int),
+        "gpk_parser_set_options": ([vp, c_int, c_int], c_int),
+        "gpk_parser_set_outputs": ([vp, u32], c_int),
+        "gpk_parser_decoder_for": ([vp, i64], c_int),
+        "gpk_parser_set_ethertype": ([vp, u32, ctypes.c_int32], c_int),
+        "gpk_parser_set_ipprotocol": ([vp, u32, ctypes.c_int32], c_int),
+        "gpk_parser_set_tcp_port": ([vp, u32, ctypes.c_int32], c_int),
+        "gpk_parser_set_udp_port": ([vp, u32, ctypes.c_int32], c_int),
+        "gpk_ctx_create": ([P(vp), c_int], c_int),
+        "gpk_ctx_destroy": ([vp], c_int),
+        "gpk_decode_batch": ([vp, vp, P(Batch), P(Results), vp], c_int),
+        "gpk_decode_batch_host": ([vp, vp, P(Batch), P(Results)], c_int),
+        "gpk_decoded_list": ([vp, vp, P(Batch), u64, P(i64), u32, P(u32)], c_int),
+        "gpk_decoded_list_host": ([vp, vp, ctypes.c_char_p, u32, P(i64), u32, P(u32)], c_int),
+        "gpk_host_alloc": ([P(vp), ctypes.c_size_t], c_int),
+        "gpk_host_free": ([vp], c_int),
+        "gpk_format_error": ([ctypes.c_uint, u32, u32, ctypes.c_char_p, ctypes.c_size_t], c_int),
+        "gpk_layer_type_name": ([i64, ctypes.c_char_p, ctypes.c_size_t], c_int),
+        "gpk_code_layer_type": ([ctypes.c_uint], i64),
+        "gpk_strerror": ([c_int], ctypes.c_char_p),
+        "gpk_last_hip_error": ([], ctypes.c_char_p),
+        "gpk_abi_version": ([], c_int),
+    }
+    for name, (args, res) in sig.items():
+        f = getattr(L, name)
+        f.argtypes = args
+        f.restype = res
+    _lib = L
+    return L
+
+
+def check(rc):
+    if rc != GPK_OK:
+        L = lib()
+        raise GpkError("gpk: %s (%d) %s" % (L.gpk_strerror(rc).decode(), rc, L.gpk_last_hip_error().decode()))
+    return rc
+
+
+_synth = None
+
+
+def synth_lib():
+    """libgpk_synth.so: synthetic benchmark batches (bench/test infrastructure)."""
+    global _synth
+    if _synth is None:
+        if not os.path.exists(SYNTH_PATH):
+            raise ImportError("gopacket_amd: %s is not built" % SYNTH_PATH)
+        S = ctypes.CDLL(SYNTH_PATH)
+        S.gpk_synth_len.argtypes = [ctypes.c_int, ctypes.c_uint64]
+        S.gpk_synth_len.restype = ctypes.c_uint32
+        S.gpk_synth_fill.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_void_p]
+        S.gpk_synth_fill.restype = ctypes.c_uint32
+        S.gpk_synth_batch_host.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p,
+                                           ctypes.c_void_p, ctypes.c_void_p]
+        S.gpk_synth_batch_host.restype = ctypes.c_uint64
+        S.gpk_synth_device.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p,
+                                       ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+        S.gpk_synth_device.restype = ctypes.c_int
+        S.gpk_synth_bytes.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64]
+        S.gpk_synth_bytes.restype = ctypes.c_uint64
+        _synth = S
+    return _synth

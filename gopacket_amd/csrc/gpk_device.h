@@ -1,0 +1,574 @@
+// gpk_device.h — per-packet DecodingLayerParser state machine for gfx950.
+//
+// One lane runs DecodingLayerParser.DecodeLayers (parser.go:303-317) for one
+// packet, following LayersDecoder's loop (layers_decoder.go:60-79). The layer
+// decoders below restate layers/{ethernet,dot1q,ip4,ip6,tcp,udp}.go; their
+// results must be bit-identical to the reference (checked against oracle/).
+//
+// Bytes come from a per-lane LDS window holding the first ~128 bytes of the
+// packet (filled by the kernel with coalesced 16-byte loads); positions past
+// the window fall back to global byte loads (deep stacks, long options).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/gpk.h"
+
+namespace gpk {
+
+// ---- configuration uploaded once per parser change ------------------------
+struct DevTables {
+  int32_t ethertype[65536];
+  int32_t tcp_port[65536];
+  int32_t udp_port[65536];
+  int32_t ipprotocol[256];
+  uint8_t dispatch[GPK_MAX_LAYER_TYPE];  // LayerType -> GPK_DEC_*
+};
+
+struct KParams {
+  const uint8_t* data;
+  const uint64_t* offsets;
+  const uint32_t* caplens;
+  uint64_t n;
+  gpk_record* records;
+  uint32_t* err_args;
+  uint64_t* flows;
+  gpk_layout* layouts;
+  const DevTables* tab;
+  int64_t first;
+  uint32_t outputs;
+  int32_t ignore_unsupported;
+};
+
+// LDS geometry: per lane a header window of WIN_CHUNKS 16-byte chunks.
+// Slot stride is odd in dwords so byte/dword reads at equal packet positions
+// from 32 lanes hit 32 different banks.
+constexpr int kBlock = 256;
+constexpr int kWaves = kBlock / 64;
+constexpr int kWinChunks = 8;
+constexpr int kSlotDw = kWinChunks * 4 + 1;  // 33
+constexpr int kLdsBytes = kBlock * kSlotDw * 4;
+
+// Dynamic LDS of the decode kernels (one declaration, aliased everywhere).
+extern __shared__ __attribute__((aligned(16))) uint32_t gpk_smem[];
+
+__device__ __forceinline__ uint32_t lds8(uint32_t byte_addr) {
+  return ((const uint8_t*)gpk_smem)[byte_addr];
+}
+
+// Packet byte reader: LDS window first, global memory past it.
+struct Rd {
+  const uint8_t* g;  // packet start (global)
+  uint32_t lb;       // LDS byte address of packet byte 0
+  uint32_t win;      // packet bytes present in LDS
+};
+
+__device__ __forceinline__ uint32_t rd8(const Rd& r, uint32_t p) {
+  return p < r.win ? lds8(r.lb + p) : (uint32_t)r.g[p];
+}
+__device__ __forceinline__ uint32_t rd16(const Rd& r, uint32_t p) { return (rd8(r, p) << 8) | rd8(r, p + 1); }
+__device__ __forceinline__ uint32_t rd32(const Rd& r, uint32_t p) { return (rd16(r, p) << 16) | rd16(r, p + 2); }
+
+// Outcome of one DecodeFromBytes + NextLayerType + LayerPayload, returned by
+// value (a struct passed by reference through the inlined decoders ends up in
+// scratch memory).
+struct Res {
+  uint32_t err, a0, a1;  // GPK_ERR_* and its arguments
+  uint32_t trunc;        // DecodeFeedback.SetTruncated was called
+  uint32_t off, len;     // LayerPayload()
+  int32_t next;          // NextLayerType()
+  uint32_t aux;          // UDP: len(Contents)+len(Payload)
+};
+
+__device__ __forceinline__ Res rerr(uint32_t trunc, uint32_t code, uint32_t a0 = 0, uint32_t a1 = 0) {
+  Res x;
+  x.err = code;
+  x.a0 = a0;
+  x.a1 = a1;
+  x.trunc = trunc;
+  x.off = x.len = 0;
+  x.next = 0;
+  x.aux = 0;
+  return x;
+}
+__device__ __forceinline__ Res rok(uint32_t trunc, uint32_t off, uint32_t len, int32_t next, uint32_t aux = 0) {
+  Res x;
+  x.err = x.a0 = x.a1 = 0;
+  x.trunc = trunc;
+  x.off = off;
+  x.len = len;
+  x.next = next;
+  x.aux = aux;
+  return x;
+}
+
+// ---- layers/ethernet.go:42-63 (+ NextLayerType :111-113) ------------------
+__device__ __forceinline__ Res dec_ethernet(const DevTables* T, const Rd& r, uint32_t off, uint32_t len) {
+  if (len < 14) return rerr(0, GPK_ERR_ETH_TOO_SMALL);
+  uint32_t et = rd16(r, off + 12);
+  uint32_t plen = len - 14, trunc = 0;
+  if (et < 0x0600) {  // 802.3 length field: EthernetTypeLLC, trim or flag
+    if (plen < et) trunc = 1;
+    else plen = et;
+    et = 0;
+  }
+  return rok(trunc, off + 14, plen, T->ethertype[et]);
+}
+
+// ---- layers/dot1q.go:30-41, :49-51 -----------------------------------------
+__device__ __forceinline__ Res dec_dot1q(const DevTables* T, const Rd& r, uint32_t off, uint32_t len) {
+  if (len < 4) return rerr(1, GPK_ERR_DOT1Q_SHORT, len);
+  return rok(0, off + 4, len - 4, T->ethertype[rd16(r, off + 2)]);
+}
+
+// ---- layers/ip4.go:178-271, :277-282 ---------------------------------------
+__device__ __forceinline__ Res dec_ipv4(const DevTables* T, const Rd& r, uint32_t off, uint32_t len) {
+  if (len < 20) return rerr(1, GPK_ERR_IP4_HDR_SHORT, len);
+  uint32_t b0 = rd8(r, off);
+  uint32_t length = rd16(r, off + 2);
+  uint32_t ihl = b0 & 0xf;
+  if (length == 0) length = len & 0xffff;  // TSO, uint16 wrap (ip4.go:189-193)
+  if (length < 20) return rerr(0, GPK_ERR_IP4_LEN_SMALL, length);
+  if (ihl < 5) return rerr(0, GPK_ERR_IP4_IHL_SMALL, ihl);
+  uint32_t hl = ihl * 4;
+  if (hl > length) return rerr(0, GPK_ERR_IP4_IHL_GT_LEN, ihl, length);
+  uint32_t trunc = 0;
+  if (len > length) {
+    len = length;
+  } else if (len < length) {
+    trunc = 1;
+    if (hl > len) return rerr(1, GPK_ERR_IP4_HDR_MISSING);
+  }
+  // options (ip4.go:217-256)
+  uint32_t p = off + 20, rem = hl - 20;
+  while (rem > 0) {
+    uint32_t t = rd8(r, p);
+    if (t == 0) break;
+    uint32_t ol = 1;
+    if (t != 1) {
+      if (rem < 2) return rerr(1, GPK_ERR_IP4_OPT_SHORT, rem);
+      ol = rd8(r, p + 1);
+      if (rem < ol) return rerr(1, GPK_ERR_IP4_OPT_EXCEEDS, t, ol);
+      if (ol <= 2) return rerr(trunc, GPK_ERR_IP4_OPT_BADLEN, t, ol);
+    }
+    p += ol;
+    rem -= ol;
+  }
+  uint32_t ff = rd16(r, off + 6);
+  int32_t next = ((ff & 0x2000u) || (ff & 0x1fffu)) ? GPK_LT_FRAGMENT : T->ipprotocol[rd8(r, off + 9)];
+  return rok(trunc, off + hl, len - hl, next);
+}
+
+// ---- IPv6: layers/ip6.go:221-278 with inline HopByHop :509-526,
+//      decodeIPv6ExtensionBase :418-432, TLV :327-346, jumbogram :54-76,
+//      NextLayerType :286-291 -------------------------------------------------
+__device__ __forceinline__ Res dec_ipv6(const DevTables* T, const Rd& r, uint32_t off, uint32_t len) {
+  if (len < 40) return rerr(1, GPK_ERR_IP6_HDR_SHORT, len);
+  uint32_t length = rd16(r, off + 4);
+  uint32_t nh = rd8(r, off + 6);
+  uint32_t poff = off + 40, plen = len - 40;
+  uint32_t next_nh = nh;
+  if (nh == 0) {
+    if (plen < 2) return rerr(1, GPK_ERR_IP6_EXT_SHORT, plen);
+    uint32_t hnh = rd8(r, poff);
+    uint32_t actual = rd8(r, poff + 1) * 8 + 8;
+    if (plen < actual) return rerr(0, GPK_ERR_IP6_EXT_LEN, plen, actual);
+    uint32_t have = 0, joff = 0, jlen = 0;
+    for (uint32_t q = 2; q < actual;) {
+      uint32_t rem = plen - q;
+      if (rem < 2) return rerr(1, GPK_ERR_IP6_TLV_SHORT);
+      uint32_t t = rd8(r, poff + q);
+      uint32_t al = 1;
+      if (t != 0) {
+        al = rd8(r, poff + q + 1) + 2;
+        if (rem < al) return rerr(1, GPK_ERR_IP6_TLV_TOO_SMALL);
+        if (t == 0xC2 && !have) {
+          have = 1;
+          joff = poff + q + 2;
+          jlen = al - 2;
+        }
+      }
+      q += al;
+    }
+    next_nh = hnh;
+    if (have) {
+      if (jlen != 4) return rerr(0, GPK_ERR_IP6_JUMBO_TLV_LEN);
+      uint32_t l = rd32(r, joff);
+      if (l <= 65535u) return rerr(0, GPK_ERR_IP6_JUMBO_SMALL);
+      if (length != 0) return rerr(0, GPK_ERR_IP6_JUMBO_AND_LEN);
+      uint32_t trunc = 0;
+      if (l > plen) {  // payload stays at the HopByHop header (ip6.go:249-256)
+        trunc = 1;
+        l = plen;
+      }
+      return rok(trunc, poff, l, T->ipprotocol[hnh]);
+    }
+    if (length == 0) return rerr(0, GPK_ERR_IP6_LEN0_NO_JUMBO);
+    poff += actual;  // ip6.go:262, then trimmed to the full Length below
+    plen -= actual;
+  }
+  if (length == 0) return rerr(0, GPK_ERR_IP6_LEN0, nh);
+  uint32_t trunc = 0;
+  if (length > plen) {
+    trunc = 1;
+    length = plen;
+  }
+  return rok(trunc, poff, length, T->ipprotocol[next_nh]);
+}
+
+// ---- IPv6ExtensionSkipper ip6.go:443-461 (base :418-432) -------------------
+__device__ __forceinline__ Res dec_ipv6_ext(const DevTables* T, const Rd& r, uint32_t off, uint32_t len) {
+  if (len < 2) return rerr(1, GPK_ERR_IP6_EXT_SHORT, len);
+  uint32_t nh = rd8(r, off);
+  uint32_t actual = rd8(r, off + 1) * 8 + 8;
+  if (len < actual) return rerr(0, GPK_ERR_IP6_EXT_LEN, len, actual);
+  return rok(0, off + actual, len - actual, T->ipprotocol[nh]);
+}
+
+// ---- MPTCP option body tcp.go:347-533 with Go's bounds checks ---------------
+// The option slice has len = bytes left in the TCP header and cap = bytes to
+// the end of the packet. data[i] needs i < len; data[lo:hi] needs hi <= cap
+// then lo <= hi; data[lo:] needs lo <= len. Returns err (0 = ok) and the
+// option length in x.len.
+#define GPK_IDX(i)                                                                  \
+  do {                                                                              \
+    if ((uint32_t)(i) >= slen) return rerr(0, GPK_ERR_PANIC_INDEX, (i), slen);      \
+  } while (0)
+#define GPK_SL(lo, hi)                                                                          \
+  do {                                                                                          \
+    if ((uint32_t)(hi) > scap) return rerr(0, GPK_ERR_PANIC_SLICE_ACAP, (hi), scap);            \
+    if ((uint32_t)(lo) > (uint32_t)(hi)) return rerr(0, GPK_ERR_PANIC_SLICE_B, (lo), (hi));     \
+  } while (0)
+
+__device__ __forceinline__ Res mptcp_option(const Rd& r, uint32_t p, uint32_t slen, uint32_t scap) {
+  GPK_IDX(1);
+  uint32_t ol = rd8(r, p + 1);
+  if (ol == 0) return rerr(0, GPK_ERR_MPTCP_LEN, ol);
+  GPK_IDX(2);
+  uint32_t b2 = rd8(r, p + 2);
+  switch (b2 >> 4) {
+    case 0:  // MP_CAPABLE
+      if (ol != 4 && ol != 12 && ol != 20 && ol != 22 && ol != 24) return rerr(0, GPK_ERR_MP_CAPABLE_LEN, ol);
+      GPK_IDX(3);
+      if (ol >= 12) GPK_SL(4, 12);
+      if (ol >= 20) GPK_SL(12, 20);
+      if (ol >= 22) GPK_SL(20, 22);
+      if (ol == 24) GPK_SL(22, 24);
+      break;
+    case 1:  // MP_JOIN
+      if (ol != 12 && ol != 16 && ol != 24) return rerr(0, GPK_ERR_MP_JOIN_LEN, ol);
+      if (ol == 12) {
+        GPK_IDX(3);
+        GPK_SL(4, 8);
+        GPK_SL(8, 12);
+      } else if (ol == 16) {
+        GPK_IDX(3);
+        GPK_SL(4, 12);
+        GPK_SL(12, 16);
+      } else {
+        GPK_SL(4, 24);
+      }
+      break;
+    case 2: {  // DSS, optionMptcpDsslen tcp.go:553-571
+      GPK_IDX(3);
+      uint32_t f = rd8(r, p + 3);
+      uint32_t A = f & 1, a = f & 2, M = f & 4, m = f & 8;
+      uint32_t l0 = 4 + (A ? (a ? 8 : 4) : 0) + (M ? (m ? 14 : 10) : 0);
+      uint32_t l1 = l0 + (M ? 2 : 0);
+      if (ol != l0 && ol != l1) return rerr(0, GPK_ERR_DSS_LEN, ol);
+      uint32_t lo = 4;
+      if (A) {
+        uint32_t w = a ? 8 : 4;
+        GPK_SL(lo, lo + w);
+        lo += w;
+      }
+      if (M) {
+        uint32_t w = m ? 8 : 4;
+        GPK_SL(lo, lo + w);
+        lo += w;
+        GPK_SL(lo, lo + 4);
+        lo += 4;
+        GPK_SL(lo, lo + 2);
+        lo += 2;
+        if (((ol - lo) & 0xff) == 2) GPK_SL(lo, lo + 2);
+      }
+      break;
+    }
+    case 3: {  // ADD_ADDR, isValidOptionMptcpAddAddrlen tcp.go:573-585
+      uint32_t ver1 = (b2 & 0xf) <= 1;
+      uint32_t e = ver1 ? (b2 & 1) : 0;
+      uint32_t chk = (ver1 && !e) ? ((ol - 8) & 0xff) : ol;
+      if (!(chk == 8 || chk == 10 || chk == 20 || chk == 22)) return rerr(0, GPK_ERR_ADD_ADDR_LEN, ol);
+      GPK_IDX(3);
+      uint32_t lenopt = ol;
+      if (ver1 && !e) {
+        uint32_t lo = (ol - 8) & 0xff;
+        if (lo > slen) return rerr(0, GPK_ERR_PANIC_SLICE_B, lo, slen);
+        lenopt = lo;
+      }
+      if (lenopt == 8) {
+        GPK_SL(4, 8);
+      } else if (lenopt == 10) {
+        GPK_SL(4, 8);
+        GPK_SL(8, 10);
+      } else if (lenopt == 20) {
+        GPK_SL(4, 20);
+      } else if (lenopt == 22) {
+        GPK_SL(4, 20);
+        GPK_SL(20, 22);
+      }
+      break;
+    }
+    case 4:  // REMOVE_ADDR: reads data[3+n] for n < len-3; first bad index is len(data)
+      if (ol < 4) return rerr(0, GPK_ERR_REM_ADDR_LEN, ol);
+      if (ol > slen) return rerr(0, GPK_ERR_PANIC_INDEX, slen, slen);
+      break;
+    case 5:  // MP_PRIO
+      if (ol != 3 && ol != 4) return rerr(0, GPK_ERR_MP_PRIO_LEN, ol);
+      if (ol == 4) GPK_IDX(3);
+      break;
+    case 6:  // MP_FAIL
+      if (ol != 12) return rerr(0, GPK_ERR_MP_FAIL_LEN, ol);
+      GPK_SL(4, 12);
+      break;
+    case 7:  // MP_FASTCLOSE
+      if (ol != 12) return rerr(0, GPK_ERR_MP_FASTCLOSE_LEN, ol);
+      GPK_SL(4, 12);
+      break;
+    case 8:  // MP_TCPRST
+      if (ol != 4) return rerr(0, GPK_ERR_MP_TCPRST_LEN, ol);
+      GPK_IDX(3);
+      break;
+    default:
+      break;
+  }
+  return rok(0, 0, ol, 0);
+}
+#undef GPK_IDX
+#undef GPK_SL
+
+// ---- layers/tcp.go:291-551, NextLayerType :591-597 --------------------------
+__device__ __forceinline__ Res dec_tcp(const DevTables* T, const Rd& r, uint32_t off, uint32_t len,
+                                       uint32_t caplen) {
+  if (len < 20) return rerr(1, GPK_ERR_TCP_HDR_SHORT, len);
+  uint32_t ports = rd32(r, off);
+  uint32_t doff = rd8(r, off + 12) >> 4;
+  if (doff < 5) return rerr(0, GPK_ERR_TCP_DOFF_SMALL, doff);
+  uint32_t ds = doff * 4;
+  if (ds > len) return rerr(1, GPK_ERR_TCP_DOFF_GT_LEN);
+  uint32_t p = off + 20, slen = ds - 20, scap = caplen - p;
+  while (slen > 0) {
+    uint32_t t = rd8(r, p);
+    if (t == 0) break;  // EndList, Padding = rest
+    uint32_t ol = 1;
+    if (t == 30) {
+      Res x = mptcp_option(r, p, slen, scap);
+      if (x.err) return x;
+      ol = x.len;
+      if (ol > slen) return rerr(0, GPK_ERR_PANIC_SLICE_B, ol, slen);  // data[OptionLength:] (tcp.go:548)
+    } else if (t != 1) {
+      if (slen < 2) return rerr(1, GPK_ERR_TCP_OPT_SHORT, slen);
+      ol = rd8(r, p + 1);
+      if (ol < 2) return rerr(0, GPK_ERR_TCP_OPT_LEN_SMALL, ol);
+      if (ol > slen) return rerr(1, GPK_ERR_TCP_OPT_EXCEEDS, ol, slen);
+    }
+    p += ol;
+    slen -= ol;
+    scap -= ol;
+  }
+  int32_t lt = T->tcp_port[ports & 0xffff];
+  if (lt == GPK_LT_PAYLOAD) lt = T->tcp_port[ports >> 16];
+  return rok(0, off + ds, len - ds, lt);
+}
+
+// ---- layers/udp.go:30-56, :114-119 -----------------------------------------
+__device__ __forceinline__ Res dec_udp(const DevTables* T, const Rd& r, uint32_t off, uint32_t len) {
+  if (len < 8) return rerr(1, GPK_ERR_UDP_HDR_SHORT, len);
+  uint32_t ports = rd32(r, off);
+  uint32_t length = rd16(r, off + 4);
+  uint32_t hlen = len, trunc = 0;
+  if (length >= 8) {
+    if (length > len) trunc = 1;
+    else hlen = length;
+  } else if (length != 0) {
+    return rerr(0, GPK_ERR_UDP_TOO_SMALL, length);
+  }
+  int32_t lt = T->udp_port[ports & 0xffff];
+  if (lt == GPK_LT_PAYLOAD) lt = T->udp_port[ports >> 16];
+  return rok(trunc, off + 8, hlen - 8, lt, hlen);
+}
+
+__device__ __forceinline__ uint32_t code_of(int32_t typ) {
+  switch (typ) {
+    case GPK_LT_ETHERNET: return GPK_CODE_ETHERNET;
+    case GPK_LT_DOT1Q: return GPK_CODE_DOT1Q;
+    case GPK_LT_IPV4: return GPK_CODE_IPV4;
+    case GPK_LT_IPV6: return GPK_CODE_IPV6;
+    case GPK_LT_IPV6_HOPBYHOP: return GPK_CODE_IPV6_HOPBYHOP;
+    case GPK_LT_IPV6_ROUTING: return GPK_CODE_IPV6_ROUTING;
+    case GPK_LT_IPV6_FRAGMENT: return GPK_CODE_IPV6_FRAGMENT;
+    case GPK_LT_IPV6_DESTINATION: return GPK_CODE_IPV6_DESTINATION;
+    case GPK_LT_TCP: return GPK_CODE_TCP;
+    case GPK_LT_UDP: return GPK_CODE_UDP;
+    case GPK_LT_PAYLOAD: return GPK_CODE_PAYLOAD;
+    case GPK_LT_FRAGMENT: return GPK_CODE_FRAGMENT;
+    default: return GPK_CODE_NONE;
+  }
+}
+
+__device__ __forceinline__ int kind_for(const DevTables* T, int64_t typ) {
+  return (typ >= 0 && typ < GPK_MAX_LAYER_TYPE) ? (int)T->dispatch[typ] : GPK_DEC_NONE;
+}
+
+// Result of running the parser on one packet.
+// Per decoder instance (gopacket keeps one struct per DecodingLayer, so the
+// last successful DecodeFromBytes wins): the [start, end) of the data slice it
+// was handed. Named registers, not an array: a runtime-indexed per-lane array
+// would live in scratch memory.
+struct Parse {
+  uint64_t layers;
+  uint32_t nlayers;
+  uint32_t s_eth, e_eth, s_d1q, e_d1q, s_ip4, e_ip4, s_ip6, e_ip6;
+  uint32_t s_ext, e_ext, s_tcp, e_tcp, s_udp, e_udp, s_app, e_app;
+  uint32_t app_kind;  // GPK_DEC_PAYLOAD / GPK_DEC_FRAGMENT of s_app/e_app
+  uint32_t dirty;     // bit per decoder kind: its struct was left mid-decode
+  uint32_t last_net;  // GPK_DEC_IPV4 / GPK_DEC_IPV6 / 0
+  uint32_t transport; // GPK_DEC_TCP / GPK_DEC_UDP / 0
+  uint32_t udp_hlen;
+
+  __device__ __forceinline__ void init() {
+    layers = 0;
+    nlayers = 0;
+    s_eth = e_eth = s_d1q = e_d1q = s_ip4 = e_ip4 = s_ip6 = e_ip6 = GPK_LAYOUT_ABSENT;
+    s_ext = e_ext = s_tcp = e_tcp = s_udp = e_udp = s_app = e_app = GPK_LAYOUT_ABSENT;
+    app_kind = 0;
+    dirty = 0;
+    last_net = 0;
+    transport = 0;
+    udp_hlen = 0;
+  }
+  __device__ __forceinline__ void set(int kind, uint32_t s, uint32_t e) {
+    switch (kind) {
+      case GPK_DEC_ETHERNET: s_eth = s; e_eth = e; break;
+      case GPK_DEC_DOT1Q: s_d1q = s; e_d1q = e; break;
+      case GPK_DEC_IPV4: s_ip4 = s; e_ip4 = e; break;
+      case GPK_DEC_IPV6: s_ip6 = s; e_ip6 = e; break;
+      case GPK_DEC_IPV6_EXT: s_ext = s; e_ext = e; break;
+      case GPK_DEC_TCP: s_tcp = s; e_tcp = e; break;
+      case GPK_DEC_UDP: s_udp = s; e_udp = e; break;
+      default: s_app = s; e_app = e; app_kind = kind; break;
+    }
+  }
+  __device__ __forceinline__ uint32_t start(uint32_t kind) const {
+    switch (kind) {
+      case GPK_DEC_ETHERNET: return s_eth;
+      case GPK_DEC_DOT1Q: return s_d1q;
+      case GPK_DEC_IPV4: return s_ip4;
+      case GPK_DEC_IPV6: return s_ip6;
+      case GPK_DEC_IPV6_EXT: return s_ext;
+      case GPK_DEC_TCP: return s_tcp;
+      case GPK_DEC_UDP: return s_udp;
+      default: return kind == app_kind ? s_app : GPK_LAYOUT_ABSENT;
+    }
+  }
+  __device__ __forceinline__ uint32_t end(uint32_t kind) const {
+    switch (kind) {
+      case GPK_DEC_ETHERNET: return e_eth;
+      case GPK_DEC_DOT1Q: return e_d1q;
+      case GPK_DEC_IPV4: return e_ip4;
+      case GPK_DEC_IPV6: return e_ip6;
+      case GPK_DEC_IPV6_EXT: return e_ext;
+      case GPK_DEC_TCP: return e_tcp;
+      case GPK_DEC_UDP: return e_udp;
+      default: return kind == app_kind ? e_app : GPK_LAYOUT_ABSENT;
+    }
+  }
+};
+
+// DecodeLayers: parser.go:303-317 + layers_decoder.go:60-79.
+// FULL: also writes every decoded LayerType to list[] (gpk_decoded_list).
+struct Outcome {
+  uint32_t err, a0, a1, trunc;
+};
+
+template <bool FULL>
+__device__ __forceinline__ Outcome run_parser(const KParams& P, const Rd& r, uint32_t caplen, Parse& q,
+                                              int64_t* list = nullptr, uint32_t list_cap = 0) {
+  const DevTables* T = P.tab;
+  q.init();
+  Outcome out{0, 0, 0, 0};
+  int kind = kind_for(T, P.first);
+  if (kind == GPK_DEC_NONE) {  // LayersDecoder :12-16: (first, nil), decoded untouched
+    if (!P.ignore_unsupported) out.err = GPK_ERR_UNSUPPORTED, out.a0 = (uint32_t)P.first;
+    return out;
+  }
+  int32_t typ = (int32_t)P.first;
+  uint32_t off = 0, len = caplen;
+  for (;;) {
+    Res x;
+    switch (kind) {
+      case GPK_DEC_ETHERNET: x = dec_ethernet(T, r, off, len); break;
+      case GPK_DEC_DOT1Q: x = dec_dot1q(T, r, off, len); break;
+      case GPK_DEC_IPV4: x = dec_ipv4(T, r, off, len); break;
+      case GPK_DEC_IPV6: x = dec_ipv6(T, r, off, len); break;
+      case GPK_DEC_IPV6_EXT: x = dec_ipv6_ext(T, r, off, len); break;
+      case GPK_DEC_TCP: x = dec_tcp(T, r, off, len, caplen); break;
+      case GPK_DEC_UDP: x = dec_udp(T, r, off, len); break;
+      default:  // gopacket.Payload / gopacket.Fragment (base.go:61-70, :115-124)
+        x = rok(0, off + len, 0, GPK_LT_ZERO);
+        break;
+    }
+    out.trunc |= x.trunc;
+    if (x.err) {
+      q.dirty |= 1u << kind;
+      out.err = x.err;
+      out.a0 = x.a0;
+      out.a1 = x.a1;
+      return out;
+    }
+    if (q.nlayers < GPK_MAX_INLINE_LAYERS) q.layers |= (uint64_t)code_of(typ) << (4 * q.nlayers);
+    if (FULL && q.nlayers < list_cap) list[q.nlayers] = typ;
+    q.nlayers++;
+    q.set(kind, off, off + len);
+    if (kind == GPK_DEC_UDP) q.udp_hlen = x.aux;
+    if (kind == GPK_DEC_IPV4 || kind == GPK_DEC_IPV6) q.last_net = kind;
+    if (kind == GPK_DEC_TCP || kind == GPK_DEC_UDP) q.transport = kind;
+    typ = x.next;
+    off = x.off;
+    len = x.len;
+    if (len == 0) return out;  // LayerPayload() empty: success (layers_decoder.go:71-73)
+    kind = kind_for(T, typ);
+    if (kind == GPK_DEC_NONE) {  // (typ, nil): UnsupportedLayerType unless typ == 0
+      if (typ != GPK_LT_ZERO && !P.ignore_unsupported) out.err = GPK_ERR_UNSUPPORTED, out.a0 = (uint32_t)typ;
+      return out;
+    }
+  }
+}
+
+__device__ __forceinline__ bool clean(const Parse& q, uint32_t kind) {
+  return q.start(kind) != GPK_LAYOUT_ABSENT && !((q.dirty >> kind) & 1);
+}
+
+// FoldChecksum, checksum.go:53-58
+__device__ __forceinline__ uint32_t fold(uint32_t c) {
+  c = (c >> 16) + (c & 0xffff);
+  c = (c >> 16) + (c & 0xffff);
+  return (~c) & 0xffff;
+}
+
+// FNV-1a 64 step (flows.go:60-70): h = (h ^ b) * 0x100000001b3.
+__device__ __forceinline__ uint64_t fnv_step(uint64_t h, uint32_t b) {
+  h ^= b;
+  return h * 1099511628211ull;
+}
+__device__ __forceinline__ uint64_t fnv_range(const Rd& r, uint32_t p, uint32_t n) {
+  uint64_t h = 14695981039346656037ull;
+  for (uint32_t i = 0; i < n; i++) h = fnv_step(h, rd8(r, p + i));
+  return h;
+}
+// Flow.FastHash flows.go:167-174
+__device__ __forceinline__ uint64_t flow_hash(uint64_t hs, uint64_t hd, uint32_t typ) {
+  return ((hs + hd) ^ (uint64_t)typ) * 1099511628211ull;
+}
+
+}  // namespace gpk

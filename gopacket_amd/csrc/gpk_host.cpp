@@ -1,0 +1,453 @@
+// gpk_host.cpp — C ABI (include/gpk.h) around the gfx950 decode kernels.
+//
+// Host-side pieces of the DecodingLayerParser surface:
+//   * gpk_parser: the DecodingLayerContainer (parser.go:147-169, Map semantics:
+//     later Put overrides) + DecodingLayerParserOptions (parser.go:337-351) +
+//     the next-layer tables (layers/enums.go:294-353, layers/ports.go:54-183).
+//   * gpk_ctx: one device, its uploaded table copy and staging buffers.
+//   * error text: the exact strings DecodeLayers returns (see gpk.h enum).
+// There is no CPU decode path here: every packet is decoded by the device.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <string>
+
+#include "../../include/gpk.h"
+#include "gpk_device.h"
+#include "gpk_registry_gen.h"
+
+extern "C" hipError_t gpk_launch_decode(const gpk::KParams* P, int with_l4, int with_layout, hipStream_t stream);
+extern "C" hipError_t gpk_launch_list(const gpk::KParams* P, uint64_t index, int64_t* out, uint32_t cap,
+                                      uint32_t* out_n, hipStream_t stream);
+
+namespace {
+
+thread_local char g_hip_err[256] = "";
+
+int hip_fail(hipError_t e, const char* what) {
+  snprintf(g_hip_err, sizeof(g_hip_err), "%s: %s", what, hipGetErrorString(e));
+  return GPK_EHIP;
+}
+#define HIPCHK(x)                                     \
+  do {                                                \
+    hipError_t _e = (x);                              \
+    if (_e != hipSuccess) return hip_fail(_e, #x);    \
+  } while (0)
+
+}  // namespace
+
+struct gpk_parser {
+  int64_t first;
+  int ignore_panic = 0;
+  int ignore_unsupported = 0;
+  uint32_t outputs = GPK_OUT_ALL;
+  uint64_t version = 1;  // bumped on every change; ctx re-uploads tables
+  gpk::DevTables tab;
+};
+
+struct gpk_ctx {
+  int device = 0;
+  gpk::DevTables* dtab = nullptr;
+  const gpk_parser* uploaded = nullptr;
+  uint64_t uploaded_version = 0;
+  // staging for gpk_decode_batch_host / gpk_decoded_list
+  void* dbuf = nullptr;
+  size_t dbuf_bytes = 0;
+  hipStream_t stream = nullptr;
+  std::mutex mu;
+};
+
+static void default_tables(gpk::DevTables& t) {
+  memset(&t, 0, sizeof(t));
+  for (int i = 0; i < GPK_N_ETHERTYPE_ROWS; i++) t.ethertype[GPK_ETHERTYPE_ROWS[i].value] = GPK_ETHERTYPE_ROWS[i].layer_type;
+  for (int i = 0; i < GPK_N_IPPROTOCOL_ROWS; i++) t.ipprotocol[GPK_IPPROTOCOL_ROWS[i].value] = GPK_IPPROTOCOL_ROWS[i].layer_type;
+  for (int p = 0; p < 65536; p++) t.tcp_port[p] = t.udp_port[p] = GPK_LT_PAYLOAD;
+  for (int i = 0; i < GPK_N_TCP_PORT_SWITCH; i++) t.tcp_port[GPK_TCP_PORT_SWITCH[i].port] = GPK_TCP_PORT_SWITCH[i].layer_type;
+  for (int i = 0; i < GPK_N_UDP_PORT_SWITCH; i++) t.udp_port[GPK_UDP_PORT_SWITCH[i].port] = GPK_UDP_PORT_SWITCH[i].layer_type;
+  for (int i = 0; i < GPK_N_TCP_PORT_OVERRIDE; i++) t.tcp_port[GPK_TCP_PORT_OVERRIDE[i].port] = GPK_TCP_PORT_OVERRIDE[i].layer_type;
+  for (int i = 0; i < GPK_N_UDP_PORT_OVERRIDE; i++) t.udp_port[GPK_UDP_PORT_OVERRIDE[i].port] = GPK_UDP_PORT_OVERRIDE[i].layer_type;
+}
+
+extern "C" {
+
+int gpk_abi_version(void) { return GPK_ABI_VERSION; }
+
+const char* gpk_strerror(int status) {
+  switch (status) {
+    case GPK_OK: return "ok";
+    case GPK_EINVAL: return "invalid argument";
+    case GPK_ENOMEM: return "out of memory";
+    case GPK_EHIP: return "HIP runtime error";
+    case GPK_ENODEV: return "no such device";
+    case GPK_EUNSUPP: return "unsupported configuration";
+    default: return "unknown status";
+  }
+}
+
+const char* gpk_last_hip_error(void) { return g_hip_err; }
+
+// ---- parser ------------------------------------------------------------------
+int gpk_parser_create(gpk_parser** out, int64_t first) {
+  if (!out) return GPK_EINVAL;
+  gpk_parser* p = new (std::nothrow) gpk_parser;
+  if (!p) return GPK_ENOMEM;
+  p->first = first;
+  default_tables(p->tab);
+  *out = p;
+  return GPK_OK;
+}
+
+int gpk_parser_destroy(gpk_parser* p) {
+  delete p;
+  return GPK_OK;
+}
+
+static void put(gpk_parser* p, int lt, int kind) {
+  if (lt >= 0 && lt < GPK_MAX_LAYER_TYPE) p->tab.dispatch[lt] = (uint8_t)kind;
+}
+
+int gpk_parser_add_decoder(gpk_parser* p, int kind) {
+  if (!p) return GPK_EINVAL;
+  switch (kind) {  // CanDecode() of each DecodingLayer
+    case GPK_DEC_ETHERNET: put(p, GPK_LT_ETHERNET, kind); break;
+    case GPK_DEC_DOT1Q: put(p, GPK_LT_DOT1Q, kind); break;
+    case GPK_DEC_IPV4: put(p, GPK_LT_IPV4, kind); break;
+    case GPK_DEC_IPV6: put(p, GPK_LT_IPV6, kind); break;
+    case GPK_DEC_IPV6_EXT:  // LayerClassIPv6Extension, layertypes.go:200-206
+      put(p, GPK_LT_IPV6_HOPBYHOP, kind);
+      put(p, GPK_LT_IPV6_ROUTING, kind);
+      put(p, GPK_LT_IPV6_FRAGMENT, kind);
+      put(p, GPK_LT_IPV6_DESTINATION, kind);
+      break;
+    case GPK_DEC_TCP: put(p, GPK_LT_TCP, kind); break;
+    case GPK_DEC_UDP: put(p, GPK_LT_UDP, kind); break;
+    case GPK_DEC_PAYLOAD: put(p, GPK_LT_PAYLOAD, kind); break;
+    case GPK_DEC_FRAGMENT: put(p, GPK_LT_FRAGMENT, kind); break;
+    default: return GPK_EUNSUPP;
+  }
+  p->version++;
+  return GPK_OK;
+}
+
+int gpk_parser_set_options(gpk_parser* p, int ignore_panic, int ignore_unsupported) {
+  if (!p) return GPK_EINVAL;
+  p->ignore_panic = ignore_panic != 0;
+  p->ignore_unsupported = ignore_unsupported != 0;
+  return GPK_OK;
+}
+
+int gpk_parser_set_outputs(gpk_parser* p, uint32_t outputs) {
+  if (!p || (outputs & ~GPK_OUT_ALL)) return GPK_EINVAL;
+  p->outputs = outputs;
+  return GPK_OK;
+}
+
+int gpk_parser_decoder_for(const gpk_parser* p, int64_t lt) {
+  if (!p || lt < 0 || lt >= GPK_MAX_LAYER_TYPE) return GPK_DEC_NONE;
+  return p->tab.dispatch[lt];
+}
+
+int gpk_parser_set_ethertype(gpk_parser* p, uint32_t v, int32_t lt) {
+  if (!p || v > 0xffff) return GPK_EINVAL;
+  p->tab.ethertype[v] = lt;
+  p->version++;
+  return GPK_OK;
+}
+int gpk_parser_set_ipprotocol(gpk_parser* p, uint32_t v, int32_t lt) {
+  if (!p || v > 0xff) return GPK_EINVAL;
+  p->tab.ipprotocol[v] = lt;
+  p->version++;
+  return GPK_OK;
+}
+int gpk_parser_set_tcp_port(gpk_parser* p, uint32_t v, int32_t lt) {
+  if (!p || v > 0xffff) return GPK_EINVAL;
+  p->tab.tcp_port[v] = lt;
+  p->version++;
+  return GPK_OK;
+}
+int gpk_parser_set_udp_port(gpk_parser* p, uint32_t v, int32_t lt) {
+  if (!p || v > 0xffff) return GPK_EINVAL;
+  p->tab.udp_port[v] = lt;
+  p->version++;
+  return GPK_OK;
+}
+
+// ---- context -----------------------------------------------------------------
+int gpk_ctx_create(gpk_ctx** out, int device) {
+  if (!out) return GPK_EINVAL;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return GPK_ENODEV;
+  HIPCHK(hipSetDevice(device));
+  gpk_ctx* c = new (std::nothrow) gpk_ctx;
+  if (!c) return GPK_ENOMEM;
+  c->device = device;
+  if (hipMalloc(&c->dtab, sizeof(gpk::DevTables)) != hipSuccess) {
+    delete c;
+    return GPK_ENOMEM;
+  }
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    (void)hipFree(c->dtab);
+    delete c;
+    return GPK_EHIP;
+  }
+  *out = c;
+  return GPK_OK;
+}
+
+int gpk_ctx_destroy(gpk_ctx* c) {
+  if (!c) return GPK_OK;
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  if (c->dtab) (void)hipFree(c->dtab);
+  if (c->dbuf) (void)hipFree(c->dbuf);
+  delete c;
+  return GPK_OK;
+}
+
+static int upload(gpk_ctx* c, const gpk_parser* p, hipStream_t s) {
+  if (c->uploaded == p && c->uploaded_version == p->version) return GPK_OK;
+  HIPCHK(hipMemcpyAsync(c->dtab, &p->tab, sizeof(gpk::DevTables), hipMemcpyHostToDevice, s));
+  HIPCHK(hipStreamSynchronize(s));  // p->tab may change after we return
+  c->uploaded = p;
+  c->uploaded_version = p->version;
+  return GPK_OK;
+}
+
+static int make_params(gpk_ctx* c, const gpk_parser* p, const gpk_batch* b, const gpk_results* o,
+                       gpk::KParams& P) {
+  if (!c || !p || !b) return GPK_EINVAL;
+  if (b->n && (!b->data || !b->offsets || !b->caplens)) return GPK_EINVAL;
+  // 16-byte chunk reads never leave the 16-byte granule of a valid byte only
+  // if the packet buffer itself is 16-byte aligned.
+  if (((uintptr_t)b->data & 15) != 0) return GPK_EINVAL;
+  if (o && b->n && !o->records) return GPK_EINVAL;
+  if (o && (p->outputs & GPK_OUT_FLOWS) && b->n && !o->flows) return GPK_EINVAL;
+  P.data = b->data;
+  P.offsets = b->offsets;
+  P.caplens = b->caplens;
+  P.n = b->n;
+  P.records = o ? o->records : nullptr;
+  P.err_args = o ? o->err_args : nullptr;
+  P.flows = o && (p->outputs & GPK_OUT_FLOWS) ? o->flows : nullptr;
+  P.layouts = o ? o->layouts : nullptr;
+  P.tab = c->dtab;
+  P.first = p->first;
+  P.outputs = p->outputs;
+  P.ignore_unsupported = p->ignore_unsupported;
+  return GPK_OK;
+}
+
+int gpk_decode_batch(gpk_ctx* c, const gpk_parser* p, const gpk_batch* b, const gpk_results* o, void* stream) {
+  if (!o) return GPK_EINVAL;
+  gpk::KParams P;
+  int rc = make_params(c, p, b, o, P);
+  if (rc) return rc;
+  hipStream_t s = (hipStream_t)stream;
+  std::lock_guard<std::mutex> g(c->mu);
+  HIPCHK(hipSetDevice(c->device));
+  rc = upload(c, p, s);
+  if (rc) return rc;
+  HIPCHK(gpk_launch_decode(&P, (p->outputs & GPK_OUT_L4_CSUM) != 0, o->layouts != nullptr, s));
+  return GPK_OK;
+}
+
+static int ensure_dbuf(gpk_ctx* c, size_t bytes) {
+  if (c->dbuf_bytes >= bytes) return GPK_OK;
+  if (c->dbuf) (void)hipFree(c->dbuf);
+  c->dbuf = nullptr;
+  c->dbuf_bytes = 0;
+  if (hipMalloc(&c->dbuf, bytes) != hipSuccess) return GPK_ENOMEM;
+  c->dbuf_bytes = bytes;
+  return GPK_OK;
+}
+
+static size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
+
+int gpk_decode_batch_host(gpk_ctx* c, const gpk_parser* p, const gpk_batch* hb, const gpk_results* ho) {
+  if (!c || !p || !hb || !ho) return GPK_EINVAL;
+  if (hb->n && (!hb->data || !hb->offsets || !hb->caplens || !ho->records)) return GPK_EINVAL;
+  const uint64_t n = hb->n;
+  const bool flows = (p->outputs & GPK_OUT_FLOWS) && ho->flows;
+  if ((p->outputs & GPK_OUT_FLOWS) && !ho->flows && n) return GPK_EINVAL;
+  size_t o_data = 0, o_off = align_up(o_data + hb->data_bytes + 16), o_cap = align_up(o_off + n * 8),
+         o_rec = align_up(o_cap + n * 4), o_err = align_up(o_rec + n * sizeof(gpk_record)),
+         o_fl = align_up(o_err + (ho->err_args ? n * 8 : 0)), o_lay = align_up(o_fl + (flows ? n * 24 : 0)),
+         total = align_up(o_lay + (ho->layouts ? n * sizeof(gpk_layout) : 0));
+  std::lock_guard<std::mutex> g(c->mu);
+  HIPCHK(hipSetDevice(c->device));
+  int rc = ensure_dbuf(c, total);
+  if (rc) return rc;
+  char* d = (char*)c->dbuf;
+  hipStream_t s = c->stream;
+  HIPCHK(hipMemcpyAsync(d + o_data, hb->data, hb->data_bytes, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(d + o_off, hb->offsets, n * 8, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(d + o_cap, hb->caplens, n * 4, hipMemcpyHostToDevice, s));
+  if (ho->err_args) HIPCHK(hipMemsetAsync(d + o_err, 0, n * 8, s));
+  gpk_batch db{(const uint8_t*)(d + o_data), (const uint64_t*)(d + o_off), (const uint32_t*)(d + o_cap), n,
+               hb->data_bytes};
+  gpk_results dr{(gpk_record*)(d + o_rec), ho->err_args ? (uint32_t*)(d + o_err) : nullptr,
+                 flows ? (uint64_t*)(d + o_fl) : nullptr, ho->layouts ? (gpk_layout*)(d + o_lay) : nullptr};
+  gpk::KParams P;
+  rc = make_params(c, p, &db, &dr, P);
+  if (rc) return rc;
+  rc = upload(c, p, s);
+  if (rc) return rc;
+  HIPCHK(gpk_launch_decode(&P, (p->outputs & GPK_OUT_L4_CSUM) != 0, dr.layouts != nullptr, s));
+  HIPCHK(hipMemcpyAsync(ho->records, dr.records, n * sizeof(gpk_record), hipMemcpyDeviceToHost, s));
+  if (ho->err_args) HIPCHK(hipMemcpyAsync(ho->err_args, dr.err_args, n * 8, hipMemcpyDeviceToHost, s));
+  if (flows) HIPCHK(hipMemcpyAsync(ho->flows, dr.flows, n * 24, hipMemcpyDeviceToHost, s));
+  if (ho->layouts) HIPCHK(hipMemcpyAsync(ho->layouts, dr.layouts, n * sizeof(gpk_layout), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  return GPK_OK;
+}
+
+int gpk_decoded_list(gpk_ctx* c, const gpk_parser* p, const gpk_batch* b, uint64_t index, int64_t* out_types,
+                     uint32_t cap, uint32_t* out_n) {
+  if (!out_n || (cap && !out_types)) return GPK_EINVAL;
+  gpk::KParams P;
+  int rc = make_params(c, p, b, nullptr, P);
+  if (rc) return rc;
+  if (index >= b->n) return GPK_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  HIPCHK(hipSetDevice(c->device));
+  rc = ensure_dbuf(c, align_up(8 * (size_t)cap) + 256);
+  if (rc) return rc;
+  int64_t* dl = (int64_t*)c->dbuf;
+  uint32_t* dn = (uint32_t*)((char*)c->dbuf + align_up(8 * (size_t)cap));
+  hipStream_t s = c->stream;
+  rc = upload(c, p, s);
+  if (rc) return rc;
+  HIPCHK(gpk_launch_list(&P, index, dl, cap, dn, s));
+  uint32_t n = 0;
+  HIPCHK(hipMemcpyAsync(&n, dn, 4, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  uint32_t k = n < cap ? n : cap;
+  if (k) HIPCHK(hipMemcpy(out_types, dl, 8 * (size_t)k, hipMemcpyDeviceToHost));
+  *out_n = n;
+  return GPK_OK;
+}
+
+int gpk_decoded_list_host(gpk_ctx* c, const gpk_parser* p, const uint8_t* pkt, uint32_t caplen, int64_t* out_types,
+                          uint32_t cap, uint32_t* out_n) {
+  if (!c || !p || !out_n || (caplen && !pkt) || (cap && !out_types)) return GPK_EINVAL;
+  size_t o_off = align_up((size_t)caplen + 16), o_cap = o_off + 256, o_list = o_cap + 256,
+         o_n = align_up(o_list + 8 * (size_t)cap), total = o_n + 256;
+  std::lock_guard<std::mutex> g(c->mu);
+  HIPCHK(hipSetDevice(c->device));
+  int rc = ensure_dbuf(c, total);
+  if (rc) return rc;
+  char* d = (char*)c->dbuf;
+  hipStream_t s = c->stream;
+  uint64_t zero = 0;
+  HIPCHK(hipMemcpyAsync(d, pkt, caplen, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(d + o_off, &zero, 8, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(d + o_cap, &caplen, 4, hipMemcpyHostToDevice, s));
+  gpk_batch db{(const uint8_t*)d, (const uint64_t*)(d + o_off), (const uint32_t*)(d + o_cap), 1, caplen};
+  gpk::KParams P;
+  rc = make_params(c, p, &db, nullptr, P);
+  if (rc) return rc;
+  rc = upload(c, p, s);
+  if (rc) return rc;
+  HIPCHK(gpk_launch_list(&P, 0, (int64_t*)(d + o_list), cap, (uint32_t*)(d + o_n), s));
+  uint32_t n = 0;
+  HIPCHK(hipMemcpyAsync(&n, d + o_n, 4, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  uint32_t k = n < cap ? n : cap;
+  if (k) HIPCHK(hipMemcpy(out_types, d + o_list, 8 * (size_t)k, hipMemcpyDeviceToHost));
+  *out_n = n;
+  return GPK_OK;
+}
+
+int gpk_host_alloc(void** out, size_t bytes) {
+  if (!out) return GPK_EINVAL;
+  HIPCHK(hipHostMalloc(out, bytes, hipHostMallocDefault));
+  return GPK_OK;
+}
+
+int gpk_host_free(void* p) {
+  if (p) HIPCHK(hipHostFree(p));
+  return GPK_OK;
+}
+
+// ---- error values ------------------------------------------------------------
+int gpk_layer_type_name(int64_t lt, char* buf, size_t cap) {
+  // LayerType.String(), layertype.go:101-111
+  for (int i = 0; i < GPK_N_LAYER_TYPE_NAMES; i++)
+    if (GPK_LAYER_TYPE_NAMES[i].id == lt) return snprintf(buf, cap, "%s", GPK_LAYER_TYPE_NAMES[i].name);
+  return snprintf(buf, cap, "%lld", (long long)lt);
+}
+
+static const char* ip_protocol_name(uint32_t v) {
+  // IPProtocol.String(), enums_generated.go:131-140
+  for (int i = 0; i < GPK_N_IPPROTOCOL_ROWS; i++)
+    if ((uint32_t)GPK_IPPROTOCOL_ROWS[i].value == v) return GPK_IPPROTOCOL_ROWS[i].name;
+  return "UnknownIPProtocol";
+}
+
+int gpk_format_error(unsigned code, uint32_t a0, uint32_t a1, char* buf, size_t cap) {
+  char lt[64];
+  switch (code) {
+    case GPK_ERR_NONE: return snprintf(buf, cap, "%s", "");
+    case GPK_ERR_UNSUPPORTED:  // parser.go:325-327
+      gpk_layer_type_name((int32_t)a0, lt, sizeof(lt));
+      return snprintf(buf, cap, "No decoder for layer type %s", lt);
+    // panicToError parser.go:329-333 wrapping Go runtime bounds errors
+    case GPK_ERR_PANIC_INDEX: return snprintf(buf, cap, "panic: runtime error: index out of range [%u] with length %u", a0, a1);
+    case GPK_ERR_PANIC_SLICE_ACAP: return snprintf(buf, cap, "panic: runtime error: slice bounds out of range [:%u] with capacity %u", a0, a1);
+    case GPK_ERR_PANIC_SLICE_B: return snprintf(buf, cap, "panic: runtime error: slice bounds out of range [%u:%u]", a0, a1);
+    case GPK_ERR_ETH_TOO_SMALL: return snprintf(buf, cap, "Ethernet packet too small");
+    case GPK_ERR_DOT1Q_SHORT: return snprintf(buf, cap, "802.1Q tag length %u too short", a0);
+    case GPK_ERR_IP4_HDR_SHORT: return snprintf(buf, cap, "Invalid ip4 header. Length %u less than 20", a0);
+    case GPK_ERR_IP4_LEN_SMALL: return snprintf(buf, cap, "Invalid (too small) IP length (%u < 20)", a0);
+    case GPK_ERR_IP4_IHL_SMALL: return snprintf(buf, cap, "Invalid (too small) IP header length (%u < 5)", a0);
+    case GPK_ERR_IP4_IHL_GT_LEN: return snprintf(buf, cap, "Invalid IP header length > IP length (%u > %u)", a0, a1);
+    case GPK_ERR_IP4_HDR_MISSING: return snprintf(buf, cap, "Not all IP header bytes available");
+    case GPK_ERR_IP4_OPT_SHORT: return snprintf(buf, cap, "Invalid ip4 option length. Length %u less than 2", a0);
+    case GPK_ERR_IP4_OPT_EXCEEDS:
+      return snprintf(buf, cap, "IP option length exceeds remaining IP header size, option type %u length %u", a0, a1);
+    case GPK_ERR_IP4_OPT_BADLEN: return snprintf(buf, cap, "Invalid IP option type %u length %u. Must be greater than 2", a0, a1);
+    case GPK_ERR_IP6_HDR_SHORT: return snprintf(buf, cap, "Invalid ip6 header. Length %u less than 40", a0);
+    case GPK_ERR_IP6_JUMBO_AND_LEN: return snprintf(buf, cap, "IPv6 has jumbo length and IPv6 length is not 0");
+    case GPK_ERR_IP6_LEN0_NO_JUMBO: return snprintf(buf, cap, "IPv6 length 0, but HopByHop header does not have jumbogram option");
+    case GPK_ERR_IP6_LEN0: return snprintf(buf, cap, "IPv6 length 0, but next header is %s, not HopByHop", ip_protocol_name(a0));
+    case GPK_ERR_IP6_TLV_SHORT: return snprintf(buf, cap, "IPv6 header option too small");
+    case GPK_ERR_IP6_TLV_TOO_SMALL: return snprintf(buf, cap, "IPv6 header TLV option too small");
+    case GPK_ERR_IP6_EXT_SHORT: return snprintf(buf, cap, "Invalid ip6-extension header. Length %u less than 2", a0);
+    case GPK_ERR_IP6_EXT_LEN: return snprintf(buf, cap, "Invalid ip6-extension header. Length %u less than specified length %u", a0, a1);
+    case GPK_ERR_IP6_JUMBO_TLV_LEN: return snprintf(buf, cap, "Jumbo length TLV data must have length 4");
+    case GPK_ERR_IP6_JUMBO_SMALL: return snprintf(buf, cap, "Jumbo length cannot be less than %d", 65535 + 1);
+    case GPK_ERR_TCP_HDR_SHORT: return snprintf(buf, cap, "Invalid TCP header. Length %u less than 20", a0);
+    case GPK_ERR_TCP_DOFF_SMALL: return snprintf(buf, cap, "Invalid TCP data offset %u < 5", a0);
+    case GPK_ERR_TCP_DOFF_GT_LEN: return snprintf(buf, cap, "TCP data offset greater than packet length");
+    case GPK_ERR_MPTCP_LEN: return snprintf(buf, cap, "MPTCP bad option length %u", a0);
+    case GPK_ERR_MP_CAPABLE_LEN: return snprintf(buf, cap, "MP_CAPABLE bad option length %u", a0);
+    case GPK_ERR_MP_JOIN_LEN: return snprintf(buf, cap, "MP_JOIN bad option length %u", a0);
+    case GPK_ERR_DSS_LEN: return snprintf(buf, cap, "DSS bad option length %u", a0);
+    case GPK_ERR_ADD_ADDR_LEN: return snprintf(buf, cap, "ADD_ADDR bad option length %u", a0);
+    case GPK_ERR_REM_ADDR_LEN: return snprintf(buf, cap, "Rem_ADDR bad option length %u", a0);
+    case GPK_ERR_MP_PRIO_LEN: return snprintf(buf, cap, "MP_PRIO bad option length %u", a0);
+    case GPK_ERR_MP_FAIL_LEN: return snprintf(buf, cap, "MP_FAIL bad option length %u", a0);
+    case GPK_ERR_MP_FASTCLOSE_LEN: return snprintf(buf, cap, "MP_FASTCLOSE bad option length %u", a0);
+    case GPK_ERR_MP_TCPRST_LEN: return snprintf(buf, cap, "MP_TCPRST bad option length %u", a0);
+    case GPK_ERR_TCP_OPT_SHORT: return snprintf(buf, cap, "Invalid TCP option length. Length %u less than 2", a0);
+    case GPK_ERR_TCP_OPT_LEN_SMALL: return snprintf(buf, cap, "Invalid TCP option length %u < 2", a0);
+    case GPK_ERR_TCP_OPT_EXCEEDS: return snprintf(buf, cap, "Invalid TCP option length %u exceeds remaining %u bytes", a0, a1);
+    case GPK_ERR_UDP_HDR_SHORT: return snprintf(buf, cap, "Invalid UDP header. Length %u less than 8", a0);
+    case GPK_ERR_UDP_TOO_SMALL: return snprintf(buf, cap, "UDP packet too small: %u bytes", a0);
+    default: return snprintf(buf, cap, "unknown gpk error %u", code);
+  }
+}
+
+int64_t gpk_code_layer_type(unsigned code) {
+  static const int64_t map[13] = {GPK_LT_ZERO,          GPK_LT_ETHERNET,       GPK_LT_DOT1Q,
+                                  GPK_LT_IPV4,          GPK_LT_IPV6,           GPK_LT_IPV6_HOPBYHOP,
+                                  GPK_LT_IPV6_ROUTING,  GPK_LT_IPV6_FRAGMENT,  GPK_LT_IPV6_DESTINATION,
+                                  GPK_LT_TCP,           GPK_LT_UDP,            GPK_LT_PAYLOAD,
+                                  GPK_LT_FRAGMENT};
+  return code < 13 ? map[code] : -1;
+}
+
+}  // extern "C"

@@ -1,0 +1,145 @@
+"""Thin object layer over the C ABI: parser configuration, device context and
+batch decode calls (host-memory and device-resident). The gopacket-shaped API
+(DecodingLayerParser, layers.*) in parser.py / layers.py is built on this.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from ._lib import check, lib
+
+DECODER_KINDS = {
+    "Ethernet": _lib.DEC_ETHERNET, "Dot1Q": _lib.DEC_DOT1Q, "IPv4": _lib.DEC_IPV4, "IPv6": _lib.DEC_IPV6,
+    "IPv6ExtensionSkipper": _lib.DEC_IPV6_EXT, "TCP": _lib.DEC_TCP, "UDP": _lib.DEC_UDP,
+    "Payload": _lib.DEC_PAYLOAD, "Fragment": _lib.DEC_FRAGMENT,
+}
+
+
+class ParserConfig:
+    """gpk_parser: container + options + next-layer tables (parser.go:182-241)."""
+
+    def __init__(self, first, decoder_kinds=(), ignore_panic=False, ignore_unsupported=False,
+                 outputs=_lib.OUT_ALL):
+        h = ctypes.c_void_p()
+        check(lib().gpk_parser_create(ctypes.byref(h), int(first)))
+        self.h = h
+        self.first = int(first)
+        for k in decoder_kinds:
+            self.add_decoder(k)
+        self.set_options(ignore_panic, ignore_unsupported)
+        self.set_outputs(outputs)
+
+    def add_decoder(self, kind):
+        check(lib().gpk_parser_add_decoder(self.h, int(kind)))
+
+    def set_options(self, ignore_panic, ignore_unsupported):
+        self.ignore_panic = bool(ignore_panic)
+        self.ignore_unsupported = bool(ignore_unsupported)
+        check(lib().gpk_parser_set_options(self.h, int(self.ignore_panic), int(self.ignore_unsupported)))
+
+    def set_outputs(self, outputs):
+        self.outputs = int(outputs)
+        check(lib().gpk_parser_set_outputs(self.h, self.outputs))
+
+    def decoder_for(self, layer_type):
+        return lib().gpk_parser_decoder_for(self.h, int(layer_type))
+
+    def set_ethertype(self, v, lt):
+        check(lib().gpk_parser_set_ethertype(self.h, int(v), int(lt)))
+
+    def set_ipprotocol(self, v, lt):
+        check(lib().gpk_parser_set_ipprotocol(self.h, int(v), int(lt)))
+
+    def set_tcp_port(self, v, lt):
+        check(lib().gpk_parser_set_tcp_port(self.h, int(v), int(lt)))
+
+    def set_udp_port(self, v, lt):
+        check(lib().gpk_parser_set_udp_port(self.h, int(v), int(lt)))
+
+    def __del__(self):
+        h = getattr(self, "h", None)
+        if h and _lib._lib is not None:
+            _lib._lib.gpk_parser_destroy(h)
+            self.h = None
+
+
+class Context:
+    """gpk_ctx: one GPU."""
+
+    def __init__(self, device=0):
+        h = ctypes.c_void_p()
+        check(lib().gpk_ctx_create(ctypes.byref(h), int(device)))
+        self.h = h
+        self.device = device
+
+    def __del__(self):
+        h = getattr(self, "h", None)
+        if h and _lib._lib is not None:
+            _lib._lib.gpk_ctx_destroy(h)
+            self.h = None
+
+    def decode_host(self, parser, data, offsets, caplens, layouts=False):
+        """Host batch in, host results out (copies HtoD, decodes, copies DtoH)."""
+        data = np.ascontiguousarray(data, dtype=np.uint8)
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        caplens = np.ascontiguousarray(caplens, dtype=np.uint32)
+        n = len(offsets)
+        if n and int(offsets.max()) + int(caplens.max()) > len(data):
+            pass  # offsets[i]+caplens[i] is checked per packet below
+        if n and np.any(offsets.astype(np.uint64) + caplens.astype(np.uint64) > len(data)):
+            raise ValueError("packet range outside the data buffer")
+        rec = np.zeros(n, _lib.RECORD_DTYPE)
+        err = np.zeros(2 * n, np.uint32)
+        flows = np.zeros(3 * n, np.uint64)
+        lay = np.zeros(n, _lib.LAYOUT_DTYPE) if layouts else None
+        b = _lib.Batch(data.ctypes.data, offsets.ctypes.data, caplens.ctypes.data, n, len(data))
+        r = _lib.Results(rec.ctypes.data, err.ctypes.data, flows.ctypes.data,
+                         lay.ctypes.data if layouts else None)
+        check(lib().gpk_decode_batch_host(self.h, parser.h, ctypes.byref(b), ctypes.byref(r)))
+        return dict(records=rec, err_args=err, flows=flows, layouts=lay)
+
+    def decode_device(self, parser, data, offsets, caplens, records, err_args=None, flows=None, layouts=None,
+                      stream=None):
+        """Device-resident decode: every argument is a torch CUDA tensor (or an
+        object with data_ptr()); enqueued on `stream` (torch stream or raw handle)."""
+        n = offsets.numel()
+        b = _lib.Batch(data.data_ptr(), offsets.data_ptr(), caplens.data_ptr(), n, data.numel())
+        r = _lib.Results(records.data_ptr(), err_args.data_ptr() if err_args is not None else None,
+                         flows.data_ptr() if flows is not None else None,
+                         layouts.data_ptr() if layouts is not None else None)
+        if stream is None:
+            sp = None
+        elif isinstance(stream, int):
+            sp = stream
+        else:
+            sp = stream.cuda_stream
+        check(lib().gpk_decode_batch(self.h, parser.h, ctypes.byref(b), ctypes.byref(r), sp))
+
+    def decoded_list_host(self, parser, pkt, cap=65536):
+        out = (ctypes.c_int64 * cap)()
+        n = ctypes.c_uint32()
+        pkt = bytes(pkt)
+        check(lib().gpk_decoded_list_host(self.h, parser.h, pkt, len(pkt), out, cap, ctypes.byref(n)))
+        return [out[i] for i in range(min(n.value, cap))]
+
+
+def format_error(code, a0=0, a1=0):
+    buf = ctypes.create_string_buffer(512)
+    lib().gpk_format_error(int(code), int(a0) & 0xFFFFFFFF, int(a1) & 0xFFFFFFFF, buf, 512)
+    return buf.value.decode()
+
+
+def layer_type_name(lt):
+    buf = ctypes.create_string_buffer(128)
+    lib().gpk_layer_type_name(int(lt), buf, 128)
+    return buf.value.decode()
+
+
+CODE_TO_LAYER_TYPE = (0, 17, 15, 20, 21, 46, 47, 48, 49, 44, 45, 2, 3)
+
+
+def decode_codes(layers_word, n):
+    """The inline decoded list of a gpk_record (first min(n,16) entries)."""
+    w = int(layers_word)
+    return [CODE_TO_LAYER_TYPE[(w >> (4 * k)) & 15] for k in range(min(n, _lib.MAX_INLINE_LAYERS))]

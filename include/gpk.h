@@ -1,0 +1,292 @@
+/*
+ * gpk.h — C ABI of the MI355X packet decode / checksum / flow-hash engine.
+ *
+ * This is the drop-in boundary for gopacket's DecodingLayerParser fast path.
+ * A Go program binds it through cgo (stub in INTEGRATION.md); the Python and
+ * C++ host mirrors in this repo bind it through ctypes / direct linking.
+ * Plain C types only: pointers, sizes, fixed-width integers. No torch, no HIP
+ * types leak through (streams are passed as void*).
+ *
+ * What each entry point replaces in the reference (gopacket, /root/reference):
+ *   gpk_parser_create / gpk_parser_set_*   NewDecodingLayerParser(first, decoders...)
+ *                                          parser.go:222-233, AddDecodingLayer :200,
+ *                                          SetDecodingLayerContainer :238-241,
+ *                                          DecodingLayerParserOptions :337-351
+ *   gpk_tables_default / gpk_tables_set_*  EthernetType/IPProtocol metadata tables
+ *                                          layers/enums.go:294-353, enums_generated.go:76-156;
+ *                                          RegisterTCPPortLayerType / RegisterUDPPortLayerType
+ *                                          layers/ports.go:99-104,178-183
+ *   gpk_decode_batch                       DecodingLayerParser.DecodeLayers (parser.go:303-317)
+ *                                          applied to every packet of a batch, plus, per packet,
+ *                                          IPv4.VerifyChecksum (layers/ip4.go:323-332),
+ *                                          TCP/UDP.VerifyChecksum (layers/tcp.go:626-640,
+ *                                          layers/udp.go:144-158, layers/tcpip.go:54-69) and
+ *                                          Flow.FastHash of LinkFlow/NetworkFlow/TransportFlow
+ *                                          (flows.go:167-174, layers/ethernet.go:38,
+ *                                          layers/ip4.go:63, layers/ip6.go:49, layers/tcp.go:614,
+ *                                          layers/udp.go:132)
+ *   gpk_decode_batch_host                  the same, starting and ending in host memory
+ *                                          (pcap/afpacket sources hand over host buffers)
+ *   gpk_format_error                       the error values DecodeLayers returns
+ *                                          (UnsupportedLayerType parser.go:321-327, panicToError
+ *                                          :329-333, and every fmt.Errorf/errors.New site of
+ *                                          layers/{ethernet,dot1q,ip4,ip6,tcp,udp}.go)
+ *
+ * Every function returns 0 on success or a negative GPK_E* status. No C++
+ * exception crosses this boundary.
+ */
+#ifndef GPK_H
+#define GPK_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GPK_ABI_VERSION 1
+
+/* ---- status codes -------------------------------------------------------- */
+#define GPK_OK 0
+#define GPK_EINVAL (-1)     /* bad argument / batch description */
+#define GPK_ENOMEM (-2)     /* device or host allocation failed */
+#define GPK_EHIP (-3)       /* HIP runtime error (see gpk_last_hip_error) */
+#define GPK_ENODEV (-4)     /* no gfx950 device / device ordinal out of range */
+#define GPK_EUNSUPP (-5)    /* configuration the device path does not implement */
+
+/* ---- LayerType ids (gopacket decode.go:106-117, layers/layertypes.go) ---- */
+#define GPK_LT_ZERO 0
+#define GPK_LT_PAYLOAD 2
+#define GPK_LT_FRAGMENT 3
+#define GPK_LT_DOT1Q 15
+#define GPK_LT_ETHERNET 17
+#define GPK_LT_IPV4 20
+#define GPK_LT_IPV6 21
+#define GPK_LT_TCP 44
+#define GPK_LT_UDP 45
+#define GPK_LT_IPV6_HOPBYHOP 46
+#define GPK_LT_IPV6_ROUTING 47
+#define GPK_LT_IPV6_FRAGMENT 48
+#define GPK_LT_IPV6_DESTINATION 49
+#define GPK_MAX_LAYER_TYPE 2000 /* layertype.go:41 maxLayerType */
+
+/* ---- DecodingLayer implementations the device runs ----------------------- *
+ * Each registers the LayerTypes of its CanDecode() class.                    */
+#define GPK_DEC_NONE 0
+#define GPK_DEC_ETHERNET 1      /* layers.Ethernet          {17}            */
+#define GPK_DEC_DOT1Q 2         /* layers.Dot1Q             {15}            */
+#define GPK_DEC_IPV4 3          /* layers.IPv4              {20}            */
+#define GPK_DEC_IPV6 4          /* layers.IPv6              {21}            */
+#define GPK_DEC_IPV6_EXT 5      /* layers.IPv6ExtensionSkipper {46,47,48,49} (ip6.go:437-461) */
+#define GPK_DEC_TCP 6           /* layers.TCP               {44}            */
+#define GPK_DEC_UDP 7           /* layers.UDP               {45}            */
+#define GPK_DEC_PAYLOAD 8       /* gopacket.Payload         {2}  (base.go:40-70)   */
+#define GPK_DEC_FRAGMENT 9      /* gopacket.Fragment        {3}  (base.go:97-124)  */
+#define GPK_NUM_DEC 10
+
+/* ---- compact codes of the decoded LayerType list --------------------------
+ * gpk_record.layers holds decoded[i] as a 4-bit code in bits [4i, 4i+4).     */
+#define GPK_CODE_NONE 0
+#define GPK_CODE_ETHERNET 1
+#define GPK_CODE_DOT1Q 2
+#define GPK_CODE_IPV4 3
+#define GPK_CODE_IPV6 4
+#define GPK_CODE_IPV6_HOPBYHOP 5
+#define GPK_CODE_IPV6_ROUTING 6
+#define GPK_CODE_IPV6_FRAGMENT 7
+#define GPK_CODE_IPV6_DESTINATION 8
+#define GPK_CODE_TCP 9
+#define GPK_CODE_UDP 10
+#define GPK_CODE_PAYLOAD 11
+#define GPK_CODE_FRAGMENT 12
+#define GPK_MAX_INLINE_LAYERS 16
+
+/* ---- error sites ----------------------------------------------------------
+ * One code per error value DecodeLayers can return. Args are in
+ * err_args[2*i], err_args[2*i+1]; gpk_format_error renders the exact Go text. */
+enum gpk_err {
+  GPK_ERR_NONE = 0,
+  GPK_ERR_UNSUPPORTED = 1,        /* a0=LayerType      parser.go:326  */
+  GPK_ERR_PANIC_INDEX = 2,        /* a0=index a1=len   runtime "index out of range [a0] with length a1" */
+  GPK_ERR_PANIC_SLICE_ACAP = 3,   /* a0=high a1=cap    runtime "slice bounds out of range [:a0] with capacity a1" */
+  GPK_ERR_PANIC_SLICE_B = 4,      /* a0=low a1=high    runtime "slice bounds out of range [a0:a1]" */
+  GPK_ERR_ETH_TOO_SMALL = 10,     /* ethernet.go:44 */
+  GPK_ERR_DOT1Q_SHORT = 11,       /* a0=len dot1q.go:33 */
+  GPK_ERR_IP4_HDR_SHORT = 20,     /* a0=len ip4.go:181 */
+  GPK_ERR_IP4_LEN_SMALL = 21,     /* a0=Length ip4.go:196 */
+  GPK_ERR_IP4_IHL_SMALL = 22,     /* a0=IHL ip4.go:198 */
+  GPK_ERR_IP4_IHL_GT_LEN = 23,    /* a0=IHL a1=Length ip4.go:200 */
+  GPK_ERR_IP4_HDR_MISSING = 24,   /* ip4.go:208 */
+  GPK_ERR_IP4_OPT_SHORT = 25,     /* a0=remaining ip4.go:241 */
+  GPK_ERR_IP4_OPT_EXCEEDS = 26,   /* a0=type a1=length ip4.go:247 */
+  GPK_ERR_IP4_OPT_BADLEN = 27,    /* a0=type a1=length ip4.go:250 */
+  GPK_ERR_IP6_HDR_SHORT = 30,     /* a0=len ip6.go:224 */
+  GPK_ERR_IP6_JUMBO_AND_LEN = 31, /* ip6.go:258 */
+  GPK_ERR_IP6_LEN0_NO_JUMBO = 32, /* ip6.go:260 */
+  GPK_ERR_IP6_LEN0 = 33,          /* a0=NextHeader ip6.go:267 */
+  GPK_ERR_IP6_TLV_SHORT = 34,     /* ip6.go:330 */
+  GPK_ERR_IP6_TLV_TOO_SMALL = 35, /* ip6.go:342 */
+  GPK_ERR_IP6_EXT_SHORT = 36,     /* a0=len ip6.go:421 */
+  GPK_ERR_IP6_EXT_LEN = 37,       /* a0=len a1=actual ip6.go:427 */
+  GPK_ERR_IP6_JUMBO_TLV_LEN = 38, /* ip6.go:68 */
+  GPK_ERR_IP6_JUMBO_SMALL = 39,   /* ip6.go:72 */
+  GPK_ERR_TCP_HDR_SHORT = 40,     /* a0=len tcp.go:294 */
+  GPK_ERR_TCP_DOFF_SMALL = 41,    /* a0=DataOffset tcp.go:323 */
+  GPK_ERR_TCP_DOFF_GT_LEN = 42,   /* tcp.go:330 */
+  GPK_ERR_MPTCP_LEN = 43,         /* a0=len tcp.go:351 */
+  GPK_ERR_MP_CAPABLE_LEN = 44,    /* a0=len tcp.go:357 */
+  GPK_ERR_MP_JOIN_LEN = 45,       /* a0=len tcp.go:384 */
+  GPK_ERR_DSS_LEN = 46,           /* a0=len tcp.go:415 */
+  GPK_ERR_ADD_ADDR_LEN = 47,      /* a0=len tcp.go:455 */
+  GPK_ERR_REM_ADDR_LEN = 48,      /* a0=len tcp.go:487 */
+  GPK_ERR_MP_PRIO_LEN = 49,       /* a0=len tcp.go:499 */
+  GPK_ERR_MP_FAIL_LEN = 50,       /* a0=len tcp.go:509 */
+  GPK_ERR_MP_FASTCLOSE_LEN = 51,  /* a0=len tcp.go:517 */
+  GPK_ERR_MP_TCPRST_LEN = 52,     /* a0=len tcp.go:524 */
+  GPK_ERR_TCP_OPT_SHORT = 53,     /* a0=remaining tcp.go:537 */
+  GPK_ERR_TCP_OPT_LEN_SMALL = 54, /* a0=len tcp.go:541 */
+  GPK_ERR_TCP_OPT_EXCEEDS = 55,   /* a0=len a1=remaining tcp.go:544 */
+  GPK_ERR_UDP_HDR_SHORT = 60,     /* a0=len udp.go:33 */
+  GPK_ERR_UDP_TOO_SMALL = 61      /* a0=Length udp.go:53 */
+};
+
+/* ---- per-packet result record (16 B, one dwordx4 store per packet) -------- */
+typedef struct gpk_record {
+  uint64_t layers;   /* decoded list, 4-bit GPK_CODE_* per entry (first 16) */
+  uint32_t status;   /* GPK_ST_* bit fields below */
+  uint16_t ip4_csum; /* IPv4 ChecksumVerificationResult.Correct */
+  uint16_t l4_csum;  /* TCP/UDP ChecksumVerificationResult.Correct */
+} gpk_record;
+
+#define GPK_ST_ERR_MASK 0x7Fu          /* gpk_err code                         */
+#define GPK_ST_TRUNCATED (1u << 7)      /* DecodingLayerParser.Truncated        */
+#define GPK_ST_NLAYERS_SHIFT 8          /* len(decoded), saturating at 4095     */
+#define GPK_ST_NLAYERS_MASK 0xFFFu
+#define GPK_ST_IP4_CSUM (1u << 20)      /* IPv4 checksum computed               */
+#define GPK_ST_IP4_VALID (1u << 21)     /* ... and Valid                        */
+#define GPK_ST_L4_CSUM (1u << 22)       /* TCP or UDP checksum computed         */
+#define GPK_ST_L4_VALID (1u << 23)      /* ... and Valid                        */
+#define GPK_ST_L4_UDP (1u << 24)        /* the transport layer is UDP           */
+#define GPK_ST_LINK_FLOW (1u << 25)     /* flows[0*n+i] holds LinkFlow().FastHash()      */
+#define GPK_ST_NET_FLOW (1u << 26)      /* flows[1*n+i] holds NetworkFlow().FastHash()   */
+#define GPK_ST_NET_IPV6 (1u << 27)      /* the network flow is IPv6                      */
+#define GPK_ST_TRANSPORT_FLOW (1u << 28)/* flows[2*n+i] holds TransportFlow().FastHash() */
+
+static inline unsigned gpk_record_err(const gpk_record* r) { return r->status & GPK_ST_ERR_MASK; }
+static inline unsigned gpk_record_nlayers(const gpk_record* r) {
+  return (r->status >> GPK_ST_NLAYERS_SHIFT) & GPK_ST_NLAYERS_MASK;
+}
+
+/* ---- optional per-packet layout (64 B): where each layer struct points ----
+ * For every DecodingLayer implementation (slot = kind-1, Payload and Fragment
+ * share slot 7) the byte range [start, end) — relative to the packet start —
+ * of the data slice handed to the LAST successful DecodeFromBytes of that
+ * instance (gopacket reuses one struct per type, parser.go:21-28, so the last
+ * writer wins). 0xFFFFFFFF = the layer was not decoded. Every field value of
+ * that struct is a pure function of the packet bytes in that range.          */
+typedef struct gpk_layout {
+  uint32_t start[8];
+  uint32_t end[8];
+} gpk_layout;
+#define GPK_LAYOUT_ABSENT 0xFFFFFFFFu
+
+/* ---- outputs -------------------------------------------------------------- */
+#define GPK_OUT_IP4_CSUM 0x1u  /* IPv4.VerifyChecksum for the last IPv4 in decoded        */
+#define GPK_OUT_L4_CSUM 0x2u   /* TCP/UDP.VerifyChecksum, pseudo-header = last network layer */
+#define GPK_OUT_FLOWS 0x4u     /* Link/Network/Transport Flow.FastHash                    */
+#define GPK_OUT_ALL 0x7u
+
+/* ---- parser configuration (opaque) ---------------------------------------- */
+typedef struct gpk_parser gpk_parser;
+
+/* NewDecodingLayerParser(first): an empty container, default options. */
+int gpk_parser_create(gpk_parser** out, int64_t first_layer_type);
+int gpk_parser_destroy(gpk_parser* p);
+/* AddDecodingLayer(d) / DecodingLayerContainer.Put(d): registers every
+ * LayerType of the decoder's CanDecode() class; a later Put overrides. */
+int gpk_parser_add_decoder(gpk_parser* p, int decoder_kind);
+/* DecodingLayerParserOptions. */
+int gpk_parser_set_options(gpk_parser* p, int ignore_panic, int ignore_unsupported);
+/* Which verification / hashing results to compute (GPK_OUT_*). */
+int gpk_parser_set_outputs(gpk_parser* p, uint32_t outputs);
+/* LayerType -> decoder kind currently registered (GPK_DEC_NONE if none). */
+int gpk_parser_decoder_for(const gpk_parser* p, int64_t layer_type);
+
+/* Next-layer tables: EthernetType[65536], IPProtocol[256], TCP port[65536],
+ * UDP port[65536] -> LayerType. Defaults = the reference registry after init()
+ * (including the Modbus/ENIP port overrides). Overrides made at run time by
+ * RegisterTCPPortLayerType / RegisterUDPPortLayerType or by editing
+ * EthernetTypeMetadata / IPProtocolMetadata are mirrored with these setters. */
+int gpk_parser_set_ethertype(gpk_parser* p, uint32_t ethertype, int32_t layer_type);
+int gpk_parser_set_ipprotocol(gpk_parser* p, uint32_t proto, int32_t layer_type);
+int gpk_parser_set_tcp_port(gpk_parser* p, uint32_t port, int32_t layer_type);
+int gpk_parser_set_udp_port(gpk_parser* p, uint32_t port, int32_t layer_type);
+
+/* ---- device context ------------------------------------------------------- */
+typedef struct gpk_ctx gpk_ctx;
+int gpk_ctx_create(gpk_ctx** out, int device_ordinal);
+int gpk_ctx_destroy(gpk_ctx* ctx);
+
+/* A packed, offset-indexed packet batch. Packet i is data[offsets[i] ..
+ * offsets[i]+caplens[i]). In gpk_decode_batch every pointer is DEVICE memory.
+ * The kernels may read whole 16-byte-aligned chunks that contain a packet
+ * byte; they never touch a chunk that contains none. */
+typedef struct gpk_batch {
+  const uint8_t* data;
+  const uint64_t* offsets;
+  const uint32_t* caplens;
+  uint64_t n;
+  uint64_t data_bytes;
+} gpk_batch;
+
+typedef struct gpk_results {
+  gpk_record* records;  /* [n]   required                                   */
+  uint32_t* err_args;   /* [2n]  optional; written only for packets with err */
+  uint64_t* flows;      /* [3n]  SoA link[n], net[n], transport[n]; required
+                           if GPK_OUT_FLOWS (0 where the flow is absent)     */
+  gpk_layout* layouts;  /* [n]   optional                                    */
+} gpk_results;
+
+/* Device-resident decode of every packet of the batch, enqueued on `stream`
+ * (a hipStream_t, NULL = the null stream). Asynchronous: returns after the
+ * launch. The parser configuration is uploaded once per (ctx, parser change). */
+int gpk_decode_batch(gpk_ctx* ctx, const gpk_parser* p, const gpk_batch* batch,
+                     const gpk_results* out, void* stream);
+
+/* Host-memory variant: batch and results live in host memory (ideally pinned
+ * via gpk_host_alloc). Copies HtoD, decodes, copies DtoH; synchronous. */
+int gpk_decode_batch_host(gpk_ctx* ctx, const gpk_parser* p, const gpk_batch* host_batch,
+                          const gpk_results* host_out);
+
+/* Full decoded list of a packet whose list is longer than 16 entries
+ * (gpk_record_nlayers > 16). Device batch, device result not needed; writes
+ * up to `cap` LayerType values to host memory `out_types`, returns count. */
+int gpk_decoded_list(gpk_ctx* ctx, const gpk_parser* p, const gpk_batch* batch,
+                     uint64_t index, int64_t* out_types, uint32_t cap, uint32_t* out_n);
+
+/* Same for one packet in host memory (the single-packet DecodeLayers path). */
+int gpk_decoded_list_host(gpk_ctx* ctx, const gpk_parser* p, const uint8_t* pkt, uint32_t caplen,
+                          int64_t* out_types, uint32_t cap, uint32_t* out_n);
+
+/* Pinned host memory for gpk_decode_batch_host (hipHostMalloc). */
+int gpk_host_alloc(void** out, size_t bytes);
+int gpk_host_free(void* p);
+
+/* Exact Go error text of a record's error (no trailing NUL counted).
+ * Returns the length written (truncated to cap-1 and NUL-terminated). */
+int gpk_format_error(unsigned err_code, uint32_t a0, uint32_t a1, char* buf, size_t cap);
+/* LayerType.String() (layertype.go:101-111). */
+int gpk_layer_type_name(int64_t layer_type, char* buf, size_t cap);
+
+/* Map a compact code to its LayerType id (GPK_CODE_* -> GPK_LT_*). */
+int64_t gpk_code_layer_type(unsigned code);
+
+const char* gpk_strerror(int status);
+const char* gpk_last_hip_error(void);
+int gpk_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GPK_H */

@@ -1,0 +1,123 @@
+"""ctypes binding of the CPU oracle (oracle/liboracle.so).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg. The product package gopacket_amd never imports it.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+
+RECORD_DTYPE = np.dtype([("layers", "<u8"), ("status", "<u4"), ("ip4_csum", "<u2"), ("l4_csum", "<u2")])
+LAYOUT_DTYPE = np.dtype([("start", "<u4", (8,)), ("end", "<u4", (8,))])
+
+# decoder kinds (include/gpk.h GPK_DEC_*)
+DEC = dict(ETHERNET=1, DOT1Q=2, IPV4=3, IPV6=4, IPV6_EXT=5, TCP=6, UDP=7, PAYLOAD=8, FRAGMENT=9)
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", _HERE])
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        path = os.path.join(_HERE, "liboracle.so")
+        if not os.path.exists(path):
+            build()
+        L = ctypes.CDLL(path)
+        L.oracle_sizeof_config.restype = ctypes.c_uint64
+        L.oracle_config_init.argtypes = [ctypes.c_void_p, ctypes.c_int64]
+        L.oracle_config_put.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        L.oracle_decode_batch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                          ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+        L.oracle_decoded_list.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+                                          ctypes.c_void_p, ctypes.c_uint32]
+        L.oracle_decoded_list.restype = ctypes.c_uint32
+        L.oracle_error_string.argtypes = [ctypes.c_void_p, ctypes.c_uint, ctypes.c_uint32, ctypes.c_uint32,
+                                          ctypes.c_char_p, ctypes.c_int]
+        L.oracle_compute_checksum.argtypes = [ctypes.c_char_p, ctypes.c_uint32, ctypes.c_uint32]
+        L.oracle_compute_checksum.restype = ctypes.c_uint32
+        L.oracle_fold_checksum.argtypes = [ctypes.c_uint32]
+        L.oracle_fold_checksum.restype = ctypes.c_uint16
+        L.oracle_fnv_hash.argtypes = [ctypes.c_char_p, ctypes.c_uint32]
+        L.oracle_fnv_hash.restype = ctypes.c_uint64
+        L.oracle_flow_fast_hash.argtypes = [ctypes.c_int64, ctypes.c_char_p, ctypes.c_uint32,
+                                            ctypes.c_char_p, ctypes.c_uint32]
+        L.oracle_flow_fast_hash.restype = ctypes.c_uint64
+        L.oracle_config_set.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_uint32]
+        L.oracle_config_table.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        L.oracle_config_table.restype = ctypes.c_void_p
+        _LIB = L
+    return _LIB
+
+
+class OracleParser:
+    """The oracle's view of a DecodingLayerParser configuration."""
+
+    def __init__(self, first, decoders, ignore_unsupported=False, ignore_panic=False, outputs=7,
+                 ethertype=None, ipprotocol=None, tcp_port=None, udp_port=None):
+        L = lib()
+        self._buf = ctypes.create_string_buffer(int(L.oracle_sizeof_config()))
+        self.ptr = ctypes.cast(self._buf, ctypes.c_void_p)
+        L.oracle_config_init(self.ptr, int(first))
+        for d in decoders:
+            L.oracle_config_put(self.ptr, DEC[d] if isinstance(d, str) else int(d))
+        L.oracle_config_set(self.ptr, int(bool(ignore_unsupported)), int(bool(ignore_panic)), int(outputs))
+        for which, (count, over) in enumerate(((65536, ethertype), (256, ipprotocol),
+                                              (65536, tcp_port), (65536, udp_port))):
+            if over:
+                arr = (ctypes.c_int32 * count).from_address(L.oracle_config_table(self.ptr, which))
+                for k, v in over.items():
+                    arr[int(k)] = int(v)
+
+    def decode(self, data, offsets, caplens, nthreads=1, layouts=True):
+        L = lib()
+        data = np.ascontiguousarray(data, dtype=np.uint8)
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        caplens = np.ascontiguousarray(caplens, dtype=np.uint32)
+        n = len(offsets)
+        rec = np.zeros(n, RECORD_DTYPE)
+        err = np.zeros(2 * n, np.uint32)
+        flows = np.zeros(3 * n, np.uint64)
+        lay = np.zeros(n, LAYOUT_DTYPE) if layouts else None
+        L.oracle_decode_batch(self.ptr, data.ctypes.data, offsets.ctypes.data, caplens.ctypes.data, n,
+                              rec.ctypes.data, err.ctypes.data, flows.ctypes.data,
+                              lay.ctypes.data if layouts else None, int(nthreads))
+        return dict(records=rec, err_args=err, flows=flows, layouts=lay)
+
+    def decoded_list(self, pkt):
+        L = lib()
+        pkt = bytes(pkt)
+        out = (ctypes.c_int64 * 4096)()
+        n = L.oracle_decoded_list(self.ptr, pkt, len(pkt), out, 4096)
+        return [out[i] for i in range(min(n, 4096))]
+
+    def error_string(self, code, a0=0, a1=0):
+        buf = ctypes.create_string_buffer(512)
+        lib().oracle_error_string(self.ptr, int(code), int(a0) & 0xFFFFFFFF, int(a1) & 0xFFFFFFFF, buf, 512)
+        return buf.value.decode()
+
+
+def compute_checksum(data, csum=0):
+    data = bytes(data)
+    return lib().oracle_compute_checksum(data, len(data), csum)
+
+
+def fold_checksum(csum):
+    return lib().oracle_fold_checksum(csum)
+
+
+def fnv_hash(s):
+    s = bytes(s)
+    return lib().oracle_fnv_hash(s, len(s))
+
+
+def flow_fast_hash(typ, src, dst):
+    src, dst = bytes(src), bytes(dst)
+    return lib().oracle_flow_fast_hash(typ, src, len(src), dst, len(dst))

@@ -1,0 +1,136 @@
+"""Device (HIP, through the C ABI) vs oracle parity. Bit-exact: every record
+field, error argument, flow hash and layer layout must be identical.
+
+All packets are built here; nothing reads /root/reference at run time.
+"""
+import zlib
+
+import numpy as np
+import pytest
+
+import pktutil
+from configs import CONFIGS, assert_same, device_parser, oracle_parser
+
+pytestmark = pytest.mark.gpu
+
+
+def golden_packets():
+    g = pktutil.golden()
+    pk = [bytes.fromhex(v["hex"]) for k, v in sorted(g.items()) if "hex" in v]
+    for name in ("test_ethernet.pcap", "test_dns.pcap"):
+        pk += pktutil.read_pcap(pktutil.GOLDEN + "/" + name)[1]
+    sll = bytes.fromhex(g["mptcp_bad_len_sll2"]["hex"])
+    pk.append(sll[20:])  # the IPv4 packet inside the Linux SLL2 header
+    return pk
+
+
+def run_both(ctx, cfg, packets, align=1, pad=0, layouts=True):
+    data, off, cap = pktutil.pack(packets, align=align, pad=pad)
+    dev = ctx.decode_host(device_parser(cfg), data, off, cap, layouts=layouts)
+    ref = oracle_parser(cfg).decode(data, off, cap, nthreads=8, layouts=layouts)
+    return dev, ref
+
+
+@pytest.mark.parametrize("cfg_name", sorted(CONFIGS))
+def test_golden_packets(gpu_ctx, cfg_name):
+    dev, ref = run_both(gpu_ctx, CONFIGS[cfg_name], golden_packets())
+    assert_same(dev, ref, cfg_name)
+
+
+@pytest.mark.parametrize("cfg_name", sorted(CONFIGS))
+@pytest.mark.parametrize("align", [1, 16])
+def test_fuzz(gpu_ctx, cfg_name, align):
+    packets = pktutil.fuzz_packets(zlib.crc32(cfg_name.encode()) % 1000 + align, 40000)
+    dev, ref = run_both(gpu_ctx, CONFIGS[cfg_name], packets, align=align, pad=align // 2)
+    assert_same(dev, ref, cfg_name)
+    err = dev["records"]["status"] & 0x7F
+    assert len(np.unique(err)) > 5  # the fuzzer reaches many error sites
+
+
+@pytest.mark.parametrize("synth_cfg,cfg_name", [(2, "eth_ip4_udp_payload"), (3, "eth_ip4_tcp_payload"),
+                                                (4, "statsassembly")])
+def test_synthetic(gpu_ctx, synth_cfg, cfg_name):
+    from gopacket_amd import synth
+    data, off, cap = synth.host_batch(synth_cfg, 123456789, 100000)
+    dev = gpu_ctx.decode_host(device_parser(CONFIGS[cfg_name]), data, off, cap, layouts=True)
+    ref = oracle_parser(CONFIGS[cfg_name]).decode(data, off, cap, nthreads=8)
+    assert_same(dev, ref, "synth%d" % synth_cfg)
+
+
+def test_edge_sizes(gpu_ctx):
+    """Empty packets, 1-byte packets, a jumbogram larger than 64 KiB and the
+    snaplen maximum, at odd offsets."""
+    g = pktutil.golden()
+    base = bytes.fromhex(g["simple_tcp"]["hex"])
+    jumbo = bytearray(base)
+    jumbo += bytes(np.random.default_rng(1).integers(0, 256, 70000, dtype=np.uint8))
+    # IPv4 Length 0 (TSO): length becomes uint16(len(data)) (ip4.go:189-193)
+    jumbo[16:18] = b"\x00\x00"
+    big = bytearray(base) + bytes(262144 - len(base))
+    big[16:18] = b"\x00\x00"
+    packets = [b"", b"\x00", base[:13], base[:14], base, bytes(jumbo), bytes(big), base[:60]] * 3
+    for name in sorted(CONFIGS):
+        dev, ref = run_both(gpu_ctx, CONFIGS[name], packets, align=1, pad=3)
+        assert_same(dev, ref, name)
+
+
+def test_error_text(gpu_ctx):
+    """gpk_format_error renders the same Go text as the oracle for every error the fuzzer produced."""
+    from gopacket_amd import engine
+    cfg = CONFIGS["statsassembly"]
+    dev, _ = run_both(gpu_ctx, cfg, pktutil.fuzz_packets(7, 20000))
+    op = oracle_parser(cfg)
+    st = dev["records"]["status"]
+    seen = set()
+    for i in np.nonzero(st & 0x7F)[0]:
+        code = int(st[i] & 0x7F)
+        a0, a1 = int(dev["err_args"][2 * i]), int(dev["err_args"][2 * i + 1])
+        if (code, a0, a1) in seen:
+            continue
+        seen.add((code, a0, a1))
+        assert engine.format_error(code, a0, a1) == op.error_string(code, a0, a1)
+    assert len(seen) > 10
+
+
+def test_long_decoded_lists(gpu_ctx):
+    """Lists longer than the 16 inline codes: stacked 802.1Q tags and IPv4-in-IPv4."""
+    import struct
+    cfg = CONFIGS["statsassembly"]
+    pkts = []
+    for ntags in (15, 16, 17, 40):
+        hdr = b"\x02" * 12 + struct.pack(">H", 0x8100)
+        tags = b"".join(struct.pack(">HH", 1, 0x8100) for _ in range(ntags - 1)) + struct.pack(">HH", 1, 0x0800)
+        ip = struct.pack(">BBHHHBBH4s4s", 0x45, 0, 20 + 8, 0, 0, 64, 17, 0, b"\x01" * 4, b"\x02" * 4)
+        pkts.append(hdr + tags + ip + struct.pack(">HHHH", 1234, 5678, 8, 0))
+    ip_chain = b""
+    for k in range(20):
+        ip_chain = struct.pack(">BBHHHBBH4s4s", 0x45, 0, 20 + len(ip_chain) + (0 if k else 8), 0, 0, 64,
+                               4 if k else 17, 0, b"\x01" * 4, b"\x02" * 4) + ip_chain + (b"" if k else b"\x00" * 8)
+    pkts.append(b"\x02" * 12 + b"\x08\x00" + ip_chain)
+    dev, ref = run_both(gpu_ctx, cfg, pkts)
+    assert_same(dev, ref, "long lists")
+    dp, op = device_parser(cfg), oracle_parser(cfg)
+    for p in pkts:
+        assert gpu_ctx.decoded_list_host(dp, p) == op.decoded_list(p)
+
+
+def test_device_resident_matches_host(gpu_ctx):
+    """gpk_decode_batch on torch device tensors == gpk_decode_batch_host."""
+    import torch
+    from gopacket_amd import _lib, synth
+    cfg = CONFIGS["statsassembly"]
+    p = device_parser(cfg)
+    n = 50000
+    data, off, cap = synth.device_batch(4, 5, n)
+    rec = torch.zeros(n * 16, dtype=torch.uint8, device="cuda")
+    err = torch.zeros(2 * n, dtype=torch.int32, device="cuda")
+    fl = torch.zeros(3 * n, dtype=torch.int64, device="cuda")
+    lay = torch.zeros(n * 64, dtype=torch.uint8, device="cuda")
+    gpu_ctx.decode_device(p, data, off, cap, rec, err, fl, lay, stream=torch.cuda.current_stream())
+    torch.cuda.synchronize()
+    hd, ho, hc = synth.host_batch(4, 5, n)
+    assert np.array_equal(data.cpu().numpy()[:len(hd) - 16], hd[:len(hd) - 16])
+    host = gpu_ctx.decode_host(p, hd, ho, hc, layouts=True)
+    dev = dict(records=rec.cpu().numpy().view(_lib.RECORD_DTYPE), err_args=err.cpu().numpy().view(np.uint32),
+               flows=fl.cpu().numpy().view(np.uint64), layouts=lay.cpu().numpy().view(_lib.LAYOUT_DTYPE))
+    assert_same(dev, host, "device vs host")
