@@ -69,6 +69,18 @@ class Results(ctypes.Structure):
 _lib = None
 
 
+def _share_hip_runtime():
+    """One HIP runtime per process. PyTorch-ROCm ships its own libamdhip64
+    (SONAME libamdhip64.so.7, NEEDED as "libamdhip64.so" by libtorch_hip), so
+    if libgpk.so were loaded first the process would end up with two HIP/HSA
+    runtimes and the second one finds no device. Importing torch first makes
+    libgpk's libamdhip64.so.7 resolve to torch's already-loaded copy."""
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+
+
 def lib():
     global _lib
     if _lib is not None:
@@ -76,6 +88,7 @@ def lib():
     if not os.path.exists(LIB_PATH):
         raise ImportError("gopacket_amd: %s is not built (run __graft_entry__.build() or make -C "
                           "gopacket_amd/csrc)" % LIB_PATH)
+    _share_hip_runtime()
     L = ctypes.CDLL(LIB_PATH)
     vp, i64, u32, u64, c_int = ctypes.c_void_p, ctypes.c_int64, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int
     P = ctypes.POINTER
@@ -129,6 +142,7 @@ def synth_lib():
     if _synth is None:
         if not os.path.exists(SYNTH_PATH):
             raise ImportError("gopacket_amd: %s is not built" % SYNTH_PATH)
+        _share_hip_runtime()
         S = ctypes.CDLL(SYNTH_PATH)
         S.gpk_synth_len.argtypes = [ctypes.c_int, ctypes.c_uint64]
         S.gpk_synth_len.restype = ctypes.c_uint32

@@ -1,0 +1,413 @@
+"""gopacket/layers surface for the hot path: LayerType and enum constants and
+the DecodingLayer structs Ethernet, Dot1Q, IPv4, IPv6, IPv6ExtensionSkipper,
+TCP, UDP (layers/{ethernet,dot1q,ip4,ip6,tcp,udp}.go).
+
+These structs are filled from device results: the GPU runs DecodeLayers and
+reports, per decoder instance, the byte range its DecodeFromBytes was handed
+(gpk_layout). Every field below is then a pure read of those packet bytes,
+following the field assignments of the reference decoder it names. Option
+lists are walked from bytes whose validity the device already established
+(the device reports any option error as the packet's error instead).
+"""
+import json
+import os
+import struct
+from dataclasses import dataclass, field
+from typing import List, Optional
+
+from . import _lib
+from .gopacket import (ChecksumVerificationResult, Flow, LayerType, NewFlow, EndpointIPv4, EndpointIPv6,
+                       EndpointMAC, EndpointTCPPort, EndpointUDPPort, LayerTypePayload)
+
+_REG = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "registry_gen.json")))
+
+# ---- LayerType constants (layers/layertypes.go) -----------------------------
+_by_name = {}
+for _id, _name in _REG["layer_type_names"].items():
+    _by_name.setdefault(_name, int(_id))
+
+
+def _lt(name):
+    return LayerType(_by_name[name])
+
+
+LayerTypeARP = _lt("ARP")
+LayerTypeDot1Q = _lt("Dot1Q")
+LayerTypeEthernet = _lt("Ethernet")
+LayerTypeICMPv4 = _lt("ICMPv4")
+LayerTypeIPv4 = _lt("IPv4")
+LayerTypeIPv6 = _lt("IPv6")
+LayerTypeLLC = _lt("LLC")
+LayerTypeTCP = _lt("TCP")
+LayerTypeUDP = _lt("UDP")
+LayerTypeIPv6HopByHop = _lt("IPv6HopByHop")
+LayerTypeIPv6Routing = _lt("IPv6Routing")
+LayerTypeIPv6Fragment = _lt("IPv6Fragment")
+LayerTypeIPv6Destination = _lt("IPv6Destination")
+LayerTypeDNS = _lt("DNS")
+LayerTypeTLS = _lt("TLS")
+LayerTypeModbus = _lt("Modbus")
+LayerTypeENIP = _lt("ENIP")
+
+# ---- enums (layers/enums.go) -------------------------------------------------
+EthernetTypeLLC = 0x0000
+EthernetTypeIPv4 = 0x0800
+EthernetTypeARP = 0x0806
+EthernetTypeIPv6 = 0x86DD
+EthernetTypeDot1Q = 0x8100
+EthernetTypeQinQ = 0x88A8
+IPProtocolIPv6HopByHop = 0
+IPProtocolTCP = 6
+IPProtocolUDP = 17
+IPProtocolIPv4 = 4
+IPProtocolIPv6 = 41
+IPProtocolNoNextHeader = 59
+IPv6HopByHopOptionJumbogram = 0xC2
+
+_IPPROTO_NAMES = {v: n for v, lt, n in _REG["ipprotocol"]}
+_ETHERTYPE_NAMES = {v: n for v, lt, n in _REG["ethertype"]}
+
+
+def IPProtocolString(p):
+    return _IPPROTO_NAMES.get(p, "UnknownIPProtocol")
+
+
+def EthernetTypeString(t):
+    return _ETHERTYPE_NAMES.get(t, "UnknownEthernetType")
+
+
+def _be16(b, o):
+    return (b[o] << 8) | b[o + 1]
+
+
+def _be32(b, o):
+    return struct.unpack_from(">I", b, o)[0]
+
+
+class BaseLayer:
+    Contents: bytes = b""
+    Payload: bytes = b""
+
+    def LayerContents(self):
+        return self.Contents
+
+    def LayerPayload(self):
+        return self.Payload
+
+
+# ---- layers/ethernet.go:22-63 ------------------------------------------------
+class Ethernet(BaseLayer):
+    kind = _lib.DEC_ETHERNET
+
+    def __init__(self):
+        self.SrcMAC = self.DstMAC = b""
+        self.EthernetType = 0
+        self.Length = 0
+
+    def LayerType(self):
+        return LayerTypeEthernet
+
+    def CanDecode(self):
+        return [LayerTypeEthernet]
+
+    def _hydrate(self, d):
+        self.DstMAC = d[0:6]
+        self.SrcMAC = d[6:12]
+        self.EthernetType = _be16(d, 12)
+        self.Contents, self.Payload = d[:14], d[14:]
+        self.Length = 0
+        if self.EthernetType < 0x0600:
+            self.Length = self.EthernetType
+            self.EthernetType = EthernetTypeLLC
+            if len(self.Payload) > self.Length:
+                self.Payload = self.Payload[:self.Length]
+
+    def LinkFlow(self):
+        return NewFlow(EndpointMAC, self.SrcMAC, self.DstMAC)
+
+
+# ---- layers/dot1q.go:17-41 ---------------------------------------------------
+class Dot1Q(BaseLayer):
+    kind = _lib.DEC_DOT1Q
+
+    def __init__(self):
+        self.Priority = 0
+        self.DropEligible = False
+        self.VLANIdentifier = 0
+        self.Type = 0
+
+    def LayerType(self):
+        return LayerTypeDot1Q
+
+    def CanDecode(self):
+        return [LayerTypeDot1Q]
+
+    def _hydrate(self, d):
+        self.Priority = (d[0] & 0xE0) >> 5
+        self.DropEligible = d[0] & 0x10 != 0
+        self.VLANIdentifier = _be16(d, 0) & 0x0FFF
+        self.Type = _be16(d, 2)
+        self.Contents, self.Payload = d[:4], d[4:]
+
+
+@dataclass
+class IPv4Option:
+    OptionType: int = 0
+    OptionLength: int = 0
+    OptionData: Optional[bytes] = None
+
+
+class _Checksummed:
+    _csum = None  # (error, ChecksumVerificationResult) set from the device record
+
+    def VerifyChecksum(self):
+        """The device's checksum verification of this layer (see DecodingLayerParser)."""
+        if self._csum is None:
+            raise RuntimeError("no device checksum result attached to this layer")
+        return self._csum
+
+
+# ---- layers/ip4.go:42-271 ----------------------------------------------------
+class IPv4(BaseLayer, _Checksummed):
+    kind = _lib.DEC_IPV4
+
+    def __init__(self):
+        self.Version = self.IHL = self.TOS = 0
+        self.Length = self.Id = 0
+        self.Flags = self.FragOffset = 0
+        self.TTL = self.Protocol = self.Checksum = 0
+        self.SrcIP = self.DstIP = b""
+        self.Options: List[IPv4Option] = []
+        self.Padding = None
+
+    def LayerType(self):
+        return LayerTypeIPv4
+
+    def CanDecode(self):
+        return [LayerTypeIPv4]
+
+    def _hydrate(self, d):
+        self.Length = _be16(d, 2)
+        self.IHL = d[0] & 0x0F
+        if self.Length == 0:
+            self.Length = len(d) & 0xFFFF
+        if len(d) > self.Length:
+            d = d[:self.Length]
+        hl = self.IHL * 4
+        self.Options = []
+        self.Contents, self.Payload = d[:hl], d[hl:]
+        opts = d[20:hl]
+        while len(opts) > 0:
+            t = opts[0]
+            if t == 0:
+                self.Options.append(IPv4Option(0, 1))
+                self.Padding = opts[1:]
+                break
+            if t == 1:
+                self.Options.append(IPv4Option(1, 1))
+                opts = opts[1:]
+                continue
+            ol = opts[1]
+            self.Options.append(IPv4Option(t, ol, opts[2:ol]))
+            opts = opts[ol:]
+        ff = _be16(d, 6)
+        self.Version = d[0] >> 4
+        self.TOS = d[1]
+        self.Id = _be16(d, 4)
+        self.Flags = ff >> 13
+        self.FragOffset = ff & 0x1FFF
+        self.TTL = d[8]
+        self.Protocol = d[9]
+        self.Checksum = _be16(d, 10)
+        self.SrcIP = d[12:16]
+        self.DstIP = d[16:20]
+
+    def NetworkFlow(self):
+        return NewFlow(EndpointIPv4, self.SrcIP, self.DstIP)
+
+
+@dataclass
+class IPv6HopByHopOption:
+    OptionType: int = 0
+    OptionLength: int = 0
+    ActualLength: int = 0
+    OptionData: Optional[bytes] = None
+
+
+class IPv6HopByHop(BaseLayer):
+    def __init__(self):
+        self.NextHeader = 0
+        self.HeaderLength = 0
+        self.ActualLength = 0
+        self.Options: List[IPv6HopByHopOption] = []
+
+    def LayerType(self):
+        return LayerTypeIPv6HopByHop
+
+
+# ---- layers/ip6.go:28-278 ----------------------------------------------------
+class IPv6(BaseLayer, _Checksummed):
+    kind = _lib.DEC_IPV6
+
+    def __init__(self):
+        self.Version = self.TrafficClass = self.FlowLabel = 0
+        self.Length = self.NextHeader = self.HopLimit = 0
+        self.SrcIP = self.DstIP = b""
+        self.HopByHop = None
+        self.hbh = IPv6HopByHop()
+
+    def LayerType(self):
+        return LayerTypeIPv6
+
+    def CanDecode(self):
+        return [LayerTypeIPv6]
+
+    def _hydrate(self, d):
+        self.Version = d[0] >> 4
+        self.TrafficClass = (_be16(d, 0) >> 4) & 0xFF
+        self.FlowLabel = _be32(d, 0) & 0x000FFFFF
+        self.Length = _be16(d, 4)
+        self.NextHeader = d[6]
+        self.HopLimit = d[7]
+        self.SrcIP, self.DstIP = d[8:24], d[24:40]
+        self.HopByHop = None
+        self.Contents, self.Payload = d[:40], d[40:]
+        if self.NextHeader == IPProtocolIPv6HopByHop:
+            h, p = self.hbh, self.Payload
+            h.NextHeader, h.HeaderLength = p[0], p[1]
+            h.ActualLength = p[1] * 8 + 8
+            h.Contents, h.Payload = p[:h.ActualLength], p[h.ActualLength:]
+            h.Options = []
+            off = 2
+            while off < h.ActualLength:
+                if p[off] == 0:
+                    o = IPv6HopByHopOption(0, 0, 1, None)
+                else:
+                    al = p[off + 1] + 2
+                    o = IPv6HopByHopOption(p[off], p[off + 1], al, p[off + 2:off + al])
+                h.Options.append(o)
+                off += o.ActualLength
+            self.HopByHop = h
+            jumbo = next((o for o in h.Options if o.OptionType == IPv6HopByHopOptionJumbogram), None)
+            if jumbo is not None and self.Length == 0:
+                self.Payload = self.Payload[:min(_be32(jumbo.OptionData, 0), len(self.Payload))]
+                return
+            self.Payload = self.Payload[h.ActualLength:]
+        self.Payload = self.Payload[:min(self.Length, len(self.Payload))]
+
+    def NetworkFlow(self):
+        return NewFlow(EndpointIPv6, self.SrcIP, self.DstIP)
+
+
+# ---- layers/ip6.go:434-461 ---------------------------------------------------
+class IPv6ExtensionSkipper(BaseLayer):
+    kind = _lib.DEC_IPV6_EXT
+
+    def __init__(self):
+        self.NextHeader = 0
+
+    def CanDecode(self):
+        return [LayerTypeIPv6HopByHop, LayerTypeIPv6Routing, LayerTypeIPv6Fragment, LayerTypeIPv6Destination]
+
+    def _hydrate(self, d):
+        actual = d[1] * 8 + 8
+        self.NextHeader = d[0]
+        self.Contents, self.Payload = d[:actual], d[actual:]
+
+
+TCPOptionKindEndList, TCPOptionKindNop, TCPOptionKindMSS, TCPOptionKindTimestamps = 0, 1, 2, 8
+TCPOptionKindMultipathTCP = 30
+
+
+@dataclass
+class TCPOption:
+    OptionType: int = 0
+    OptionLength: int = 0
+    OptionData: Optional[bytes] = None
+    OptionMultipath: int = 0
+
+
+# ---- layers/tcp.go:19-551 ----------------------------------------------------
+class TCP(BaseLayer, _Checksummed):
+    kind = _lib.DEC_TCP
+
+    def __init__(self):
+        self.SrcPort = self.DstPort = 0
+        self.Seq = self.Ack = 0
+        self.DataOffset = 0
+        self.FIN = self.SYN = self.RST = self.PSH = self.ACK = self.URG = self.ECE = self.CWR = self.NS = False
+        self.Window = self.Checksum = self.Urgent = 0
+        self.Options: List[TCPOption] = []
+        self.Padding = b""
+        self.Multipath = False
+        self.sPort = self.dPort = b""
+
+    def LayerType(self):
+        return LayerTypeTCP
+
+    def CanDecode(self):
+        return [LayerTypeTCP]
+
+    def _hydrate(self, d):
+        self.SrcPort, self.DstPort = _be16(d, 0), _be16(d, 2)
+        self.sPort, self.dPort = d[0:2], d[2:4]
+        self.Seq, self.Ack = _be32(d, 4), _be32(d, 8)
+        self.DataOffset = d[12] >> 4
+        f = d[13]
+        self.FIN, self.SYN, self.RST, self.PSH = bool(f & 1), bool(f & 2), bool(f & 4), bool(f & 8)
+        self.ACK, self.URG, self.ECE, self.CWR = bool(f & 0x10), bool(f & 0x20), bool(f & 0x40), bool(f & 0x80)
+        self.NS = bool(d[12] & 1)
+        self.Window, self.Checksum, self.Urgent = _be16(d, 14), _be16(d, 16), _be16(d, 18)
+        ds = self.DataOffset * 4
+        self.Contents, self.Payload = d[:ds], d[ds:]
+        self.Options, self.Padding = [], b""
+        opts = d[20:ds]
+        while len(opts) > 0:
+            t = opts[0]
+            if t == 0:
+                self.Options.append(TCPOption(0, 1))
+                self.Padding = opts[1:]
+                break
+            if t == 1:
+                o = TCPOption(1, 1)
+            elif t == TCPOptionKindMultipathTCP:
+                self.Multipath = True
+                o = TCPOption(t, opts[1], None, opts[2] >> 4)
+            else:
+                o = TCPOption(t, opts[1], opts[2:opts[1]])
+            self.Options.append(o)
+            opts = opts[o.OptionLength:]
+
+    def TransportFlow(self):
+        return NewFlow(EndpointTCPPort, self.sPort, self.dPort)
+
+
+# ---- layers/udp.go:17-56 -----------------------------------------------------
+class UDP(BaseLayer, _Checksummed):
+    kind = _lib.DEC_UDP
+
+    def __init__(self):
+        self.SrcPort = self.DstPort = self.Length = self.Checksum = 0
+        self.sPort = self.dPort = b""
+
+    def LayerType(self):
+        return LayerTypeUDP
+
+    def CanDecode(self):
+        return [LayerTypeUDP]
+
+    def _hydrate(self, d):
+        self.SrcPort, self.DstPort = _be16(d, 0), _be16(d, 2)
+        self.sPort, self.dPort = d[0:2], d[2:4]
+        self.Length, self.Checksum = _be16(d, 4), _be16(d, 6)
+        self.Contents = d[:8]
+        if self.Length >= 8:
+            self.Payload = d[8:min(self.Length, len(d))]
+        else:
+            self.Payload = d[8:]
+
+    def TransportFlow(self):
+        return NewFlow(EndpointUDPPort, self.sPort, self.dPort)
+
+
+__all__ = [n for n in dir() if not n.startswith("_")]

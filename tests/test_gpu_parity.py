@@ -44,7 +44,8 @@ def test_fuzz(gpu_ctx, cfg_name, align):
     dev, ref = run_both(gpu_ctx, CONFIGS[cfg_name], packets, align=align, pad=align // 2)
     assert_same(dev, ref, cfg_name)
     err = dev["records"]["status"] & 0x7F
-    assert len(np.unique(err)) > 5  # the fuzzer reaches many error sites
+    if cfg_name != "first_unregistered":  # that one fails every packet with UnsupportedLayerType(LLC)
+        assert len(np.unique(err)) > 5  # the fuzzer reaches many error sites
 
 
 @pytest.mark.parametrize("synth_cfg,cfg_name", [(2, "eth_ip4_udp_payload"), (3, "eth_ip4_tcp_payload"),
