@@ -1,0 +1,236 @@
+#!/usr/bin/env python3
+"""Benchmark: device-resident Eth/IPv4/TCP decode + checksum + flow hash.
+
+A step = one gpk_decode_batch over one per-GPU batch already resident in HBM
+(BASELINE.json configs[2], "C3": 64 M synthetic 1500 B Eth/IPv4/TCP packets,
+full TCP/IP checksum + flow hash). Secondary configs C2 (64 B UDP, IPv4
+checksum) and C4 (IMIX + VLAN + IPv6, all checksums and hashes) are measured
+in the same run and reported under "configs".
+
+    python bench.py [--gpus N --steps K --warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU)
+
+Multi-GPU: every rank generates and decodes its own shard (packets
+[rank*n, (rank+1)*n)); no collective on the data path ("scaling": "weak").
+Timing: barrier + synchronize on both sides of exactly K steps, max over ranks.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+INDEX_BYTES = 12       # u64 offset + u32 caplen per packet
+
+CONFIGS = {
+    "c3": dict(synth=3, decoders=("Ethernet", "IPv4", "TCP", "Payload"), outputs=7,
+               workload="C3: 64M x 1500B Eth/IPv4/TCP, IPv4+TCP checksum, link/net/transport FastHash"),
+    "c2": dict(synth=2, decoders=("Ethernet", "IPv4", "UDP", "Payload"), outputs=1,
+               workload="C2: 64M x 64B Eth/IPv4/UDP, header decode + IPv4 checksum"),
+    "c4": dict(synth=4, decoders=("Ethernet", "Dot1Q", "IPv4", "IPv6", "IPv6ExtensionSkipper", "TCP", "UDP",
+                                  "Payload"), outputs=7,
+               workload="C4: 64M IMIX 64/594/1518 7:4:1, 40% Dot1Q/QinQ, 20% IPv6, all checksums + hashes"),
+}
+
+
+def dist_init():
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    return rank, world, local
+
+
+def barrier(world):
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+
+
+def max_over_ranks(x, world):
+    import torch
+    import torch.distributed as dist
+    if world == 1:
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def run_config(name, n, steps, warmup, rank, world, ctx, check_sample=2048):
+    import torch
+    from gopacket_amd import engine, synth
+    cfg = CONFIGS[name]
+    kinds = [engine.DECODER_KINDS[d] for d in cfg["decoders"]]
+    parser = engine.ParserConfig(17, kinds, outputs=cfg["outputs"])
+    first = rank * n
+    stream = torch.cuda.current_stream()
+    data, off, cap = synth.device_batch(cfg["synth"], first, n, stream=stream)
+    rec = torch.empty(n * 16, dtype=torch.uint8, device="cuda")
+    err = torch.zeros(2 * n, dtype=torch.int32, device="cuda")
+    fl = torch.empty(3 * n, dtype=torch.int64, device="cuda") if cfg["outputs"] & 4 else None
+    payload_bytes = int(cap.sum(dtype=torch.int64).item())
+    torch.cuda.synchronize()
+
+    def step():
+        ctx.decode_device(parser, data, off, cap, rec, err, fl, stream=stream)
+
+    for _ in range(warmup):
+        step()
+    barrier(world)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record(stream)
+    for _ in range(steps):
+        step()
+    e1.record(stream)
+    barrier(world)
+    wall = time.perf_counter() - t0
+    kernel_ms = e0.elapsed_time(e1) / steps
+    wall_max = max_over_ranks(wall, world)
+
+    parity = None
+    if check_sample:
+        parity = sample_parity(name, cfg, rec, fl, err, first, n, check_sample)
+    res = dict(n=n, payload_bytes=payload_bytes, wall_s=wall_max, kernel_ms=kernel_ms,
+               algo_bytes=payload_bytes + INDEX_BYTES * n, parity=parity)
+    del data, off, cap, rec, err, fl
+    torch.cuda.empty_cache()
+    return res
+
+
+def sample_parity(name, cfg, rec, fl, err, first, n, k):
+    """Check k sampled packets of the device result against the CPU oracle."""
+    from gopacket_amd import _lib, synth
+    from oracle import oracle as O
+    rng = np.random.default_rng(first + 17)
+    idx = np.unique(np.concatenate([rng.integers(0, n, k), [0, n - 1]]))
+    pk = [synth.packet(cfg["synth"], first + int(i)) for i in idx]
+    cap = np.array([len(x) for x in pk], np.uint32)
+    off = np.concatenate([[0], np.cumsum(cap[:-1], dtype=np.uint64)]).astype(np.uint64)
+    data = np.frombuffer(b"".join(pk) + bytes(16), np.uint8)
+    dec = [{"Ethernet": "ETHERNET", "Dot1Q": "DOT1Q", "IPv4": "IPV4", "IPv6": "IPV6",
+            "IPv6ExtensionSkipper": "IPV6_EXT", "TCP": "TCP", "UDP": "UDP", "Payload": "PAYLOAD"}[d]
+           for d in cfg["decoders"]]
+    ref = O.OracleParser(17, dec, outputs=cfg["outputs"]).decode(data, off, cap, layouts=False)
+    import torch
+    ti = torch.from_numpy(idx.astype(np.int64)).cuda()
+    got = rec.view(n, 16)[ti].cpu().numpy().reshape(-1).view(_lib.RECORD_DTYPE)
+    ok = bool(np.array_equal(got, ref["records"]))
+    if fl is not None:
+        gf = torch.stack([fl[ti], fl[n + ti], fl[2 * n + ti]]).cpu().numpy().view(np.uint64).reshape(-1)
+        ok = ok and bool(np.array_equal(gf, ref["flows"]))
+    return "%s (%d sampled packets vs oracle)" % ("bit-exact" if ok else "MISMATCH", len(idx))
+
+
+def cpu_baseline(name, seconds=12.0, batch=262144):
+    """The oracle (CPU restatement, oracle/) on the host cores over a bounded
+    sample of the same synthetic workload, replayed until ~`seconds` elapse."""
+    from gopacket_amd import synth
+    from oracle import oracle as O
+    cfg = CONFIGS[name]
+    cores = min(16, len(os.sched_getaffinity(0)))
+    data, off, cap = synth.host_batch(cfg["synth"], 0, batch)
+    dec = [{"Ethernet": "ETHERNET", "Dot1Q": "DOT1Q", "IPv4": "IPV4", "IPv6": "IPV6",
+            "IPv6ExtensionSkipper": "IPV6_EXT", "TCP": "TCP", "UDP": "UDP", "Payload": "PAYLOAD"}[d]
+           for d in cfg["decoders"]]
+    p = O.OracleParser(17, dec, outputs=cfg["outputs"])
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        p.decode(data, off, cap, nthreads=cores, layouts=False)
+        reps += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    pkts = reps * batch
+    return dict(value=pkts / el / 1e6, unit="Mpkts/s", cores=cores, kind="port",
+                sample="%d x %d-packet %s batch (%.1f MB) replayed, %.1f s, oracle/gpk_oracle.c at %d threads"
+                       % (reps, batch, name.upper(), len(data) / 1e6, el, cores))
+
+
+def load_traffic(name):
+    path = os.path.join(ROOT, "profiles", "hbm_traffic.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        t = json.load(open(path)).get(name)
+        return t
+    except Exception:
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--packets", type=int, default=64 * 2**20, help="packets per GPU")
+    ap.add_argument("--configs", default="c3,c2,c4", help="first one is the headline")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-parity", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    rank, world, local = dist_init()
+    from gopacket_amd import engine
+    ctx = engine.Context(local)
+    names = args.configs.split(",")
+    results = {}
+    for name in names:
+        results[name] = run_config(name, args.packets, args.steps, args.warmup, rank, world, ctx,
+                                   check_sample=0 if args.no_parity else 2048)
+    if rank == 0:
+        head = names[0]
+        r = results[head]
+        total_pkts = r["n"] * world * args.steps
+        value = total_pkts / r["wall_s"] / 1e6
+        achieved = r["algo_bytes"] / (r["kernel_ms"] * 1e-3) / 1e9
+        out = {
+            "metric": "Mpkts/s device-resident Eth/IPv4/TCP decode+cksum+flow-hash; % HBM roofline",
+            "value": round(value, 2), "unit": "Mpkts/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(r["wall_s"] / args.steps * 1e3, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+            "data": "synthetic (deterministic splitmix64 per packet index, generated in HBM)",
+            "config": {"workload": CONFIGS[head]["workload"], "packets_per_gpu": r["n"],
+                       "payload_bytes_per_gpu": r["payload_bytes"], "parallelism": "shard%d" % world,
+                       "parser": "+".join(CONFIGS[head]["decoders"])},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": load_traffic(head),
+                         "kernel": "gpk::decode_kernel<true,false>", "kernel_ms": round(r["kernel_ms"], 4),
+                         "algo_bytes_per_launch": r["algo_bytes"]},
+            "parity": r["parity"],
+            "configs": {},
+        }
+        for name in names[1:]:
+            s = results[name]
+            ach = s["algo_bytes"] / (s["kernel_ms"] * 1e-3) / 1e9
+            out["configs"][name] = {
+                "workload": CONFIGS[name]["workload"],
+                "value": round(s["n"] * world * args.steps / s["wall_s"] / 1e6, 2), "unit": "Mpkts/s",
+                "kernel_ms": round(s["kernel_ms"], 4), "achieved_GBps": round(ach, 1),
+                "frac": round(ach / HBM_PEAK_GBS, 4), "parity": s["parity"]}
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(head, seconds=args.cpu_seconds)
+        else:
+            out["cpu_baseline"] = None
+        print(json.dumps(out))
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

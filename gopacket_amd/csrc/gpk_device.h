@@ -45,8 +45,8 @@ struct KParams {
 // from 32 lanes hit 32 different banks.
 constexpr int kBlock = 256;
 constexpr int kWaves = kBlock / 64;
-constexpr int kWinChunks = 8;
-constexpr int kSlotDw = kWinChunks * 4 + 1;  // 33
+constexpr int kWinChunks = 9;
+constexpr int kSlotDw = kWinChunks * 4 + 1;  // 37 (odd: conflict-free)
 constexpr int kLdsBytes = kBlock * kSlotDw * 4;
 
 // Dynamic LDS of the decode kernels (one declaration, aliased everywhere).
@@ -56,18 +56,31 @@ __device__ __forceinline__ uint32_t lds8(uint32_t byte_addr) {
   return ((const uint8_t*)gpk_smem)[byte_addr];
 }
 
-// Packet byte reader: LDS window first, global memory past it.
+// Packet byte readers. RdL: the bytes are in this lane's LDS window (the
+// caller checked the whole header range), one ds_read_u8 per byte and no
+// branch. Rd: LDS window first, global memory past it (deep stacks, long
+// options, HopByHop TLVs).
+struct RdL {
+  uint32_t lb;  // LDS byte address of packet byte 0
+};
 struct Rd {
   const uint8_t* g;  // packet start (global)
   uint32_t lb;       // LDS byte address of packet byte 0
   uint32_t win;      // packet bytes present in LDS
 };
 
+__device__ __forceinline__ uint32_t rd8(const RdL& r, uint32_t p) { return lds8(r.lb + p); }
 __device__ __forceinline__ uint32_t rd8(const Rd& r, uint32_t p) {
   return p < r.win ? lds8(r.lb + p) : (uint32_t)r.g[p];
 }
-__device__ __forceinline__ uint32_t rd16(const Rd& r, uint32_t p) { return (rd8(r, p) << 8) | rd8(r, p + 1); }
-__device__ __forceinline__ uint32_t rd32(const Rd& r, uint32_t p) { return (rd16(r, p) << 16) | rd16(r, p + 2); }
+template <class R>
+__device__ __forceinline__ uint32_t rd16(const R& r, uint32_t p) {
+  return (rd8(r, p) << 8) | rd8(r, p + 1);
+}
+template <class R>
+__device__ __forceinline__ uint32_t rd32(const R& r, uint32_t p) {
+  return (rd16(r, p) << 16) | rd16(r, p + 2);
+}
 
 // Outcome of one DecodeFromBytes + NextLayerType + LayerPayload, returned by
 // value (a struct passed by reference through the inlined decoders ends up in
@@ -103,7 +116,8 @@ __device__ __forceinline__ Res rok(uint32_t trunc, uint32_t off, uint32_t len, i
 }
 
 // ---- layers/ethernet.go:42-63 (+ NextLayerType :111-113) ------------------
-__device__ __forceinline__ Res dec_ethernet(const DevTables* T, const Rd& r, uint32_t off, uint32_t len) {
+template <class R>
+__device__ __forceinline__ Res dec_ethernet(const DevTables* T, const R& r, uint32_t off, uint32_t len) {
   if (len < 14) return rerr(0, GPK_ERR_ETH_TOO_SMALL);
   uint32_t et = rd16(r, off + 12);
   uint32_t plen = len - 14, trunc = 0;
@@ -116,13 +130,15 @@ __device__ __forceinline__ Res dec_ethernet(const DevTables* T, const Rd& r, uin
 }
 
 // ---- layers/dot1q.go:30-41, :49-51 -----------------------------------------
-__device__ __forceinline__ Res dec_dot1q(const DevTables* T, const Rd& r, uint32_t off, uint32_t len) {
+template <class R>
+__device__ __forceinline__ Res dec_dot1q(const DevTables* T, const R& r, uint32_t off, uint32_t len) {
   if (len < 4) return rerr(1, GPK_ERR_DOT1Q_SHORT, len);
   return rok(0, off + 4, len - 4, T->ethertype[rd16(r, off + 2)]);
 }
 
 // ---- layers/ip4.go:178-271, :277-282 ---------------------------------------
-__device__ __forceinline__ Res dec_ipv4(const DevTables* T, const Rd& r, uint32_t off, uint32_t len) {
+template <class R>
+__device__ __forceinline__ Res dec_ipv4(const DevTables* T, const R& r, uint32_t off, uint32_t len) {
   if (len < 20) return rerr(1, GPK_ERR_IP4_HDR_SHORT, len);
   uint32_t b0 = rd8(r, off);
   uint32_t length = rd16(r, off + 2);
@@ -162,7 +178,9 @@ __device__ __forceinline__ Res dec_ipv4(const DevTables* T, const Rd& r, uint32_
 // ---- IPv6: layers/ip6.go:221-278 with inline HopByHop :509-526,
 //      decodeIPv6ExtensionBase :418-432, TLV :327-346, jumbogram :54-76,
 //      NextLayerType :286-291 -------------------------------------------------
-__device__ __forceinline__ Res dec_ipv6(const DevTables* T, const Rd& r, uint32_t off, uint32_t len) {
+template <class R>
+__device__ __forceinline__ Res dec_ipv6(const DevTables* T, const R& r, const Rd& rm, uint32_t off,
+                                        uint32_t len) {
   if (len < 40) return rerr(1, GPK_ERR_IP6_HDR_SHORT, len);
   uint32_t length = rd16(r, off + 4);
   uint32_t nh = rd8(r, off + 6);
@@ -170,17 +188,17 @@ __device__ __forceinline__ Res dec_ipv6(const DevTables* T, const Rd& r, uint32_
   uint32_t next_nh = nh;
   if (nh == 0) {
     if (plen < 2) return rerr(1, GPK_ERR_IP6_EXT_SHORT, plen);
-    uint32_t hnh = rd8(r, poff);
-    uint32_t actual = rd8(r, poff + 1) * 8 + 8;
+    uint32_t hnh = rd8(rm, poff);
+    uint32_t actual = rd8(rm, poff + 1) * 8 + 8;
     if (plen < actual) return rerr(0, GPK_ERR_IP6_EXT_LEN, plen, actual);
     uint32_t have = 0, joff = 0, jlen = 0;
     for (uint32_t q = 2; q < actual;) {
       uint32_t rem = plen - q;
       if (rem < 2) return rerr(1, GPK_ERR_IP6_TLV_SHORT);
-      uint32_t t = rd8(r, poff + q);
+      uint32_t t = rd8(rm, poff + q);
       uint32_t al = 1;
       if (t != 0) {
-        al = rd8(r, poff + q + 1) + 2;
+        al = rd8(rm, poff + q + 1) + 2;
         if (rem < al) return rerr(1, GPK_ERR_IP6_TLV_TOO_SMALL);
         if (t == 0xC2 && !have) {
           have = 1;
@@ -193,7 +211,7 @@ __device__ __forceinline__ Res dec_ipv6(const DevTables* T, const Rd& r, uint32_
     next_nh = hnh;
     if (have) {
       if (jlen != 4) return rerr(0, GPK_ERR_IP6_JUMBO_TLV_LEN);
-      uint32_t l = rd32(r, joff);
+      uint32_t l = rd32(rm, joff);
       if (l <= 65535u) return rerr(0, GPK_ERR_IP6_JUMBO_SMALL);
       if (length != 0) return rerr(0, GPK_ERR_IP6_JUMBO_AND_LEN);
       uint32_t trunc = 0;
@@ -217,7 +235,8 @@ __device__ __forceinline__ Res dec_ipv6(const DevTables* T, const Rd& r, uint32_
 }
 
 // ---- IPv6ExtensionSkipper ip6.go:443-461 (base :418-432) -------------------
-__device__ __forceinline__ Res dec_ipv6_ext(const DevTables* T, const Rd& r, uint32_t off, uint32_t len) {
+template <class R>
+__device__ __forceinline__ Res dec_ipv6_ext(const DevTables* T, const R& r, uint32_t off, uint32_t len) {
   if (len < 2) return rerr(1, GPK_ERR_IP6_EXT_SHORT, len);
   uint32_t nh = rd8(r, off);
   uint32_t actual = rd8(r, off + 1) * 8 + 8;
@@ -240,7 +259,8 @@ __device__ __forceinline__ Res dec_ipv6_ext(const DevTables* T, const Rd& r, uin
     if ((uint32_t)(lo) > (uint32_t)(hi)) return rerr(0, GPK_ERR_PANIC_SLICE_B, (lo), (hi));     \
   } while (0)
 
-__device__ __forceinline__ Res mptcp_option(const Rd& r, uint32_t p, uint32_t slen, uint32_t scap) {
+template <class R>
+__device__ __forceinline__ Res mptcp_option(const R& r, uint32_t p, uint32_t slen, uint32_t scap) {
   GPK_IDX(1);
   uint32_t ol = rd8(r, p + 1);
   if (ol == 0) return rerr(0, GPK_ERR_MPTCP_LEN, ol);
@@ -348,7 +368,8 @@ __device__ __forceinline__ Res mptcp_option(const Rd& r, uint32_t p, uint32_t sl
 #undef GPK_SL
 
 // ---- layers/tcp.go:291-551, NextLayerType :591-597 --------------------------
-__device__ __forceinline__ Res dec_tcp(const DevTables* T, const Rd& r, uint32_t off, uint32_t len,
+template <class R>
+__device__ __forceinline__ Res dec_tcp(const DevTables* T, const R& r, uint32_t off, uint32_t len,
                                        uint32_t caplen) {
   if (len < 20) return rerr(1, GPK_ERR_TCP_HDR_SHORT, len);
   uint32_t ports = rd32(r, off);
@@ -382,7 +403,8 @@ __device__ __forceinline__ Res dec_tcp(const DevTables* T, const Rd& r, uint32_t
 }
 
 // ---- layers/udp.go:30-56, :114-119 -----------------------------------------
-__device__ __forceinline__ Res dec_udp(const DevTables* T, const Rd& r, uint32_t off, uint32_t len) {
+template <class R>
+__device__ __forceinline__ Res dec_udp(const DevTables* T, const R& r, uint32_t off, uint32_t len) {
   if (len < 8) return rerr(1, GPK_ERR_UDP_HDR_SHORT, len);
   uint32_t ports = rd32(r, off);
   uint32_t length = rd16(r, off + 4);
@@ -413,6 +435,22 @@ __device__ __forceinline__ uint32_t code_of(int32_t typ) {
     case GPK_LT_PAYLOAD: return GPK_CODE_PAYLOAD;
     case GPK_LT_FRAGMENT: return GPK_CODE_FRAGMENT;
     default: return GPK_CODE_NONE;
+  }
+}
+
+// Most packet bytes a decoder's DecodeFromBytes reads past its offset
+// (IPv4/TCP: 15-word headers incl. options; IPv6: the fixed header, its
+// HopByHop TLVs always go through the mixed reader).
+__device__ __forceinline__ uint32_t max_header(int kind) {
+  switch (kind) {
+    case GPK_DEC_ETHERNET: return 14;
+    case GPK_DEC_DOT1Q: return 4;
+    case GPK_DEC_IPV4: return 60;
+    case GPK_DEC_IPV6: return 40;
+    case GPK_DEC_IPV6_EXT: return 2;
+    case GPK_DEC_TCP: return 60;
+    case GPK_DEC_UDP: return 8;
+    default: return 0;
   }
 }
 
@@ -506,14 +544,18 @@ __device__ __forceinline__ Outcome run_parser(const KParams& P, const Rd& r, uin
   uint32_t off = 0, len = caplen;
   for (;;) {
     Res x;
+    // Whole header (the most bytes this decoder may read) inside the LDS
+    // window: branch-free LDS reads; otherwise the mixed reader.
+    const bool fast = off + max_header(kind) <= r.win;
+    const RdL rl{r.lb};
     switch (kind) {
-      case GPK_DEC_ETHERNET: x = dec_ethernet(T, r, off, len); break;
-      case GPK_DEC_DOT1Q: x = dec_dot1q(T, r, off, len); break;
-      case GPK_DEC_IPV4: x = dec_ipv4(T, r, off, len); break;
-      case GPK_DEC_IPV6: x = dec_ipv6(T, r, off, len); break;
-      case GPK_DEC_IPV6_EXT: x = dec_ipv6_ext(T, r, off, len); break;
-      case GPK_DEC_TCP: x = dec_tcp(T, r, off, len, caplen); break;
-      case GPK_DEC_UDP: x = dec_udp(T, r, off, len); break;
+      case GPK_DEC_ETHERNET: x = fast ? dec_ethernet(T, rl, off, len) : dec_ethernet(T, r, off, len); break;
+      case GPK_DEC_DOT1Q: x = fast ? dec_dot1q(T, rl, off, len) : dec_dot1q(T, r, off, len); break;
+      case GPK_DEC_IPV4: x = fast ? dec_ipv4(T, rl, off, len) : dec_ipv4(T, r, off, len); break;
+      case GPK_DEC_IPV6: x = fast ? dec_ipv6(T, rl, r, off, len) : dec_ipv6(T, r, r, off, len); break;
+      case GPK_DEC_IPV6_EXT: x = fast ? dec_ipv6_ext(T, rl, off, len) : dec_ipv6_ext(T, r, off, len); break;
+      case GPK_DEC_TCP: x = fast ? dec_tcp(T, rl, off, len, caplen) : dec_tcp(T, r, off, len, caplen); break;
+      case GPK_DEC_UDP: x = fast ? dec_udp(T, rl, off, len) : dec_udp(T, r, off, len); break;
       default:  // gopacket.Payload / gopacket.Fragment (base.go:61-70, :115-124)
         x = rok(0, off + len, 0, GPK_LT_ZERO);
         break;
@@ -559,12 +601,20 @@ __device__ __forceinline__ uint32_t fold(uint32_t c) {
 // FNV-1a 64 step (flows.go:60-70): h = (h ^ b) * 0x100000001b3.
 __device__ __forceinline__ uint64_t fnv_step(uint64_t h, uint32_t b) {
   h ^= b;
-  return h * 1099511628211ull;
+  uint32_t lo = (uint32_t)h, hi = (uint32_t)(h >> 32);
+  uint64_t m = (uint64_t)lo * 0x1b3u;  // v_mad_u64_u32
+  uint32_t rhi = (uint32_t)(m >> 32) + hi * 0x1b3u + (lo << 8);
+  return ((uint64_t)rhi << 32) | (uint32_t)m;
 }
-__device__ __forceinline__ uint64_t fnv_range(const Rd& r, uint32_t p, uint32_t n) {
+template <class R>
+__device__ __forceinline__ uint64_t fnv_bytes(const R& r, uint32_t p, uint32_t n) {
   uint64_t h = 14695981039346656037ull;
   for (uint32_t i = 0; i < n; i++) h = fnv_step(h, rd8(r, p + i));
   return h;
+}
+__device__ __forceinline__ uint64_t fnv_range(const Rd& r, uint32_t p, uint32_t n) {
+  if (p + n <= r.win) return fnv_bytes(RdL{r.lb}, p, n);
+  return fnv_bytes(r, p, n);
 }
 // Flow.FastHash flows.go:167-174
 __device__ __forceinline__ uint64_t flow_hash(uint64_t hs, uint64_t hd, uint32_t typ) {

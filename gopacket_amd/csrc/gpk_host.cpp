@@ -11,6 +11,7 @@
 
 #include <cstdio>
 #include <cstring>
+#include <atomic>
 #include <mutex>
 #include <new>
 #include <string>
@@ -44,7 +45,7 @@ struct gpk_parser {
   int ignore_panic = 0;
   int ignore_unsupported = 0;
   uint32_t outputs = GPK_OUT_ALL;
-  uint64_t version = 1;  // bumped on every change; ctx re-uploads tables
+  uint64_t version = 0;  // process-unique id of the current table contents (see bump())
   gpk::DevTables tab;
 };
 
@@ -59,6 +60,11 @@ struct gpk_ctx {
   hipStream_t stream = nullptr;
   std::mutex mu;
 };
+
+// Every table change takes a new process-wide id, so a context never mistakes
+// a new parser that reuses a freed parser's address for the one it uploaded.
+static std::atomic<uint64_t> g_table_ids{1};
+static void bump(gpk_parser* p) { p->version = g_table_ids.fetch_add(1); }
 
 static void default_tables(gpk::DevTables& t) {
   memset(&t, 0, sizeof(t));
@@ -96,6 +102,7 @@ int gpk_parser_create(gpk_parser** out, int64_t first) {
   if (!p) return GPK_ENOMEM;
   p->first = first;
   default_tables(p->tab);
+  bump(p);
   *out = p;
   return GPK_OK;
 }
@@ -128,7 +135,7 @@ int gpk_parser_add_decoder(gpk_parser* p, int kind) {
     case GPK_DEC_FRAGMENT: put(p, GPK_LT_FRAGMENT, kind); break;
     default: return GPK_EUNSUPP;
   }
-  p->version++;
+  bump(p);
   return GPK_OK;
 }
 
@@ -153,25 +160,25 @@ int gpk_parser_decoder_for(const gpk_parser* p, int64_t lt) {
 int gpk_parser_set_ethertype(gpk_parser* p, uint32_t v, int32_t lt) {
   if (!p || v > 0xffff) return GPK_EINVAL;
   p->tab.ethertype[v] = lt;
-  p->version++;
+  bump(p);
   return GPK_OK;
 }
 int gpk_parser_set_ipprotocol(gpk_parser* p, uint32_t v, int32_t lt) {
   if (!p || v > 0xff) return GPK_EINVAL;
   p->tab.ipprotocol[v] = lt;
-  p->version++;
+  bump(p);
   return GPK_OK;
 }
 int gpk_parser_set_tcp_port(gpk_parser* p, uint32_t v, int32_t lt) {
   if (!p || v > 0xffff) return GPK_EINVAL;
   p->tab.tcp_port[v] = lt;
-  p->version++;
+  bump(p);
   return GPK_OK;
 }
 int gpk_parser_set_udp_port(gpk_parser* p, uint32_t v, int32_t lt) {
   if (!p || v > 0xffff) return GPK_EINVAL;
   p->tab.udp_port[v] = lt;
-  p->version++;
+  bump(p);
   return GPK_OK;
 }
 
@@ -208,7 +215,7 @@ int gpk_ctx_destroy(gpk_ctx* c) {
 }
 
 static int upload(gpk_ctx* c, const gpk_parser* p, hipStream_t s) {
-  if (c->uploaded == p && c->uploaded_version == p->version) return GPK_OK;
+  if (c->uploaded_version == p->version) return GPK_OK;
   HIPCHK(hipMemcpyAsync(c->dtab, &p->tab, sizeof(gpk::DevTables), hipMemcpyHostToDevice, s));
   HIPCHK(hipStreamSynchronize(s));  // p->tab may change after we return
   c->uploaded = p;

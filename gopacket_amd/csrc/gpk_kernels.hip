@@ -61,10 +61,11 @@ __device__ __forceinline__ uint32_t sum_words(const Rd& r, uint32_t p, uint32_t 
 }
 
 // 16 bytes of a 16-aligned chunk at absolute address A, restricted to
-// [s, e), each byte weighted <<8 when (pos - s) is even.
-__device__ __forceinline__ uint32_t chunk_sum(uint4 v, uint64_t A, uint64_t s, uint64_t e) {
-  uint32_t lo = s > A ? (uint32_t)(s - A) : 0u;          // 0..15
-  uint32_t hi = e < A + 16 ? (uint32_t)(e - A) : 16u;    // 1..16
+// [s, e); a byte at address x counts <<8 when x has parity `par` (the parity
+// of the segment's first byte: BE16 words start there).
+__device__ __forceinline__ uint32_t chunk_sum(uint4 v, uint64_t A, uint64_t s, uint64_t e, uint32_t par) {
+  uint32_t lo = s > A ? (uint32_t)(s - A) : 0u;        // 0..15
+  uint32_t hi = e < A + 16 ? (uint32_t)(e - A) : 16u;  // 1..16
   uint32_t w[4] = {v.x, v.y, v.z, v.w};
   uint32_t E = 0, O = 0;
 #pragma unroll
@@ -79,16 +80,26 @@ __device__ __forceinline__ uint32_t chunk_sum(uint4 v, uint64_t A, uint64_t s, u
   }
   E = (E & 0xffff) + (E >> 16);
   O = (O & 0xffff) + (O >> 16);
-  return (s & 1) ? (O << 8) + E : (E << 8) + O;
+  return par ? (O << 8) + E : (E << 8) + O;
 }
 
-__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, uint32_t lane) {
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    uint32_t o = __shfl_up(v, d, 64);
-    if (lane >= (uint32_t)d) v += o;
-  }
-  return v;
+// v_readlane_b32 returns int: widen through uint32_t, never through int
+// (sign extension of an address's low word above 2 GiB corrupts it).
+__device__ __forceinline__ uint32_t readlane32(uint32_t v, uint32_t lane) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, lane);
+}
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, uint32_t lane) {
+  return ((uint64_t)readlane32((uint32_t)(v >> 32), lane) << 32) | (uint64_t)readlane32((uint32_t)v, lane);
+}
+
+// Sum over the 64 lanes (all active): rotations inside each 16-lane row
+// (DPP row_ror 8,4,2,1), then the four row totals via readlane.
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xf, 0xf, false);
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x124, 0xf, 0xf, false);
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x122, 0xf, 0xf, false);
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x121, 0xf, 0xf, false);
+  return readlane32(v, 0) + readlane32(v, 16) + readlane32(v, 32) + readlane32(v, 48);
 }
 
 template <bool kL4, bool kLayout>
@@ -138,10 +149,11 @@ __global__ __launch_bounds__(kBlock) void decode_kernel(KParams P) {
   uint32_t ip4c = 0, l4c = 0;
   uint64_t lflow = 0, nflow = 0, tflow = 0;
 
-  // Job for the L4 checksum: bytes [jstart, jstart+jlen) of data.
-  uint64_t jstart = 0;
-  uint32_t jlen = 0, jinit = 0, jexist = 0;
-  bool jdone = true;
+  // L4 checksum: bytes of the segment inside the LDS window are summed here;
+  // the rest, [ja, je) of data, is a job for the wave-cooperative phase B.
+  uint64_t ja = 0, je = 0;
+  uint32_t jsum = 0, jexist = 0, jpar = 0;
+  bool job = false;
 
   if (active) {
     if ((P.outputs & GPK_OUT_IP4_CSUM) && clean(q, GPK_DEC_IPV4)) {  // ip4.go:323-332
@@ -161,14 +173,17 @@ __global__ __launch_bounds__(kBlock) void decode_kernel(KParams P) {
       init += (tk == GPK_DEC_TCP ? 6u : 17u) + (blen & 0xffff) + (blen >> 16);
       jexist = rd16(r, t0 + (tk == GPK_DEC_TCP ? 16 : 6));
       st |= GPK_ST_L4_CSUM | (tk == GPK_DEC_UDP ? GPK_ST_L4_UDP : 0u);
-      if (t0 + blen <= r.win) {
-        uint32_t c = init + sum_words_lds(r.lb + t0, blen);
-        l4c = fold(c - jexist);
-      } else {
-        jdone = false;
-        jstart = off + t0;
-        jlen = blen;
-        jinit = init;
+      uint32_t tend = t0 + blen;
+      uint32_t in_end = tend < win ? tend : win;
+      uint32_t part = t0 < in_end ? sum_words_lds(r.lb + t0, in_end - t0) : 0u;
+      if (tend <= win) {
+        l4c = fold(init + part - jexist);
+      } else if (kL4) {
+        job = true;
+        ja = off + (t0 > win ? t0 : win);
+        je = off + tend;
+        jpar = (uint32_t)((off + t0) & 1);
+        jsum = init + part;
       }
     }
     if (P.outputs & GPK_OUT_FLOWS) {
@@ -195,71 +210,68 @@ __global__ __launch_bounds__(kBlock) void decode_kernel(KParams P) {
     }
   }
 
-  // ---- Phase B: wave-cooperative L4 checksum of segments past the window ---
+  // ---- Phase B: L4 segments past the window, one packet per wave pass ------
+  // The wave takes up to four pending packets at a time; every lane loads
+  // 16-byte chunks of each (consecutive lanes -> consecutive chunks: whole
+  // cache lines per wave instruction), two 1 KiB rounds in flight per packet,
+  // then each packet's partial sums are reduced across the wave (DPP row
+  // rotations + four readlanes) into the owning lane. No LDS traffic.
   if (kL4) {
-    // Per-wave scratch overlays this wave's LDS slots (no longer read).
-    uint32_t* W = gpk_smem + (tid & ~63u) * kSlotDw;
-    uint64_t* Jst = reinterpret_cast<uint64_t*>(W);  // [64] (slot base is 8-aligned: 64*33*4 per wave)
-    uint64_t* Jen = Jst + 64;                           // [64]
-    uint32_t* Base = W + 256;                           // [65]
-    uint32_t* Acc = W + 256 + 72;                       // [64]
-    uint32_t nch = 0;
-    if (!jdone) nch = (uint32_t)(((jstart + jlen + 15) >> 4) - (jstart >> 4));
-    uint32_t incl = wave_incl_scan(nch, lane);
-    uint32_t total = __shfl(incl, 63, 64);
-    if (total) {
-      __builtin_amdgcn_wave_barrier();
-      Jst[lane] = jstart;
-      Jen[lane] = jstart + jlen;
-      Base[lane] = incl - nch;
-      if (lane == 63) Base[64] = total;
-      Acc[lane] = 0;
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      constexpr int U = 4;
-      for (uint32_t t = 0; t < total; t += 64 * U) {
-        uint4 v[U];
-        uint32_t key[U];
-        uint64_t A[U];
+    uint32_t extra = 0;
+    uint64_t pend = __ballot(job);
+    while (pend) {
+      constexpr int G = 4;
+      uint32_t jl[G];
+      uint64_t s0[G], e0[G], b0[G];
+      uint32_t pr[G];
 #pragma unroll
-        for (int u = 0; u < U; u++) {
-          uint32_t c = t + u * 64 + lane;
-          key[u] = 64;
-          if (c < total) {
-            uint32_t j = 0;
-#pragma unroll
-            for (uint32_t stp = 32; stp; stp >>= 1)
-              if (Base[j + stp] <= c) j += stp;
-            key[u] = j;
-            A[u] = ((Jst[j] >> 4) + (c - Base[j])) << 4;
-            v[u] = ld16(P.data + A[u]);
-          }
-        }
-#pragma unroll
-        for (int u = 0; u < U; u++) {
-          uint32_t j = key[u];
-          uint32_t val = j < 64 ? chunk_sum(v[u], A[u], Jst[j], Jen[j]) : 0u;
-          // segmented inclusive scan keyed by packet (keys are non-decreasing)
-#pragma unroll
-          for (int d = 1; d < 64; d <<= 1) {
-            uint32_t vo = __shfl_up(val, d, 64);
-            uint32_t ko = __shfl_up(j, d, 64);
-            if (lane >= (uint32_t)d && ko == j) val += vo;
-          }
-          uint32_t kn = __shfl_down(j, 1, 64);
-          bool last = (lane == 63) || kn != j;
-          if (last && j < 64) Acc[j] += val;
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-          __builtin_amdgcn_wave_barrier();
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      for (int g = 0; g < G; g++) {
+        jl[g] = 64;
+        s0[g] = e0[g] = b0[g] = 0;
+        pr[g] = 0;
+        if (pend) {
+          uint32_t j = (uint32_t)__builtin_ctzll(pend);
+          pend &= pend - 1;
+          jl[g] = j;
+          s0[g] = readlane64(ja, j);
+          e0[g] = readlane64(je, j);
+          pr[g] = readlane32(jpar, j);
+          b0[g] = s0[g] & ~15ull;
         }
       }
-      if (!jdone) {
-        uint32_t c = jinit + Acc[lane];
-        l4c = fold(c - jexist);
+      uint32_t acc[G];
+#pragma unroll
+      for (int g = 0; g < G; g++) acc[g] = 0;
+      for (uint64_t rr = 0;; rr += 2048) {
+        uint4 v[G][2];
+#pragma unroll
+        for (int g = 0; g < G; g++)
+#pragma unroll
+          for (int h = 0; h < 2; h++) {
+            uint64_t A = b0[g] + rr + h * 1024 + lane * 16;
+            if (A < e0[g]) v[g][h] = ld16(P.data + A);
+          }
+        bool more = false;
+#pragma unroll
+        for (int g = 0; g < G; g++) {
+#pragma unroll
+          for (int h = 0; h < 2; h++) {
+            uint64_t A = b0[g] + rr + h * 1024 + lane * 16;
+            if (A < e0[g]) acc[g] += chunk_sum(v[g][h], A, s0[g], e0[g], pr[g]);
+          }
+          more |= b0[g] + rr + 2048 < e0[g];
+        }
+        if (!more) break;
+      }
+#pragma unroll
+      for (int g = 0; g < G; g++) {
+        if (jl[g] < 64) {
+          uint32_t t = wave_sum(acc[g]);
+          if (lane == jl[g]) extra += t;
+        }
       }
     }
+    if (job) l4c = fold(jsum + extra - jexist);
   }
   if (active && (st & GPK_ST_L4_CSUM)) {
     bool udp = (st & GPK_ST_L4_UDP) != 0;

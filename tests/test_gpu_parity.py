@@ -135,3 +135,68 @@ def test_device_resident_matches_host(gpu_ctx):
     dev = dict(records=rec.cpu().numpy().view(_lib.RECORD_DTYPE), err_args=err.cpu().numpy().view(np.uint32),
                flows=fl.cpu().numpy().view(np.uint64), layouts=lay.cpu().numpy().view(_lib.LAYOUT_DTYPE))
     assert_same(dev, host, "device vs host")
+
+
+@pytest.mark.parametrize("outputs", [0, 1, 2, 4, 3, 5, 6, 7])
+@pytest.mark.parametrize("synth_cfg,cfg_name", [(2, "eth_ip4_udp_payload"), (4, "statsassembly")])
+def test_output_selection(gpu_ctx, outputs, synth_cfg, cfg_name):
+    """Every GPK_OUT_* subset (each selects a different kernel specialisation)."""
+    from gopacket_amd import synth
+    cfg = dict(CONFIGS[cfg_name], outputs=outputs)
+    data, off, cap = synth.host_batch(synth_cfg, 1000, 20000)
+    for layouts in (False, True):
+        dev = gpu_ctx.decode_host(device_parser(cfg), data, off, cap, layouts=layouts)
+        ref = oracle_parser(cfg).decode(data, off, cap, nthreads=8, layouts=layouts)
+        if not outputs & 4:
+            dev["flows"][:] = 0
+        assert_same(dev, ref, "outputs=%d layouts=%s" % (outputs, layouts))
+
+
+def test_new_parser_after_free_uploads_its_tables(gpu_ctx):
+    """A parser created after another was freed (possibly at the same address,
+    with the same number of changes) must not reuse the freed one's tables."""
+    import gc
+    from gopacket_amd import synth
+    data, off, cap = synth.host_batch(2, 0, 5000)
+    a = device_parser(CONFIGS["eth_ip4_tcp_payload"])
+    gpu_ctx.decode_host(a, data, off, cap)
+    del a
+    gc.collect()
+    for _ in range(4):
+        b = device_parser(CONFIGS["eth_ip4_udp_payload"])
+        dev = gpu_ctx.decode_host(b, data, off, cap)
+        ref = oracle_parser(CONFIGS["eth_ip4_udp_payload"]).decode(data, off, cap, layouts=False)
+        assert_same(dev, ref, "fresh parser")
+        del b
+        gc.collect()
+
+
+@pytest.mark.parametrize("base", [(1 << 31) - 700, (1 << 32) + 3, (5 << 30) + 8])
+def test_offsets_beyond_2_and_4_GiB(gpu_ctx, base):
+    """Packets placed past 2 GiB / 4 GiB in a device buffer (64-bit offsets end to end)."""
+    import torch
+    from gopacket_amd import _lib, synth
+    cfg = CONFIGS["statsassembly"]
+    hd, ho, hc = synth.host_batch(4, 77, 20000)
+    hd3, ho3, hc3 = synth.host_batch(3, 77, 4000)
+    data = torch.zeros(base + len(hd) + len(hd3) + 4096, dtype=torch.uint8, device="cuda")
+    data[base:base + len(hd)] = torch.from_numpy(hd).cuda()
+    b3 = base + len(hd)
+    data[b3:b3 + len(hd3)] = torch.from_numpy(hd3).cuda()
+    off = np.concatenate([ho + base, ho3 + b3]).astype(np.int64)
+    cap = np.concatenate([hc, hc3]).astype(np.int32)
+    n = len(off)
+    rec = torch.zeros(n * 16, dtype=torch.uint8, device="cuda")
+    err = torch.zeros(2 * n, dtype=torch.int32, device="cuda")
+    fl = torch.zeros(3 * n, dtype=torch.int64, device="cuda")
+    gpu_ctx.decode_device(device_parser(cfg), data, torch.from_numpy(off).cuda(), torch.from_numpy(cap).cuda(),
+                          rec, err, fl, stream=torch.cuda.current_stream())
+    torch.cuda.synchronize()
+    pk = [bytes(hd[o:o + c]) for o, c in zip(ho, hc)] + [bytes(hd3[o:o + c]) for o, c in zip(ho3, hc3)]
+    rd, ro, rc = pktutil.pack(pk)
+    ref = oracle_parser(cfg).decode(rd, ro, rc, layouts=False)
+    dev = dict(records=rec.cpu().numpy().view(_lib.RECORD_DTYPE), err_args=err.cpu().numpy().view(np.uint32),
+               flows=fl.cpu().numpy().view(np.uint64), layouts=None)
+    assert_same(dev, ref, "base %d" % base)
+    del data
+    torch.cuda.empty_cache()
