@@ -33,21 +33,35 @@ __device__ __forceinline__ uint4 ld16(const uint8_t* p) {
   return make_uint4(x.x, x.y, x.z, x.w);
 }
 
+// Byte sums with v_dot4_u32_u8: bytes 0,2 (even addresses) and 1,3 (odd).
+__device__ __forceinline__ uint32_t dot_even(uint32_t w, uint32_t acc) {
+  return __builtin_amdgcn_udot4(w, 0x00010001u, acc, false);
+}
+__device__ __forceinline__ uint32_t dot_odd(uint32_t w, uint32_t acc) {
+  return __builtin_amdgcn_udot4(w, 0x01000100u, acc, false);
+}
+
 // Sum of big-endian 16-bit words over LDS bytes [q, q+n) (ComputeChecksum
-// with csum = 0; an odd tail byte counts <<8). n <= window size.
+// with csum = 0, checksum.go:35-50; an odd tail byte counts <<8). Only the
+// first and last dword are masked; interior dwords are two dot4s each.
 __device__ __forceinline__ uint32_t sum_words_lds(uint32_t q, uint32_t n) {
-  uint32_t e = q + n;
-  uint32_t E = 0, O = 0;
-  for (uint32_t a = q & ~3u; a < e; a += 4) {
-    uint32_t w = gpk_smem[a >> 2];
-    uint32_t lo = q > a ? q - a : 0u;
-    uint32_t hi = e - a < 4u ? e - a : 4u;
-    w &= (0xffffffffu >> (8 * (4 - hi))) & (0xffffffffu << (8 * lo));
-    E += w & 0x00ff00ffu;
-    O += (w >> 8) & 0x00ff00ffu;
+  if (n == 0) return 0;
+  const uint32_t last = q + n - 1;
+  const uint32_t a0 = q & ~3u, a1 = last & ~3u;
+  const uint32_t mhi = 0xffffffffu >> (8 * (3 - (last & 3)));
+  uint32_t w = gpk_smem[a0 >> 2] & (0xffffffffu << (8 * (q & 3)));
+  if (a0 == a1) w &= mhi;
+  uint32_t E = dot_even(w, 0), O = dot_odd(w, 0);
+  for (uint32_t a = a0 + 4; a < a1; a += 4) {
+    w = gpk_smem[a >> 2];
+    E = dot_even(w, E);
+    O = dot_odd(w, O);
   }
-  E = (E & 0xffff) + (E >> 16);
-  O = (O & 0xffff) + (O >> 16);
+  if (a1 != a0) {
+    w = gpk_smem[a1 >> 2] & mhi;
+    E = dot_even(w, E);
+    O = dot_odd(w, O);
+  }
   return (q & 1) ? (O << 8) + E : (E << 8) + O;
 }
 
@@ -62,7 +76,8 @@ __device__ __forceinline__ uint32_t sum_words(const Rd& r, uint32_t p, uint32_t 
 
 // 16 bytes of a 16-aligned chunk at absolute address A, restricted to
 // [s, e); a byte at address x counts <<8 when x has parity `par` (the parity
-// of the segment's first byte: BE16 words start there).
+// of the segment's first byte: BE16 words start there). Used for the at most
+// two partial chunks of a segment; full chunks go through chunk_eo.
 __device__ __forceinline__ uint32_t chunk_sum(uint4 v, uint64_t A, uint64_t s, uint64_t e, uint32_t par) {
   uint32_t lo = s > A ? (uint32_t)(s - A) : 0u;        // 0..15
   uint32_t hi = e < A + 16 ? (uint32_t)(e - A) : 16u;  // 1..16
@@ -74,13 +89,22 @@ __device__ __forceinline__ uint32_t chunk_sum(uint4 v, uint64_t A, uint64_t s, u
     l = l < 0 ? 0 : (l > 4 ? 4 : l);
     h = h < 0 ? 0 : (h > 4 ? 4 : h);
     uint32_t m = h > l ? ((0xffffffffu >> (8 * (4 - (h - l)))) << (8 * l)) : 0u;
-    uint32_t x = w[d] & m;
-    E += x & 0x00ff00ffu;
-    O += (x >> 8) & 0x00ff00ffu;
+    E = dot_even(w[d] & m, E);
+    O = dot_odd(w[d] & m, O);
   }
-  E = (E & 0xffff) + (E >> 16);
-  O = (O & 0xffff) + (O >> 16);
   return par ? (O << 8) + E : (E << 8) + O;
+}
+
+// Even/odd byte sums of a full chunk.
+__device__ __forceinline__ void chunk_eo(uint4 v, uint32_t& E, uint32_t& O) {
+  E = dot_even(v.x, E);
+  O = dot_odd(v.x, O);
+  E = dot_even(v.y, E);
+  O = dot_odd(v.y, O);
+  E = dot_even(v.z, E);
+  O = dot_odd(v.z, O);
+  E = dot_even(v.w, E);
+  O = dot_odd(v.w, O);
 }
 
 // v_readlane_b32 returns int: widen through uint32_t, never through int
@@ -179,11 +203,24 @@ __global__ __launch_bounds__(kBlock) void decode_kernel(KParams P) {
       if (tend <= win) {
         l4c = fold(init + part - jexist);
       } else if (kL4) {
-        job = true;
-        ja = off + (t0 > win ? t0 : win);
-        je = off + tend;
-        jpar = (uint32_t)((off + t0) & 1);
-        jsum = init + part;
+        // Remainder [ra, re) past the window: its partial first / last
+        // 16-byte chunks are summed here, the full chunks in phase B.
+        const uint64_t ra = off + (t0 > win ? t0 : win), re = off + tend;
+        const uint32_t par = (uint32_t)((off + t0) & 1);
+        const uint64_t fa = (ra + 15) & ~15ull, fe = re & ~15ull;
+        uint32_t edge = 0;
+        if (fa > fe) {  // remainder inside a single chunk
+          edge = chunk_sum(ld16(P.data + (ra & ~15ull)), ra & ~15ull, ra, re, par);
+        } else {
+          if (ra != fa) edge += chunk_sum(ld16(P.data + (ra & ~15ull)), ra & ~15ull, ra, re, par);
+          if (re != fe) edge += chunk_sum(ld16(P.data + fe), fe, ra, re, par);
+        }
+        jsum = init + part + edge;
+        job = fa < fe;
+        ja = fa;
+        je = fe;
+        jpar = par;
+        if (!job) l4c = fold(jsum - jexist);
       }
     }
     if (P.outputs & GPK_OUT_FLOWS) {
@@ -227,7 +264,7 @@ __global__ __launch_bounds__(kBlock) void decode_kernel(KParams P) {
 #pragma unroll
       for (int g = 0; g < G; g++) {
         jl[g] = 64;
-        s0[g] = e0[g] = b0[g] = 0;
+        s0[g] = e0[g] = b0[g] = 0;  // empty slot: every load reads data[0..16), discarded
         pr[g] = 0;
         if (pend) {
           uint32_t j = (uint32_t)__builtin_ctzll(pend);
@@ -236,28 +273,33 @@ __global__ __launch_bounds__(kBlock) void decode_kernel(KParams P) {
           s0[g] = readlane64(ja, j);
           e0[g] = readlane64(je, j);
           pr[g] = readlane32(jpar, j);
-          b0[g] = s0[g] & ~15ull;
+          b0[g] = s0[g];
         }
       }
-      uint32_t acc[G];
+      uint32_t E[G], O[G];
 #pragma unroll
-      for (int g = 0; g < G; g++) acc[g] = 0;
+      for (int g = 0; g < G; g++) E[g] = O[g] = 0;
       for (uint64_t rr = 0;; rr += 2048) {
         uint4 v[G][2];
+        bool ok[G][2];
 #pragma unroll
         for (int g = 0; g < G; g++)
 #pragma unroll
           for (int h = 0; h < 2; h++) {
+            // every lane loads (a lane past the end re-reads the packet's
+            // first chunk and discards it): no exec-mask branches
             uint64_t A = b0[g] + rr + h * 1024 + lane * 16;
-            if (A < e0[g]) v[g][h] = ld16(P.data + A);
+            ok[g][h] = A < e0[g];
+            v[g][h] = ld16(P.data + (ok[g][h] ? A : b0[g]));
           }
         bool more = false;
 #pragma unroll
         for (int g = 0; g < G; g++) {
 #pragma unroll
           for (int h = 0; h < 2; h++) {
-            uint64_t A = b0[g] + rr + h * 1024 + lane * 16;
-            if (A < e0[g]) acc[g] += chunk_sum(v[g][h], A, s0[g], e0[g], pr[g]);
+            uint4 x = v[g][h];
+            if (!ok[g][h]) x = make_uint4(0, 0, 0, 0);
+            chunk_eo(x, E[g], O[g]);
           }
           more |= b0[g] + rr + 2048 < e0[g];
         }
@@ -266,7 +308,7 @@ __global__ __launch_bounds__(kBlock) void decode_kernel(KParams P) {
 #pragma unroll
       for (int g = 0; g < G; g++) {
         if (jl[g] < 64) {
-          uint32_t t = wave_sum(acc[g]);
+          uint32_t t = wave_sum(pr[g] ? (O[g] << 8) + E[g] : (E[g] << 8) + O[g]);
           if (lane == jl[g]) extra += t;
         }
       }
