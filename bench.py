@@ -59,23 +59,13 @@ def barrier(world):
     torch.cuda.synchronize()
 
 
-def max_over_ranks(x, world):
-    import torch
-    import torch.distributed as dist
-    if world == 1:
-        return x
-    t = torch.tensor([x], dtype=torch.float64, device="cuda")
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return float(t.item())
-
-
 def run_config(name, n, steps, warmup, rank, world, ctx, check_sample=2048):
     import torch
-    from gopacket_amd import engine, synth
+    from gopacket_amd import engine, shard, synth
     cfg = CONFIGS[name]
     kinds = [engine.DECODER_KINDS[d] for d in cfg["decoders"]]
     parser = engine.ParserConfig(17, kinds, outputs=cfg["outputs"])
-    first = rank * n
+    first, n = shard.weak_range(rank, n)
     stream = torch.cuda.current_stream()
     data, off, cap = synth.device_batch(cfg["synth"], first, n, stream=stream)
     rec = torch.empty(n * 16, dtype=torch.uint8, device="cuda")
@@ -99,7 +89,7 @@ def run_config(name, n, steps, warmup, rank, world, ctx, check_sample=2048):
     barrier(world)
     wall = time.perf_counter() - t0
     kernel_ms = e0.elapsed_time(e1) / steps
-    wall_max = max_over_ranks(wall, world)
+    wall_max = shard.max_over_ranks(wall, world, device="cuda")
 
     parity = None
     if check_sample:

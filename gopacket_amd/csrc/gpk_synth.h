@@ -119,7 +119,7 @@ GPK_HD void describe(int cfg, uint64_t i, Desc& d) {
     d.hbh = d.v6 && ((r1 >> 16) % 100) == 0;
     d.udp = ((r1 >> 24) % 10) >= 7;
     uint32_t l3room = d.len - 14 - 4 * d.ntags;
-    if (d.v6 && l3room < 40 + 8 * d.hbh + 20) d.v6 = d.hbh = 0;  // IPv6 + L4 must fit
+    if (d.v6 && l3room < 40 + 8 * d.hbh + 8) d.v6 = d.hbh = 0;  // IPv6 + at least UDP must fit
     uint32_t l4room = l3room - (d.v6 ? 40 + 8 * d.hbh : 20);
     if (!d.udp && l4room < 20) d.udp = 1;
     uint32_t c = (uint32_t)(r2 % 1024);

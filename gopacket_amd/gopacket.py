@@ -1,0 +1,418 @@
+"""The gopacket root-package surface of the hot path, over the device engine.
+
+Mirrors (reference file:line):
+  LayerType / LayerTypeZero.. (layertype.go:20-111, decode.go:106-117)
+  Endpoint, Flow, NewFlow, FastHash (flows.go:27-224)
+  ChecksumVerificationResult (checksum.go:14-21)
+  Payload, Fragment DecodingLayers (base.go:40-124)
+  DecodingLayerParser, NewDecodingLayerParser, DecodeLayers, AddDecodingLayer,
+  UnsupportedLayerType, DecodingLayerParserOptions (parser.go:182-351)
+
+Decoding always runs on the GPU (through include/gpk.h): DecodeLayers sends
+one packet, DecodeBatch a whole PacketBatch; the per-packet results fill the
+registered layer structs exactly as the reference's DecodeLayers would.
+"""
+import json
+import os
+import struct
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _lib
+
+_REG = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "registry_gen.json")))
+_LT_NAMES = {int(k): v for k, v in _REG["layer_type_names"].items()}
+
+
+class LayerType(int):
+    """gopacket.LayerType (layertype.go:20); String() per layertype.go:101-111."""
+
+    def String(self):
+        return _LT_NAMES.get(int(self), str(int(self)))
+
+    __str__ = String
+
+    def __repr__(self):
+        return "LayerType(%s)" % self.String()
+
+
+LayerTypeZero = LayerType(0)
+LayerTypeDecodeFailure = LayerType(1)
+LayerTypePayload = LayerType(2)
+LayerTypeFragment = LayerType(3)
+
+# ---- errors ----------------------------------------------------------------
+
+
+class GoError:
+    """An `error` value returned by DecodeLayers (compare with Error())."""
+
+    def __init__(self, msg):
+        self.msg = msg
+
+    def Error(self):
+        return self.msg
+
+    __str__ = Error
+
+    def __repr__(self):
+        return "GoError(%r)" % self.msg
+
+    def __eq__(self, other):
+        return isinstance(other, GoError) and other.Error() == self.Error()
+
+
+class UnsupportedLayerType(GoError):
+    """parser.go:319-327"""
+
+    def __init__(self, typ):
+        self.typ = LayerType(typ)
+        super().__init__("No decoder for layer type %s" % self.typ.String())
+
+
+class GoPanic(RuntimeError):
+    """A decoder panic with IgnorePanic set: the reference lets it propagate."""
+
+
+# ---- checksum / flows ------------------------------------------------------
+
+
+@dataclass
+class ChecksumVerificationResult:
+    Valid: bool = False
+    Correct: int = 0
+    Actual: int = 0
+
+
+EndpointInvalid, EndpointIPv4, EndpointIPv6, EndpointMAC, EndpointTCPPort, EndpointUDPPort = 0, 1, 2, 3, 4, 5
+MaxEndpointSize = 16
+_FNV_BASIS = 14695981039346656037
+_FNV_PRIME = 1099511628211
+_M64 = (1 << 64) - 1
+
+
+def _fnv(b):
+    h = _FNV_BASIS
+    for x in b:
+        h = ((h ^ x) * _FNV_PRIME) & _M64
+    return h
+
+
+class Endpoint:
+    """flows.go:32-97"""
+
+    def __init__(self, typ, raw):
+        if len(raw) > MaxEndpointSize:
+            raise GoPanic("raw byte length greater than MaxEndpointSize")
+        self.typ, self.raw = typ, bytes(raw)
+
+    def EndpointType(self):
+        return self.typ
+
+    def Raw(self):
+        return self.raw
+
+    def FastHash(self):
+        return ((_fnv(self.raw) ^ self.typ) * _FNV_PRIME) & _M64
+
+    def __eq__(self, o):
+        return isinstance(o, Endpoint) and (self.typ, self.raw) == (o.typ, o.raw)
+
+    def __hash__(self):
+        return hash((self.typ, self.raw))
+
+    def String(self):
+        if self.typ in (EndpointIPv4, EndpointIPv6):
+            import ipaddress
+            return str(ipaddress.ip_address(self.raw))
+        if self.typ == EndpointMAC:
+            return ":".join("%02x" % b for b in self.raw)
+        if self.typ in (EndpointTCPPort, EndpointUDPPort):
+            return str(struct.unpack(">H", self.raw)[0])
+        return "%d:%s" % (self.typ, list(self.raw))
+
+    __str__ = String
+
+
+class Flow:
+    """flows.go:142-224. FastHash() of a Flow taken from a decoded packet is
+    the hash the device computed; a Flow built by hand hashes on the host."""
+
+    def __init__(self, typ, src, dst, fast_hash=None):
+        if len(src) > MaxEndpointSize or len(dst) > MaxEndpointSize:
+            raise GoPanic("flow raw byte length greater than MaxEndpointSize")
+        self.typ, self.src, self.dst = typ, bytes(src), bytes(dst)
+        self._hash = fast_hash
+
+    def FastHash(self):
+        if self._hash is not None:
+            return self._hash
+        return (((_fnv(self.src) + _fnv(self.dst)) & _M64) ^ self.typ) * _FNV_PRIME & _M64
+
+    def EndpointType(self):
+        return self.typ
+
+    def Endpoints(self):
+        return Endpoint(self.typ, self.src), Endpoint(self.typ, self.dst)
+
+    def Src(self):
+        return Endpoint(self.typ, self.src)
+
+    def Dst(self):
+        return Endpoint(self.typ, self.dst)
+
+    def Reverse(self):
+        return Flow(self.typ, self.dst, self.src, self._hash)  # FastHash is symmetric
+
+    def __eq__(self, o):
+        return isinstance(o, Flow) and (self.typ, self.src, self.dst) == (o.typ, o.src, o.dst)
+
+    def __hash__(self):
+        return hash((self.typ, self.src, self.dst))
+
+    def String(self):
+        return "%s->%s" % (self.Src(), self.Dst())
+
+    __str__ = String
+
+
+def NewFlow(t, src, dst):
+    return Flow(t, src, dst)
+
+
+# ---- Payload / Fragment ----------------------------------------------------
+
+
+class Payload:
+    """base.go:40-70"""
+    kind = _lib.DEC_PAYLOAD
+
+    def __init__(self):
+        self.data = b""
+
+    def CanDecode(self):
+        return [LayerTypePayload]
+
+    def LayerType(self):
+        return LayerTypePayload
+
+    def NextLayerType(self):
+        return LayerTypeZero
+
+    def LayerContents(self):
+        return self.data
+
+    def LayerPayload(self):
+        return b""
+
+    def Payload(self):
+        return self.data
+
+    def _hydrate(self, d):
+        self.data = d
+
+
+class Fragment(Payload):
+    """base.go:95-124"""
+    kind = _lib.DEC_FRAGMENT
+
+    def CanDecode(self):
+        return [LayerTypeFragment]
+
+    def LayerType(self):
+        return LayerTypeFragment
+
+
+# ---- packet batches ------------------------------------------------------------
+
+
+class PacketBatch:
+    """A packed, offset-indexed host batch (the gpk_batch layout)."""
+
+    def __init__(self, data, offsets, caplens):
+        self.data = np.ascontiguousarray(data, dtype=np.uint8)
+        self.offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        self.caplens = np.ascontiguousarray(caplens, dtype=np.uint32)
+
+    @classmethod
+    def from_packets(cls, packets):
+        packets = [bytes(p) for p in packets]
+        caplens = np.array([len(p) for p in packets], np.uint32)
+        offsets = np.zeros(len(packets), np.uint64)
+        if len(packets) > 1:
+            offsets[1:] = np.cumsum(caplens[:-1], dtype=np.uint64)
+        return cls(np.frombuffer(b"".join(packets) + bytes(16), np.uint8), offsets, caplens)
+
+    def __len__(self):
+        return len(self.offsets)
+
+    def packet(self, i):
+        o, c = int(self.offsets[i]), int(self.caplens[i])
+        return bytes(self.data[o:o + c])
+
+
+# ---- the parser ------------------------------------------------------------------
+
+_DEFAULT_CTX = None
+
+
+def _default_ctx():
+    global _DEFAULT_CTX
+    if _DEFAULT_CTX is None:
+        from .engine import Context
+        _DEFAULT_CTX = Context(int(os.environ.get("GPK_DEVICE", "0")))
+    return _DEFAULT_CTX
+
+
+class DecodingLayerParser:
+    """parser.go:182-317 over the GPU engine.
+
+    Differences that are not semantic: the container is always the Map form
+    (Sparse/Array/Map decode identically, layers_decoder.go:18-100); layer
+    structs are refreshed from device results, so per-packet state that the
+    reference leaves stale across calls (TCP.Multipath, IPv4.Padding) is
+    per packet here (parity notes P6)."""
+
+    def __init__(self, first, *decoders, ctx=None):
+        self.first = LayerType(first)
+        self.IgnorePanic = False
+        self.IgnoreUnsupported = False
+        self.Truncated = False
+        self._decoders = {}  # kind -> instance (last Put wins)
+        self._ctx = ctx
+        self._cfg = None
+        for d in decoders:
+            self.AddDecodingLayer(d)
+
+    def AddDecodingLayer(self, d):
+        self._decoders[d.kind] = d
+        self._cfg = None
+
+    def _config(self, outputs=_lib.OUT_ALL):
+        from .engine import ParserConfig
+        key = (tuple(sorted(self._decoders)), self.IgnorePanic, self.IgnoreUnsupported, outputs)
+        if self._cfg is None or self._cfg[0] != key:
+            p = ParserConfig(int(self.first), sorted(self._decoders), ignore_panic=self.IgnorePanic,
+                             ignore_unsupported=self.IgnoreUnsupported, outputs=outputs)
+            self._cfg = (key, p)
+        return self._cfg[1]
+
+    def ctx(self):
+        return self._ctx or _default_ctx()
+
+    def DecodeLayers(self, data, decoded):
+        """Decode one packet on the GPU; fills the registered layers and the
+        `decoded` list (truncated first, as parser.go:303-317 does)."""
+        batch = PacketBatch.from_packets([data])
+        res = self.DecodeBatch(batch, layouts=True)
+        return res.Hydrate(0, decoded)
+
+    def DecodeBatch(self, batch, layouts=False, outputs=_lib.OUT_ALL):
+        cfg = self._config(outputs)
+        r = self.ctx().decode_host(cfg, batch.data, batch.offsets, batch.caplens, layouts=layouts)
+        return BatchResult(self, batch, r)
+
+
+def NewDecodingLayerParser(first, *decoders):
+    return DecodingLayerParser(first, *decoders)
+
+
+class BatchResult:
+    """Device results of DecodeBatch, with per-packet gopacket views."""
+
+    def __init__(self, parser, batch, r):
+        self.parser, self.batch = parser, batch
+        self.records, self.err_args, self.flows, self.layouts = r["records"], r["err_args"], r["flows"], \
+            r["layouts"]
+
+    def __len__(self):
+        return len(self.records)
+
+    def status(self, i):
+        return int(self.records[i]["status"])
+
+    def Truncated(self, i):
+        return bool(self.status(i) & _lib.ST_TRUNCATED)
+
+    def Decoded(self, i):
+        from .engine import decode_codes
+        st = self.status(i)
+        n = (st >> _lib.ST_NLAYERS_SHIFT) & _lib.ST_NLAYERS_MASK
+        if n <= _lib.MAX_INLINE_LAYERS:
+            return [LayerType(t) for t in decode_codes(self.records[i]["layers"], n)]
+        full = self.parser.ctx().decoded_list_host(self.parser._config(), self.batch.packet(i))
+        return [LayerType(t) for t in full]
+
+    def Err(self, i):
+        """The error value DecodeLayers returns for packet i (None = nil)."""
+        from .engine import format_error
+        code = self.status(i) & _lib.ST_ERR_MASK
+        if code == 0:
+            return None
+        a0, a1 = int(self.err_args[2 * i]), int(self.err_args[2 * i + 1])
+        if code == 1:
+            return UnsupportedLayerType(struct.unpack("<i", struct.pack("<I", a0))[0])
+        msg = format_error(code, a0, a1)
+        if code in (2, 3, 4) and self.parser.IgnorePanic:
+            raise GoPanic(msg[len("panic: "):])
+        return GoError(msg)
+
+    def FlowHashes(self, i):
+        """(LinkFlow, NetworkFlow, TransportFlow) FastHash values; None where absent."""
+        st, n = self.status(i), len(self.records)
+        f = self.flows
+        return (int(f[i]) if st & _lib.ST_LINK_FLOW else None,
+                int(f[n + i]) if st & _lib.ST_NET_FLOW else None,
+                int(f[2 * n + i]) if st & _lib.ST_TRANSPORT_FLOW else None)
+
+    def IPv4Checksum(self, i):
+        st = self.status(i)
+        if not st & _lib.ST_IP4_CSUM:
+            return None
+        return bool(st & _lib.ST_IP4_VALID), int(self.records[i]["ip4_csum"])
+
+    def L4Checksum(self, i):
+        st = self.status(i)
+        if not st & _lib.ST_L4_CSUM:
+            return None
+        return bool(st & _lib.ST_L4_VALID), int(self.records[i]["l4_csum"])
+
+    def Hydrate(self, i, decoded):
+        """Make the parser's layer structs and `decoded` look exactly as after
+        DecodeLayers(packet i, decoded); returns its error value."""
+        p = self.parser
+        if p.first.__int__() not in [int(t) for d in p._decoders.values() for t in d.CanDecode()]:
+            # LayersDecoder (layers_decoder.go:12-16): decoded is not truncated
+            p.Truncated = False
+            return None if p.IgnoreUnsupported else UnsupportedLayerType(p.first)
+        decoded[:] = self.Decoded(i)
+        p.Truncated = self.Truncated(i)
+        err = self.Err(i)
+        if self.layouts is None:
+            raise ValueError("Hydrate needs layouts=True results")
+        pkt = self.batch.packet(i)
+        lay = self.layouts[i]
+        st = self.status(i)
+        lh, nh, th = self.FlowHashes(i)
+        for slot, kind in enumerate(_lib.LAYOUT_SLOTS):
+            s = int(lay["start"][slot])
+            if s == _lib.LAYOUT_ABSENT:
+                continue
+            e = int(lay["end"][slot])
+            if slot == 7:
+                kind = _lib.DEC_PAYLOAD if _lib.DEC_PAYLOAD in p._decoders and \
+                    LayerTypePayload in decoded else _lib.DEC_FRAGMENT
+            inst = p._decoders.get(kind)
+            if inst is None:
+                continue
+            inst._hydrate(pkt[s:e])
+            if kind == _lib.DEC_ETHERNET and lh is not None:
+                inst._link_hash = lh
+            if kind == _lib.DEC_IPV4 and st & _lib.ST_IP4_CSUM:
+                inst._csum = (None, ChecksumVerificationResult(bool(st & _lib.ST_IP4_VALID),
+                                                               int(self.records[i]["ip4_csum"]), inst.Checksum))
+            if kind in (_lib.DEC_TCP, _lib.DEC_UDP) and st & _lib.ST_L4_CSUM:
+                inst._csum = (None, ChecksumVerificationResult(bool(st & _lib.ST_L4_VALID),
+                                                               int(self.records[i]["l4_csum"]), inst.Checksum))
+        return err

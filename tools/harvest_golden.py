@@ -22,8 +22,8 @@ import sys
 ARRAYS = {
     # layers/decode_test.go:23-61 testSimpleTCPPacket (420 B Eth/IPv4/TCP HTTP GET)
     "simple_tcp": ("layers/decode_test.go", "testSimpleTCPPacket"),
-    # layers/decode_test.go:532-547 TestDecodeSmallTCPPacketHasEmptyPayload
-    "small_tcp_trailer": ("layers/decode_test.go", 535),
+    # layers/decode_test.go:532-547 TestDecodeSmallTCPPacketHasEmptyPayload (literal at :533)
+    "small_tcp_trailer": ("layers/decode_test.go", 533),
     # layers/decode_test.go:549-572 TestDecodeVLANPacket
     "vlan_tcp": ("layers/decode_test.go", 551),
     # layers/decode_test.go:1018-1031 TestDecodeUDPPacketTooSmall
