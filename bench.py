@@ -59,7 +59,30 @@ def barrier(world):
     torch.cuda.synchronize()
 
 
-def run_config(name, n, steps, warmup, rank, world, ctx, check_sample=2048):
+def probe_read(data, nbytes, steps, stream):
+    """Achievable streaming-read rate over the same buffer (GB/s): a kernel
+    that only loads the bytes (gpk_probe_read), timed like the decode."""
+    import torch
+    from gopacket_amd import _lib
+    S = _lib.synth_lib()
+    sink = torch.zeros(1, dtype=torch.int32, device="cuda")
+    blocks = 256 * 8
+
+    def go():
+        rc = S.gpk_probe_read(data.data_ptr(), nbytes, sink.data_ptr(), blocks, stream.cuda_stream)
+        assert rc == 0
+
+    go()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(steps):
+        go()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    return (nbytes & ~15) / (e0.elapsed_time(e1) / steps * 1e-3) / 1e9
+
+
+def run_config(name, n, steps, warmup, rank, world, ctx, check_sample=2048, probe=False):
     import torch
     from gopacket_amd import engine, shard, synth
     cfg = CONFIGS[name]
@@ -91,11 +114,12 @@ def run_config(name, n, steps, warmup, rank, world, ctx, check_sample=2048):
     kernel_ms = e0.elapsed_time(e1) / steps
     wall_max = shard.max_over_ranks(wall, world, device="cuda")
 
+    probe_gbs = probe_read(data, payload_bytes, steps, stream) if probe else None
     parity = None
     if check_sample:
         parity = sample_parity(name, cfg, rec, fl, err, first, n, check_sample)
     res = dict(n=n, payload_bytes=payload_bytes, wall_s=wall_max, kernel_ms=kernel_ms,
-               algo_bytes=payload_bytes + INDEX_BYTES * n, parity=parity)
+               algo_bytes=payload_bytes + INDEX_BYTES * n, parity=parity, probe_gbs=probe_gbs)
     del data, off, cap, rec, err, fl
     torch.cuda.empty_cache()
     return res
@@ -171,6 +195,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
+    ap.add_argument("--no-probe", action="store_true", help="skip the streaming-read reference kernel")
     args = ap.parse_args()
 
     import torch
@@ -181,7 +206,8 @@ def main():
     results = {}
     for name in names:
         results[name] = run_config(name, args.packets, args.steps, args.warmup, rank, world, ctx,
-                                   check_sample=0 if args.no_parity else 2048)
+                                   check_sample=0 if args.no_parity else 2048,
+                                   probe=not args.no_probe)
     if rank == 0:
         head = names[0]
         r = results[head]
@@ -200,7 +226,8 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": load_traffic(head),
                          "kernel": "gpk::decode_kernel<true,false>", "kernel_ms": round(r["kernel_ms"], 4),
-                         "algo_bytes_per_launch": r["algo_bytes"]},
+                         "algo_bytes_per_launch": r["algo_bytes"],
+                         "probe_read_GBps": r["probe_gbs"] and round(r["probe_gbs"], 1)},
             "parity": r["parity"],
             "configs": {},
         }
@@ -211,7 +238,8 @@ def main():
                 "workload": CONFIGS[name]["workload"],
                 "value": round(s["n"] * world * args.steps / s["wall_s"] / 1e6, 2), "unit": "Mpkts/s",
                 "kernel_ms": round(s["kernel_ms"], 4), "achieved_GBps": round(ach, 1),
-                "frac": round(ach / HBM_PEAK_GBS, 4), "parity": s["parity"]}
+                "frac": round(ach / HBM_PEAK_GBS, 4), "parity": s["parity"],
+                "probe_read_GBps": s["probe_gbs"] and round(s["probe_gbs"], 1)}
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(head, seconds=args.cpu_seconds)
         else:

@@ -11,7 +11,12 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libgpk.so")
+# GPK_LIB_VARIANT=<name> loads build/libgpk_<name>.so instead: compile-time
+# kernel variants built by `make -C gopacket_amd/csrc variant V=<name>
+# VDEFS=...` for A/B measurements (tools/ab.sh). Unset in normal use.
+_VARIANT = os.environ.get("GPK_LIB_VARIANT")
+LIB_PATH = (os.path.join(_HERE, "build", "libgpk_%s.so" % _VARIANT) if _VARIANT
+            else os.path.join(_HERE, "libgpk.so"))
 SYNTH_PATH = os.path.join(_HERE, "libgpk_synth.so")
 
 # include/gpk.h constants
@@ -156,5 +161,8 @@ def synth_lib():
         S.gpk_synth_device.restype = ctypes.c_int
         S.gpk_synth_bytes.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64]
         S.gpk_synth_bytes.restype = ctypes.c_uint64
+        S.gpk_probe_read.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int,
+                                     ctypes.c_void_p]
+        S.gpk_probe_read.restype = ctypes.c_int
         _synth = S
     return _synth

@@ -27,11 +27,23 @@ namespace gpk {
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-// Streaming 16-byte load (read-once packet bytes: non-temporal).
-__device__ __forceinline__ uint4 ld16(const uint8_t* p) {
-  u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+#ifndef GPK_NT_A
+#define GPK_NT_A 1
+#endif
+#ifndef GPK_NT_B
+#define GPK_NT_B 1
+#endif
+
+// 16-byte load; read-once packet bytes are non-temporal.
+template <bool kNT>
+__device__ __forceinline__ uint4 ld16t(const uint8_t* p) {
+  u32x4 x = kNT ? __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p))
+                : *reinterpret_cast<const u32x4*>(p);
   return make_uint4(x.x, x.y, x.z, x.w);
 }
+// header window and partial edge chunks (phase A) / full chunks (phase B)
+__device__ __forceinline__ uint4 ld16(const uint8_t* p) { return ld16t<GPK_NT_A>(p); }
+__device__ __forceinline__ uint4 ld16b(const uint8_t* p) { return ld16t<GPK_NT_B>(p); }
 
 // Byte sums with v_dot4_u32_u8: bytes 0,2 (even addresses) and 1,3 (odd).
 __device__ __forceinline__ uint32_t dot_even(uint32_t w, uint32_t acc) {
@@ -290,7 +302,7 @@ __global__ __launch_bounds__(kBlock) void decode_kernel(KParams P) {
             // first chunk and discards it): no exec-mask branches
             uint64_t A = b0[g] + rr + h * 1024 + lane * 16;
             ok[g][h] = A < e0[g];
-            v[g][h] = ld16(P.data + (ok[g][h] ? A : b0[g]));
+            v[g][h] = ld16b(P.data + (ok[g][h] ? A : b0[g]));
           }
         bool more = false;
 #pragma unroll

@@ -75,6 +75,34 @@ __global__ void fill_kernel(int cfg, uint64_t first, uint64_t n, uint8_t* data, 
 
 }  // namespace
 
+// Streaming-read probe: byte sum of data[0, nbytes) (nbytes % 16 == 0) with
+// coalesced 16-byte non-temporal loads, 4 in flight per lane. It moves the
+// same bytes as the decode kernel with none of its work, so its rate is the
+// achievable HBM read rate of this box for that buffer (bench.py context
+// for roofline.frac).
+__global__ __launch_bounds__(256) void probe_read_kernel(const uint8_t* data, uint64_t nvec, uint32_t* out) {
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  const u32x4* v = reinterpret_cast<const u32x4*>(data);
+  const uint64_t stride = (uint64_t)gridDim.x * 256;
+  uint64_t k = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  uint32_t acc = 0;
+  for (; k + 3 * stride < nvec; k += 4 * stride) {
+    u32x4 a = __builtin_nontemporal_load(v + k);
+    u32x4 b = __builtin_nontemporal_load(v + k + stride);
+    u32x4 c = __builtin_nontemporal_load(v + k + 2 * stride);
+    u32x4 d = __builtin_nontemporal_load(v + k + 3 * stride);
+    acc = __builtin_amdgcn_udot4(a.x ^ b.y ^ c.z ^ d.w, 0x01010101u, acc, false);
+    acc = __builtin_amdgcn_udot4(a.y ^ b.z ^ c.w ^ d.x, 0x01010101u, acc, false);
+    acc = __builtin_amdgcn_udot4(a.z ^ b.w ^ c.x ^ d.y, 0x01010101u, acc, false);
+    acc = __builtin_amdgcn_udot4(a.w ^ b.x ^ c.y ^ d.z, 0x01010101u, acc, false);
+  }
+  for (; k < nvec; k += stride) {
+    u32x4 a = __builtin_nontemporal_load(v + k);
+    acc = __builtin_amdgcn_udot4(a.x ^ a.y ^ a.z ^ a.w, 0x01010101u, acc, false);
+  }
+  if (acc == 0x9e3779b9u) out[0] = acc;  // keep the loads live; practically never stores
+}
+
 extern "C" {
 
 uint32_t gpk_synth_len(int cfg, uint64_t i) { return frame_len(cfg, i); }
@@ -118,10 +146,10 @@ int gpk_synth_device(int cfg, uint64_t first, uint64_t n, uint8_t* data, uint64_
     // 64-bit running sum (IMIX batches exceed 4 GiB)
     hipcub::TransformInputIterator<uint64_t, Widen, const uint32_t*> in(caplens, Widen());
     size_t tmp_bytes = 0;
-    hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, in, offsets, (int)n, s);
+    if (hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, in, offsets, (int)n, s) != hipSuccess) return -2;
     void* tmp = nullptr;
     if (hipMallocAsync(&tmp, tmp_bytes, s) != hipSuccess) return -2;
-    hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, in, offsets, (int)n, s);
+    if (hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, in, offsets, (int)n, s) != hipSuccess) return -2;
     (void)hipFreeAsync(tmp, s);
   }
   hipLaunchKernelGGL(fill_kernel, g, b, 0, s, cfg, first, n, data, offsets);
@@ -134,6 +162,12 @@ uint64_t gpk_synth_bytes(int cfg, uint64_t first, uint64_t n) {
   uint64_t t = 0;
   for (uint64_t k = 0; k < n; k++) t += frame_len(cfg, first + k);
   return t;
+}
+
+// Launch the streaming-read probe over data[0, nbytes & ~15) on `stream`.
+int gpk_probe_read(const uint8_t* data, uint64_t nbytes, uint32_t* out, int blocks, void* stream) {
+  hipLaunchKernelGGL(probe_read_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, data, nbytes / 16, out);
+  return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
 }  // extern "C"
