@@ -196,12 +196,17 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--no-probe", action="store_true", help="skip the streaming-read reference kernel")
+    ap.add_argument("--tables", default="auto", choices=["auto", "global"],
+                    help="next-layer tables: compact LDS copy (auto) or device-memory tables (global)")
     args = ap.parse_args()
 
     import torch
     rank, world, local = dist_init()
     from gopacket_amd import engine
     ctx = engine.Context(local)
+    if args.tables == "global":
+        from gopacket_amd import _lib
+        ctx.set_table_mode(_lib.TABLES_GLOBAL)
     names = args.configs.split(",")
     results = {}
     for name in names:

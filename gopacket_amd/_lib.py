@@ -22,6 +22,7 @@ SYNTH_PATH = os.path.join(_HERE, "libgpk_synth.so")
 # include/gpk.h constants
 GPK_OK = 0
 OUT_IP4_CSUM, OUT_L4_CSUM, OUT_FLOWS, OUT_ALL = 1, 2, 4, 7
+TABLES_AUTO, TABLES_GLOBAL = 0, 1
 DEC_NONE, DEC_ETHERNET, DEC_DOT1Q, DEC_IPV4, DEC_IPV6, DEC_IPV6_EXT, DEC_TCP, DEC_UDP, DEC_PAYLOAD, \
     DEC_FRAGMENT = range(10)
 ST_ERR_MASK = 0x7F
@@ -50,9 +51,8 @@ EXPORTS = (
     "gpk_parser_create", "gpk_parser_destroy", "gpk_parser_add_decoder", "gpk_parser_set_options",
     "gpk_parser_set_outputs", "gpk_parser_decoder_for", "gpk_parser_set_ethertype",
     "gpk_parser_set_ipprotocol", "gpk_parser_set_tcp_port", "gpk_parser_set_udp_port", "gpk_ctx_create",
-    "gpk_ctx_destroy", "gpk_decode_batch", "gpk_decode_batch_host", "gpk_decoded_list", "gpk_decoded_list_host",
-    "gpk_host_alloc",
-    "gpk_host_free", "gpk_format_error", "gpk_layer_type_name", "gpk_code_layer_type", "gpk_strerror",
+    "gpk_ctx_destroy", "gpk_ctx_set_table_mode", "gpk_decode_batch", "gpk_decode_batch_host", "gpk_decoded_list",
+    "gpk_decoded_list_host", "gpk_host_alloc", "gpk_host_free", "gpk_format_error", "gpk_layer_type_name", "gpk_code_layer_type", "gpk_strerror",
     "gpk_last_hip_error", "gpk_abi_version",
 )
 
@@ -110,6 +110,7 @@ def lib():
         "gpk_parser_set_udp_port": ([vp, u32, ctypes.c_int32], c_int),
         "gpk_ctx_create": ([P(vp), c_int], c_int),
         "gpk_ctx_destroy": ([vp], c_int),
+        "gpk_ctx_set_table_mode": ([vp, c_int], c_int),
         "gpk_decode_batch": ([vp, vp, P(Batch), P(Results), vp], c_int),
         "gpk_decode_batch_host": ([vp, vp, P(Batch), P(Results)], c_int),
         "gpk_decoded_list": ([vp, vp, P(Batch), u64, P(i64), u32, P(u32)], c_int),

@@ -25,6 +25,26 @@ struct DevTables {
   uint8_t dispatch[GPK_MAX_LAYER_TYPE];  // LayerType -> GPK_DEC_*
 };
 
+// Compact copy of a parser's lookup tables (LTab), built by the host when
+// they fit (gpk_host.cpp build_compact) and copied into LDS by every block.
+// Blob layout in dwords: LayerType per handle, kind|code<<4 per handle (u8),
+// handle per IP protocol (u8), then the hash slots of the EtherType, TCP port
+// and UDP port tables.
+constexpr int kCtVal = 0;
+constexpr int kCtKc = 128;
+constexpr int kCtIpp = 160;
+constexpr int kCtSlots = 224;
+constexpr int kCtMaxHandles = 128;
+constexpr int kCtMaxSlots = 512;
+constexpr int kCtDwords = kCtSlots + kCtMaxSlots;
+struct CompactGeom {
+  uint32_t eth_off, eth_shift, eth_mask, eth_probe, eth_def;  // off: dwords from the blob base
+  uint32_t tcp_off, tcp_shift, tcp_mask, tcp_probe, tcp_def;
+  uint32_t udp_off, udp_shift, udp_mask, udp_probe, udp_def;
+  uint32_t frag_h, zero_h, first_h, payload_h;
+  uint32_t words;  // blob dwords to copy
+};
+
 struct KParams {
   const uint8_t* data;
   const uint64_t* offsets;
@@ -38,6 +58,9 @@ struct KParams {
   int64_t first;
   uint32_t outputs;
   int32_t ignore_unsupported;
+  int32_t first_kind;       // decoder registered for `first` (GPK_DEC_NONE if none)
+  const uint32_t* ctab;     // compact blob in device memory, or null: global tables
+  CompactGeom cg;
 };
 
 // LDS geometry: per lane a header window of WIN_CHUNKS 16-byte chunks.
@@ -116,8 +139,8 @@ __device__ __forceinline__ Res rok(uint32_t trunc, uint32_t off, uint32_t len, i
 }
 
 // ---- layers/ethernet.go:42-63 (+ NextLayerType :111-113) ------------------
-template <class R>
-__device__ __forceinline__ Res dec_ethernet(const DevTables* T, const R& r, uint32_t off, uint32_t len) {
+template <class TT, class R>
+__device__ __forceinline__ Res dec_ethernet(const TT& T, const R& r, uint32_t off, uint32_t len) {
   if (len < 14) return rerr(0, GPK_ERR_ETH_TOO_SMALL);
   uint32_t et = rd16(r, off + 12);
   uint32_t plen = len - 14, trunc = 0;
@@ -126,19 +149,19 @@ __device__ __forceinline__ Res dec_ethernet(const DevTables* T, const R& r, uint
     else plen = et;
     et = 0;
   }
-  return rok(trunc, off + 14, plen, T->ethertype[et]);
+  return rok(trunc, off + 14, plen, T.eth(et));
 }
 
 // ---- layers/dot1q.go:30-41, :49-51 -----------------------------------------
-template <class R>
-__device__ __forceinline__ Res dec_dot1q(const DevTables* T, const R& r, uint32_t off, uint32_t len) {
+template <class TT, class R>
+__device__ __forceinline__ Res dec_dot1q(const TT& T, const R& r, uint32_t off, uint32_t len) {
   if (len < 4) return rerr(1, GPK_ERR_DOT1Q_SHORT, len);
-  return rok(0, off + 4, len - 4, T->ethertype[rd16(r, off + 2)]);
+  return rok(0, off + 4, len - 4, T.eth(rd16(r, off + 2)));
 }
 
 // ---- layers/ip4.go:178-271, :277-282 ---------------------------------------
-template <class R>
-__device__ __forceinline__ Res dec_ipv4(const DevTables* T, const R& r, uint32_t off, uint32_t len) {
+template <class TT, class R>
+__device__ __forceinline__ Res dec_ipv4(const TT& T, const R& r, uint32_t off, uint32_t len) {
   if (len < 20) return rerr(1, GPK_ERR_IP4_HDR_SHORT, len);
   uint32_t b0 = rd8(r, off);
   uint32_t length = rd16(r, off + 2);
@@ -171,15 +194,15 @@ __device__ __forceinline__ Res dec_ipv4(const DevTables* T, const R& r, uint32_t
     rem -= ol;
   }
   uint32_t ff = rd16(r, off + 6);
-  int32_t next = ((ff & 0x2000u) || (ff & 0x1fffu)) ? GPK_LT_FRAGMENT : T->ipprotocol[rd8(r, off + 9)];
+  int32_t next = ((ff & 0x2000u) || (ff & 0x1fffu)) ? T.frag() : T.ipp(rd8(r, off + 9));
   return rok(trunc, off + hl, len - hl, next);
 }
 
 // ---- IPv6: layers/ip6.go:221-278 with inline HopByHop :509-526,
 //      decodeIPv6ExtensionBase :418-432, TLV :327-346, jumbogram :54-76,
 //      NextLayerType :286-291 -------------------------------------------------
-template <class R>
-__device__ __forceinline__ Res dec_ipv6(const DevTables* T, const R& r, const Rd& rm, uint32_t off,
+template <class TT, class R>
+__device__ __forceinline__ Res dec_ipv6(const TT& T, const R& r, const Rd& rm, uint32_t off,
                                         uint32_t len) {
   if (len < 40) return rerr(1, GPK_ERR_IP6_HDR_SHORT, len);
   uint32_t length = rd16(r, off + 4);
@@ -219,7 +242,7 @@ __device__ __forceinline__ Res dec_ipv6(const DevTables* T, const R& r, const Rd
         trunc = 1;
         l = plen;
       }
-      return rok(trunc, poff, l, T->ipprotocol[hnh]);
+      return rok(trunc, poff, l, T.ipp(hnh));
     }
     if (length == 0) return rerr(0, GPK_ERR_IP6_LEN0_NO_JUMBO);
     poff += actual;  // ip6.go:262, then trimmed to the full Length below
@@ -231,17 +254,17 @@ __device__ __forceinline__ Res dec_ipv6(const DevTables* T, const R& r, const Rd
     trunc = 1;
     length = plen;
   }
-  return rok(trunc, poff, length, T->ipprotocol[next_nh]);
+  return rok(trunc, poff, length, T.ipp(next_nh));
 }
 
 // ---- IPv6ExtensionSkipper ip6.go:443-461 (base :418-432) -------------------
-template <class R>
-__device__ __forceinline__ Res dec_ipv6_ext(const DevTables* T, const R& r, uint32_t off, uint32_t len) {
+template <class TT, class R>
+__device__ __forceinline__ Res dec_ipv6_ext(const TT& T, const R& r, uint32_t off, uint32_t len) {
   if (len < 2) return rerr(1, GPK_ERR_IP6_EXT_SHORT, len);
   uint32_t nh = rd8(r, off);
   uint32_t actual = rd8(r, off + 1) * 8 + 8;
   if (len < actual) return rerr(0, GPK_ERR_IP6_EXT_LEN, len, actual);
-  return rok(0, off + actual, len - actual, T->ipprotocol[nh]);
+  return rok(0, off + actual, len - actual, T.ipp(nh));
 }
 
 // ---- MPTCP option body tcp.go:347-533 with Go's bounds checks ---------------
@@ -368,8 +391,8 @@ __device__ __forceinline__ Res mptcp_option(const R& r, uint32_t p, uint32_t sle
 #undef GPK_SL
 
 // ---- layers/tcp.go:291-551, NextLayerType :591-597 --------------------------
-template <class R>
-__device__ __forceinline__ Res dec_tcp(const DevTables* T, const R& r, uint32_t off, uint32_t len,
+template <class TT, class R>
+__device__ __forceinline__ Res dec_tcp(const TT& T, const R& r, uint32_t off, uint32_t len,
                                        uint32_t caplen) {
   if (len < 20) return rerr(1, GPK_ERR_TCP_HDR_SHORT, len);
   uint32_t ports = rd32(r, off);
@@ -397,14 +420,12 @@ __device__ __forceinline__ Res dec_tcp(const DevTables* T, const R& r, uint32_t 
     slen -= ol;
     scap -= ol;
   }
-  int32_t lt = T->tcp_port[ports & 0xffff];
-  if (lt == GPK_LT_PAYLOAD) lt = T->tcp_port[ports >> 16];
-  return rok(0, off + ds, len - ds, lt);
+  return rok(0, off + ds, len - ds, T.tcp(ports));
 }
 
 // ---- layers/udp.go:30-56, :114-119 -----------------------------------------
-template <class R>
-__device__ __forceinline__ Res dec_udp(const DevTables* T, const R& r, uint32_t off, uint32_t len) {
+template <class TT, class R>
+__device__ __forceinline__ Res dec_udp(const TT& T, const R& r, uint32_t off, uint32_t len) {
   if (len < 8) return rerr(1, GPK_ERR_UDP_HDR_SHORT, len);
   uint32_t ports = rd32(r, off);
   uint32_t length = rd16(r, off + 4);
@@ -415,9 +436,7 @@ __device__ __forceinline__ Res dec_udp(const DevTables* T, const R& r, uint32_t 
   } else if (length != 0) {
     return rerr(0, GPK_ERR_UDP_TOO_SMALL, length);
   }
-  int32_t lt = T->udp_port[ports & 0xffff];
-  if (lt == GPK_LT_PAYLOAD) lt = T->udp_port[ports >> 16];
-  return rok(trunc, off + 8, hlen - 8, lt, hlen);
+  return rok(trunc, off + 8, hlen - 8, T.udp(ports), hlen);
 }
 
 __device__ __forceinline__ uint32_t code_of(int32_t typ) {
@@ -438,6 +457,85 @@ __device__ __forceinline__ uint32_t code_of(int32_t typ) {
   }
 }
 
+
+// ---- next-layer lookups ------------------------------------------------------
+// A decoder's NextLayerType() yields a "type handle": GTab (global tables,
+// any configuration) uses the LayerType itself; LTab (the compact copy in
+// LDS, used whenever the parser's tables fit, see CompactGeom) uses an index
+// into the parser's dictionary of distinct LayerTypes. Either way kind(h) is
+// the registered DecodingLayer (parser.go:177-183 decoders map), lt(h) the
+// LayerType and code(h) its 4-bit record code.
+// TCP/UDP: the destination port's type unless that is Payload, then the
+// source port's (tcp.go:591-597, udp.go:114-119).
+struct GTab {
+  const DevTables* T;
+  __device__ __forceinline__ int32_t eth(uint32_t k) const { return T->ethertype[k]; }
+  __device__ __forceinline__ int32_t ipp(uint32_t k) const { return T->ipprotocol[k]; }
+  __device__ __forceinline__ int32_t frag() const { return GPK_LT_FRAGMENT; }
+  __device__ __forceinline__ int32_t zero() const { return GPK_LT_ZERO; }
+  __device__ __forceinline__ int32_t first(int64_t lt) const { return (int32_t)lt; }
+  __device__ __forceinline__ int32_t tcp(uint32_t ports) const {
+    int32_t lt = T->tcp_port[ports & 0xffff];
+    return lt == GPK_LT_PAYLOAD ? T->tcp_port[ports >> 16] : lt;
+  }
+  __device__ __forceinline__ int32_t udp(uint32_t ports) const {
+    int32_t lt = T->udp_port[ports & 0xffff];
+    return lt == GPK_LT_PAYLOAD ? T->udp_port[ports >> 16] : lt;
+  }
+  __device__ __forceinline__ int kind(int32_t h) const {
+    return (h >= 0 && h < GPK_MAX_LAYER_TYPE) ? (int)T->dispatch[h] : GPK_DEC_NONE;
+  }
+  __device__ __forceinline__ int32_t lt(int32_t h) const { return h; }
+  __device__ __forceinline__ uint32_t code(int32_t h) const { return code_of(h); }
+};
+
+// Compact tables in LDS (dword offsets from the blob base). Lookup of a
+// 16-bit key in an open-addressed table: home slot (k * 0x9E3779B1) >> shift,
+// linear probing; the host records the longest probe so an absent key stops
+// after at most that many slots. Entry = key | handle << 16, empty =
+// 0xFFFFFFFF.
+struct LTab {
+  CompactGeom g;  // from the kernel arguments: scalar registers
+  uint32_t base;  // LDS dword index of the blob
+  __device__ __forceinline__ int32_t probe(uint32_t k, uint32_t off, uint32_t shift, uint32_t mask,
+                                           uint32_t maxp, uint32_t def) const {
+    uint32_t h = (k * 0x9E3779B1u) >> shift;
+    for (uint32_t i = 0; i <= maxp; i++) {
+      uint32_t e = gpk_smem[base + off + ((h + i) & mask)];  // off: from the blob base
+      if (e == 0xffffffffu) break;  // empty (before the key test: key 0xFFFF)
+      if ((e & 0xffffu) == k) return (int32_t)(e >> 16);
+    }
+    return (int32_t)def;
+  }
+  __device__ __forceinline__ int32_t eth(uint32_t k) const {
+    return probe(k, g.eth_off, g.eth_shift, g.eth_mask, g.eth_probe, g.eth_def);
+  }
+  __device__ __forceinline__ int32_t ipp(uint32_t k) const {
+    return (int32_t)((gpk_smem[base + kCtIpp + (k >> 2)] >> (8 * (k & 3))) & 0xff);
+  }
+  __device__ __forceinline__ int32_t frag() const { return (int32_t)g.frag_h; }
+  __device__ __forceinline__ int32_t zero() const { return (int32_t)g.zero_h; }
+  __device__ __forceinline__ int32_t first(int64_t) const { return (int32_t)g.first_h; }
+  __device__ __forceinline__ int32_t port(uint32_t k, uint32_t t) const {
+    return t ? probe(k, g.udp_off, g.udp_shift, g.udp_mask, g.udp_probe, g.udp_def)
+             : probe(k, g.tcp_off, g.tcp_shift, g.tcp_mask, g.tcp_probe, g.tcp_def);
+  }
+  __device__ __forceinline__ int32_t tcp(uint32_t ports) const {
+    int32_t h = port(ports & 0xffff, 0);
+    return h == (int32_t)g.payload_h ? port(ports >> 16, 0) : h;
+  }
+  __device__ __forceinline__ int32_t udp(uint32_t ports) const {
+    int32_t h = port(ports & 0xffff, 1);
+    return h == (int32_t)g.payload_h ? port(ports >> 16, 1) : h;
+  }
+  __device__ __forceinline__ uint32_t kc(int32_t h) const {
+    return (gpk_smem[base + kCtKc + ((uint32_t)h >> 2)] >> (8 * (h & 3))) & 0xff;
+  }
+  __device__ __forceinline__ int kind(int32_t h) const { return (int)(kc(h) & 15); }
+  __device__ __forceinline__ int32_t lt(int32_t h) const { return (int32_t)gpk_smem[base + kCtVal + h]; }
+  __device__ __forceinline__ uint32_t code(int32_t h) const { return kc(h) >> 4; }
+};
+
 // Most packet bytes a decoder's DecodeFromBytes reads past its offset
 // (IPv4/TCP: 15-word headers incl. options; IPv6: the fixed header, its
 // HopByHop TLVs always go through the mixed reader).
@@ -454,9 +552,6 @@ __device__ __forceinline__ uint32_t max_header(int kind) {
   }
 }
 
-__device__ __forceinline__ int kind_for(const DevTables* T, int64_t typ) {
-  return (typ >= 0 && typ < GPK_MAX_LAYER_TYPE) ? (int)T->dispatch[typ] : GPK_DEC_NONE;
-}
 
 // Result of running the parser on one packet.
 // Per decoder instance (gopacket keeps one struct per DecodingLayer, so the
@@ -529,18 +624,17 @@ struct Outcome {
   uint32_t err, a0, a1, trunc;
 };
 
-template <bool FULL>
-__device__ __forceinline__ Outcome run_parser(const KParams& P, const Rd& r, uint32_t caplen, Parse& q,
+template <bool FULL, class TT>
+__device__ __forceinline__ Outcome run_parser(const KParams& P, const TT& T, const Rd& r, uint32_t caplen, Parse& q,
                                               int64_t* list = nullptr, uint32_t list_cap = 0) {
-  const DevTables* T = P.tab;
   q.init();
   Outcome out{0, 0, 0, 0};
-  int kind = kind_for(T, P.first);
+  int kind = P.first_kind;  // host: decoder registered for P.first
   if (kind == GPK_DEC_NONE) {  // LayersDecoder :12-16: (first, nil), decoded untouched
     if (!P.ignore_unsupported) out.err = GPK_ERR_UNSUPPORTED, out.a0 = (uint32_t)P.first;
     return out;
   }
-  int32_t typ = (int32_t)P.first;
+  int32_t typ = T.first(P.first);
   uint32_t off = 0, len = caplen;
   for (;;) {
     Res x;
@@ -557,7 +651,7 @@ __device__ __forceinline__ Outcome run_parser(const KParams& P, const Rd& r, uin
       case GPK_DEC_TCP: x = fast ? dec_tcp(T, rl, off, len, caplen) : dec_tcp(T, r, off, len, caplen); break;
       case GPK_DEC_UDP: x = fast ? dec_udp(T, rl, off, len) : dec_udp(T, r, off, len); break;
       default:  // gopacket.Payload / gopacket.Fragment (base.go:61-70, :115-124)
-        x = rok(0, off + len, 0, GPK_LT_ZERO);
+        x = rok(0, off + len, 0, T.zero());
         break;
     }
     out.trunc |= x.trunc;
@@ -568,8 +662,8 @@ __device__ __forceinline__ Outcome run_parser(const KParams& P, const Rd& r, uin
       out.a1 = x.a1;
       return out;
     }
-    if (q.nlayers < GPK_MAX_INLINE_LAYERS) q.layers |= (uint64_t)code_of(typ) << (4 * q.nlayers);
-    if (FULL && q.nlayers < list_cap) list[q.nlayers] = typ;
+    if (q.nlayers < GPK_MAX_INLINE_LAYERS) q.layers |= (uint64_t)T.code(typ) << (4 * q.nlayers);
+    if (FULL && q.nlayers < list_cap) list[q.nlayers] = T.lt(typ);
     q.nlayers++;
     q.set(kind, off, off + len);
     if (kind == GPK_DEC_UDP) q.udp_hlen = x.aux;
@@ -579,9 +673,10 @@ __device__ __forceinline__ Outcome run_parser(const KParams& P, const Rd& r, uin
     off = x.off;
     len = x.len;
     if (len == 0) return out;  // LayerPayload() empty: success (layers_decoder.go:71-73)
-    kind = kind_for(T, typ);
+    kind = T.kind(typ);
     if (kind == GPK_DEC_NONE) {  // (typ, nil): UnsupportedLayerType unless typ == 0
-      if (typ != GPK_LT_ZERO && !P.ignore_unsupported) out.err = GPK_ERR_UNSUPPORTED, out.a0 = (uint32_t)typ;
+      const int32_t lt = T.lt(typ);
+      if (lt != GPK_LT_ZERO && !P.ignore_unsupported) out.err = GPK_ERR_UNSUPPORTED, out.a0 = (uint32_t)lt;
       return out;
     }
   }

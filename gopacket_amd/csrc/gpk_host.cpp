@@ -13,6 +13,8 @@
 #include <cstring>
 #include <atomic>
 #include <mutex>
+#include <unordered_map>
+#include <vector>
 #include <new>
 #include <string>
 
@@ -52,6 +54,10 @@ struct gpk_parser {
 struct gpk_ctx {
   int device = 0;
   gpk::DevTables* dtab = nullptr;
+  uint32_t* dctab = nullptr;  // compact blob (gpk::kCtDwords), valid when compact
+  bool compact = false;
+  bool force_global = false;  // gpk_ctx_set_table_mode(GPK_TABLES_GLOBAL)
+  gpk::CompactGeom cg{};
   const gpk_parser* uploaded = nullptr;
   uint64_t uploaded_version = 0;
   // staging for gpk_decode_batch_host / gpk_decoded_list
@@ -195,8 +201,14 @@ int gpk_ctx_create(gpk_ctx** out, int device) {
     delete c;
     return GPK_ENOMEM;
   }
+  if (hipMalloc(&c->dctab, gpk::kCtDwords * 4) != hipSuccess) {
+    (void)hipFree(c->dtab);
+    delete c;
+    return GPK_ENOMEM;
+  }
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
     (void)hipFree(c->dtab);
+    (void)hipFree(c->dctab);
     delete c;
     return GPK_EHIP;
   }
@@ -209,17 +221,118 @@ int gpk_ctx_destroy(gpk_ctx* c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   if (c->dtab) (void)hipFree(c->dtab);
+  if (c->dctab) (void)hipFree(c->dctab);
   if (c->dbuf) (void)hipFree(c->dbuf);
   delete c;
   return GPK_OK;
 }
 
-static int upload(gpk_ctx* c, const gpk_parser* p, hipStream_t s) {
-  if (c->uploaded_version == p->version) return GPK_OK;
-  HIPCHK(hipMemcpyAsync(c->dtab, &p->tab, sizeof(gpk::DevTables), hipMemcpyHostToDevice, s));
-  HIPCHK(hipStreamSynchronize(s));  // p->tab may change after we return
-  c->uploaded = p;
-  c->uploaded_version = p->version;
+static uint32_t host_code_of(int64_t lt) {
+  for (unsigned k = 1; k < 13; k++)
+    if (gpk_code_layer_type(k) == lt) return k;
+  return GPK_CODE_NONE;
+}
+
+// Compact LDS copy of the lookup tables (gpk_device.h LTab): a dictionary of
+// the distinct LayerTypes the tables can produce (handles), the IP protocol
+// table as handles, and for each 16-bit table its most common value plus an
+// open-addressed hash of the keys that differ from it. Returns false when
+// the tables do not fit (more than kCtMaxHandles distinct types or
+// kCtMaxSlots slots): the kernels then read the global tables.
+static bool build_compact(const gpk::DevTables& t, int64_t first, uint32_t* blob, gpk::CompactGeom& g) {
+  using namespace gpk;
+  std::vector<int32_t> vals;
+  std::unordered_map<int32_t, uint32_t> idx;
+  bool ok = true;
+  auto handle = [&](int32_t lt) -> uint32_t {
+    auto it = idx.find(lt);
+    if (it != idx.end()) return it->second;
+    if (vals.size() >= (size_t)kCtMaxHandles) {
+      ok = false;
+      return 0;
+    }
+    idx[lt] = (uint32_t)vals.size();
+    vals.push_back(lt);
+    return (uint32_t)vals.size() - 1;
+  };
+  memset(blob, 0, kCtDwords * 4);
+  memset(&g, 0, sizeof(g));
+  g.zero_h = handle(GPK_LT_ZERO);
+  g.frag_h = handle(GPK_LT_FRAGMENT);
+  g.payload_h = handle(GPK_LT_PAYLOAD);
+  g.first_h = (first >= 0 && first < GPK_MAX_LAYER_TYPE) ? handle((int32_t)first) : 0;
+  uint8_t* ipp = (uint8_t*)(blob + kCtIpp);
+  for (int k = 0; k < 256; k++) ipp[k] = (uint8_t)handle(t.ipprotocol[k]);
+  uint32_t next_slot = kCtSlots;
+  auto hash_table = [&](const int32_t* tab, uint32_t& off, uint32_t& shift, uint32_t& mask, uint32_t& maxp,
+                        uint32_t& def) {
+    std::unordered_map<int32_t, uint32_t> count;
+    for (int k = 0; k < 65536; k++) count[tab[k]]++;
+    int32_t dv = tab[0];
+    for (auto& kv : count)
+      if (kv.second > count[dv]) dv = kv.first;
+    def = handle(dv);
+    uint32_t nex = 65536 - count[dv];
+    uint32_t bits = 3;
+    while ((1u << bits) < 2 * nex) bits++;
+    const uint32_t size = 1u << bits;
+    if (next_slot + size > (uint32_t)kCtDwords) {
+      ok = false;
+      return;
+    }
+    off = next_slot;
+    shift = 32 - bits;
+    mask = size - 1;
+    maxp = 0;
+    for (uint32_t i = 0; i < size; i++) blob[off + i] = 0xffffffffu;
+    for (uint32_t k = 0; k < 65536; k++) {
+      if (tab[k] == dv) continue;
+      uint32_t h = (k * 0x9E3779B1u) >> shift, d = 0;
+      while (blob[off + ((h + d) & mask)] != 0xffffffffu) d++;
+      blob[off + ((h + d) & mask)] = k | (handle(tab[k]) << 16);
+      if (d > maxp) maxp = d;
+    }
+    next_slot += size;
+  };
+  hash_table(t.ethertype, g.eth_off, g.eth_shift, g.eth_mask, g.eth_probe, g.eth_def);
+  if (ok) hash_table(t.tcp_port, g.tcp_off, g.tcp_shift, g.tcp_mask, g.tcp_probe, g.tcp_def);
+  if (ok) hash_table(t.udp_port, g.udp_off, g.udp_shift, g.udp_mask, g.udp_probe, g.udp_def);
+  if (!ok) return false;
+  uint8_t* kc = (uint8_t*)(blob + kCtKc);
+  for (size_t h = 0; h < vals.size(); h++) {
+    const int32_t lt = vals[h];
+    const uint32_t kind = (lt >= 0 && lt < GPK_MAX_LAYER_TYPE) ? t.dispatch[lt] : GPK_DEC_NONE;
+    kc[h] = (uint8_t)(kind | (host_code_of(lt) << 4));
+    blob[kCtVal + h] = (uint32_t)lt;
+  }
+  g.words = next_slot;
+  return true;
+}
+
+// Tables of parser p on the device (global copy always, compact copy when it
+// fits), and the table fields of P.
+int gpk_ctx_set_table_mode(gpk_ctx* c, int mode) {
+  if (!c || (mode != GPK_TABLES_AUTO && mode != GPK_TABLES_GLOBAL)) return GPK_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  c->force_global = mode == GPK_TABLES_GLOBAL;
+  c->uploaded_version = 0;  // rebuild on the next call
+  return GPK_OK;
+}
+
+static int upload(gpk_ctx* c, const gpk_parser* p, hipStream_t s, gpk::KParams& P) {
+  if (c->uploaded_version != p->version) {
+    static thread_local uint32_t blob[gpk::kCtDwords];
+    HIPCHK(hipMemcpyAsync(c->dtab, &p->tab, sizeof(gpk::DevTables), hipMemcpyHostToDevice, s));
+    c->compact = !c->force_global && build_compact(p->tab, p->first, blob, c->cg);
+    if (c->compact) HIPCHK(hipMemcpyAsync(c->dctab, blob, gpk::kCtDwords * 4, hipMemcpyHostToDevice, s));
+    HIPCHK(hipStreamSynchronize(s));  // p->tab and blob may change after we return
+    c->uploaded = p;
+    c->uploaded_version = p->version;
+  }
+  P.tab = c->dtab;
+  P.ctab = c->compact ? c->dctab : nullptr;
+  P.cg = c->cg;
+  P.first_kind = (p->first >= 0 && p->first < GPK_MAX_LAYER_TYPE) ? p->tab.dispatch[p->first] : GPK_DEC_NONE;
   return GPK_OK;
 }
 
@@ -240,7 +353,9 @@ static int make_params(gpk_ctx* c, const gpk_parser* p, const gpk_batch* b, cons
   P.err_args = o ? o->err_args : nullptr;
   P.flows = o && (p->outputs & GPK_OUT_FLOWS) ? o->flows : nullptr;
   P.layouts = o ? o->layouts : nullptr;
-  P.tab = c->dtab;
+  P.tab = nullptr;  // upload()
+  P.ctab = nullptr;
+  P.first_kind = GPK_DEC_NONE;
   P.first = p->first;
   P.outputs = p->outputs;
   P.ignore_unsupported = p->ignore_unsupported;
@@ -255,7 +370,7 @@ int gpk_decode_batch(gpk_ctx* c, const gpk_parser* p, const gpk_batch* b, const 
   hipStream_t s = (hipStream_t)stream;
   std::lock_guard<std::mutex> g(c->mu);
   HIPCHK(hipSetDevice(c->device));
-  rc = upload(c, p, s);
+  rc = upload(c, p, s, P);
   if (rc) return rc;
   HIPCHK(gpk_launch_decode(&P, (p->outputs & GPK_OUT_L4_CSUM) != 0, o->layouts != nullptr, s));
   return GPK_OK;
@@ -300,7 +415,7 @@ int gpk_decode_batch_host(gpk_ctx* c, const gpk_parser* p, const gpk_batch* hb, 
   gpk::KParams P;
   rc = make_params(c, p, &db, &dr, P);
   if (rc) return rc;
-  rc = upload(c, p, s);
+  rc = upload(c, p, s, P);
   if (rc) return rc;
   HIPCHK(gpk_launch_decode(&P, (p->outputs & GPK_OUT_L4_CSUM) != 0, dr.layouts != nullptr, s));
   HIPCHK(hipMemcpyAsync(ho->records, dr.records, n * sizeof(gpk_record), hipMemcpyDeviceToHost, s));
@@ -325,7 +440,7 @@ int gpk_decoded_list(gpk_ctx* c, const gpk_parser* p, const gpk_batch* b, uint64
   int64_t* dl = (int64_t*)c->dbuf;
   uint32_t* dn = (uint32_t*)((char*)c->dbuf + align_up(8 * (size_t)cap));
   hipStream_t s = c->stream;
-  rc = upload(c, p, s);
+  rc = upload(c, p, s, P);
   if (rc) return rc;
   HIPCHK(gpk_launch_list(&P, index, dl, cap, dn, s));
   uint32_t n = 0;
@@ -356,7 +471,7 @@ int gpk_decoded_list_host(gpk_ctx* c, const gpk_parser* p, const uint8_t* pkt, u
   gpk::KParams P;
   rc = make_params(c, p, &db, nullptr, P);
   if (rc) return rc;
-  rc = upload(c, p, s);
+  rc = upload(c, p, s, P);
   if (rc) return rc;
   HIPCHK(gpk_launch_list(&P, 0, (int64_t*)(d + o_list), cap, (uint32_t*)(d + o_n), s));
   uint32_t n = 0;

@@ -28,7 +28,13 @@ namespace gpk {
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 #ifndef GPK_NT_A
-#define GPK_NT_A 1
+#define GPK_NT_A 0  // A/B (r01): temporal phase-A loads keep lines shared with phase B in L2: C3 +30%
+#endif
+#ifndef GPK_WAVES_PER_EU
+#define GPK_WAVES_PER_EU 4  // <= 128 VGPRs: 4 waves/SIMD, the LDS limit too
+#endif
+#ifndef GPK_PB_G
+#define GPK_PB_G 4  // phase B: pending packets per wave pass
 #endif
 #ifndef GPK_NT_B
 #define GPK_NT_B 1
@@ -138,47 +144,64 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
   return readlane32(v, 0) + readlane32(v, 16) + readlane32(v, 32) + readlane32(v, 48);
 }
 
-template <bool kL4, bool kLayout>
-__global__ __launch_bounds__(kBlock) void decode_kernel(KParams P) {
-  const uint32_t tid = threadIdx.x;
-  const uint32_t lane = tid & 63;
-  const uint64_t i = (uint64_t)blockIdx.x * kBlock + tid;
-  const bool active = i < P.n;
+// Header window of one packet in registers: chunks [0, nchunk) of the
+// 16-byte-aligned run holding packet bytes [0, win).
+struct Win {
+  uint4 v[kWinChunks];
+};
 
-  uint64_t off = 0;
-  uint32_t cl = 0;
-  if (active) {
-    off = P.offsets[i];
-    cl = P.caplens[i];
+struct Idx {
+  uint64_t off;
+  uint32_t cl;
+};
+
+__device__ __forceinline__ Idx load_index(const KParams& P, uint64_t i) {
+  Idx x{0, 0};
+  if (i < P.n) {
+    x.off = P.offsets[i];
+    x.cl = P.caplens[i];
   }
-  // ---- header window -> LDS slot (coalesced 16-byte chunk loads) ----------
+  return x;
+}
+
+__device__ __forceinline__ uint32_t win_chunks(const Idx& x, bool active) {
+  const uint32_t m = (uint32_t)(x.off & 15);
+  uint32_t win = kWinChunks * 16 - m;
+  if (x.cl < win) win = x.cl;
+  return active ? (m + win + 15) >> 4 : 0;
+}
+
+__device__ __forceinline__ void load_window(const KParams& P, const Idx& x, uint32_t nchunk, Win& w) {
+  const uint8_t* src = P.data + (x.off & ~15ull);
+#pragma unroll
+  for (int k = 0; k < kWinChunks; k++)
+    if ((uint32_t)k < nchunk) w.v[k] = ld16(src + 16 * k);
+}
+
+__device__ __forceinline__ void store_window(uint32_t slot_dw, uint32_t nchunk, const Win& w) {
+#pragma unroll
+  for (int k = 0; k < kWinChunks; k++)
+    if ((uint32_t)k < nchunk) {
+      gpk_smem[slot_dw + 4 * k + 0] = w.v[k].x;
+      gpk_smem[slot_dw + 4 * k + 1] = w.v[k].y;
+      gpk_smem[slot_dw + 4 * k + 2] = w.v[k].z;
+      gpk_smem[slot_dw + 4 * k + 3] = w.v[k].w;
+    }
+}
+
+template <bool kL4, bool kLayout, class TT>
+__device__ __forceinline__ void decode_packet(const KParams& P, const TT& T, uint64_t i, bool active, uint64_t off,
+                                              uint32_t cl, uint32_t slot_dw, uint32_t lane) {
   const uint32_t m = (uint32_t)(off & 15);
-  const uint32_t slot_dw = tid * kSlotDw;
   uint32_t win = kWinChunks * 16 - m;
   if (cl < win) win = cl;
-  const uint32_t nchunk = active ? (m + win + 15) >> 4 : 0;
-  {
-    const uint8_t* src = P.data + (off - m);
-    uint4 v[kWinChunks];
-#pragma unroll
-    for (int k = 0; k < kWinChunks; k++)
-      if ((uint32_t)k < nchunk) v[k] = ld16(src + 16 * k);
-#pragma unroll
-    for (int k = 0; k < kWinChunks; k++)
-      if ((uint32_t)k < nchunk) {
-        gpk_smem[slot_dw + 4 * k + 0] = v[k].x;
-        gpk_smem[slot_dw + 4 * k + 1] = v[k].y;
-        gpk_smem[slot_dw + 4 * k + 2] = v[k].z;
-        gpk_smem[slot_dw + 4 * k + 3] = v[k].w;
-      }
-  }
   Rd r{P.data + off, slot_dw * 4 + m, win};
 
   // ---- Phase A: DecodeLayers ------------------------------------------------
   Parse q;
   q.init();
   Outcome s{0, 0, 0, 0};
-  if (active) s = run_parser<false>(P, r, cl, q);
+  if (active) s = run_parser<false>(P, T, r, cl, q);
 
   uint32_t st = (s.err & GPK_ST_ERR_MASK) | (s.trunc ? GPK_ST_TRUNCATED : 0u) |
                 ((q.nlayers > GPK_ST_NLAYERS_MASK ? GPK_ST_NLAYERS_MASK : q.nlayers) << GPK_ST_NLAYERS_SHIFT);
@@ -269,7 +292,7 @@ __global__ __launch_bounds__(kBlock) void decode_kernel(KParams P) {
     uint32_t extra = 0;
     uint64_t pend = __ballot(job);
     while (pend) {
-      constexpr int G = 4;
+      constexpr int G = GPK_PB_G;
       uint32_t jl[G];
       uint64_t s0[G], e0[G], b0[G];
       uint32_t pr[G];
@@ -366,6 +389,63 @@ __global__ __launch_bounds__(kBlock) void decode_kernel(KParams P) {
   }
 }
 
+// Persistent, software-pipelined over tiles of kBlock packets: block b takes
+// tiles b, b+grid, b+2*grid, ... (grid = resident blocks, gpk_launch_decode).
+// While tile t is decoded, the header windows of tile t+grid are in flight
+// (registers) and the offsets/caplens of tile t+2*grid too, so the global
+// load latency of the read-once header bytes is hidden behind decode work.
+// The LDS slot is lane-private: no barrier between tiles.
+template <bool kL4, bool kLayout, class TT>
+__device__ __forceinline__ void decode_tiles(const KParams& P, const TT& T) {
+  const uint32_t tid = threadIdx.x;
+  const uint32_t lane = tid & 63;
+  const uint32_t slot_dw = tid * kSlotDw;
+  const uint64_t ntiles = (P.n + kBlock - 1) / kBlock;
+  const uint64_t stride = gridDim.x;
+  uint64_t t = blockIdx.x;
+  if (t >= ntiles) return;  // uniform over the block
+
+  uint64_t i = t * kBlock + tid;
+  Idx cur = load_index(P, i);
+  uint32_t nc = win_chunks(cur, i < P.n);
+  Win w;
+  load_window(P, cur, nc, w);
+  Idx nxt = load_index(P, i + stride * kBlock);
+  for (;;) {
+    store_window(slot_dw, nc, w);
+    const uint64_t i1 = i + stride * kBlock;
+    const uint32_t nc1 = win_chunks(nxt, i1 < P.n);
+    load_window(P, nxt, nc1, w);                         // tile t+grid, in flight
+    const Idx nn = load_index(P, i1 + stride * kBlock);  // tile t+2*grid
+    decode_packet<kL4, kLayout>(P, T, i, i < P.n, cur.off, cur.cl, slot_dw, lane);
+    t += stride;
+    if (t >= ntiles) break;
+    i = i1;
+    cur = nxt;
+    nc = nc1;
+    nxt = nn;
+  }
+}
+
+// kCompact: the parser's lookup tables are copied into LDS once per block
+// (after the header-window slots) and every NextLayerType lookup is an LDS
+// read; otherwise they are read from the global DevTables. Either way the
+// only vector-memory traffic of the decode is the packet bytes themselves,
+// so waiting on a lookup never waits on the next tile's prefetch.
+template <bool kL4, bool kLayout, bool kCompact>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GPK_WAVES_PER_EU, 8))) void decode_kernel(
+    KParams P) {
+  if ((uint64_t)blockIdx.x * kBlock >= P.n) return;  // uniform over the block
+  if (kCompact) {
+    const uint32_t base = kBlock * kSlotDw;
+    for (uint32_t w = threadIdx.x; w < P.cg.words; w += kBlock) gpk_smem[base + w] = P.ctab[w];
+    __syncthreads();
+    decode_tiles<kL4, kLayout>(P, LTab{P.cg, base});
+  } else {
+    decode_tiles<kL4, kLayout>(P, GTab{P.tab});
+  }
+}
+
 // Full decoded list of one packet (lists longer than the 16 inline codes).
 __global__ void list_kernel(KParams P, uint64_t index, int64_t* out, uint32_t cap, uint32_t* out_n) {
   if (threadIdx.x != 0) return;
@@ -373,26 +453,58 @@ __global__ void list_kernel(KParams P, uint64_t index, int64_t* out, uint32_t ca
   uint32_t cl = P.caplens[index];
   Rd r{P.data + off, 0, 0};  // no LDS window: every byte from global memory
   Parse q;
-  run_parser<true>(P, r, cl, q, out, cap);
+  run_parser<true>(P, GTab{P.tab}, r, cl, q, out, cap);
   *out_n = q.nlayers;
 }
 
 }  // namespace gpk
 
-extern "C" hipError_t gpk_launch_decode(const gpk::KParams* P, int with_l4, int with_layout, hipStream_t stream) {
+namespace {
+
+template <bool kL4, bool kLayout, bool kCompact>
+hipError_t launch(const gpk::KParams* P, hipStream_t stream) {
   using namespace gpk;
-  if (P->n == 0) return hipSuccess;
-  dim3 grid((unsigned)((P->n + kBlock - 1) / kBlock));
-  dim3 block(kBlock);
-  if (with_l4 && with_layout)
-    hipLaunchKernelGGL((decode_kernel<true, true>), grid, block, kLdsBytes, stream, *P);
-  else if (with_l4)
-    hipLaunchKernelGGL((decode_kernel<true, false>), grid, block, kLdsBytes, stream, *P);
-  else if (with_layout)
-    hipLaunchKernelGGL((decode_kernel<false, true>), grid, block, kLdsBytes, stream, *P);
-  else
-    hipLaunchKernelGGL((decode_kernel<false, false>), grid, block, kLdsBytes, stream, *P);
+  constexpr int lds = kCompact ? kLdsBytes + kCtDwords * 4 : kLdsBytes;
+  // Resident blocks per CU for this specialisation (cached per device).
+  static int cached_bpc[64], cached_cus[64];
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
+  if (!cached_bpc[dev]) {
+    int bpc = 0, cus = 0;
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, decode_kernel<kL4, kLayout, kCompact>, kBlock, lds);
+    if (e != hipSuccess) return e;
+    e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (e != hipSuccess) return e;
+    cached_cus[dev] = cus > 0 ? cus : 1;
+    cached_bpc[dev] = bpc > 0 ? bpc : 1;
+  }
+  // 8 rounds of resident blocks: if the occupancy figure is one block per CU
+  // high, the static tile schedule loses ~3% instead of running a second
+  // generation of late blocks; each block still pipelines >= 8 tiles.
+  const uint64_t ntiles = (P->n + kBlock - 1) / kBlock;
+  uint64_t grid = (uint64_t)cached_cus[dev] * cached_bpc[dev] * 8;
+  if (ntiles < grid * 8) grid = (ntiles + 7) / 8;
+  if (grid < 1) grid = 1;
+  hipLaunchKernelGGL((decode_kernel<kL4, kLayout, kCompact>), dim3((unsigned)grid), dim3(kBlock), lds, stream, *P);
   return hipGetLastError();
+}
+
+template <bool kCompact>
+hipError_t launch_outputs(const gpk::KParams* P, int with_l4, int with_layout, hipStream_t stream) {
+  if (with_l4 && with_layout) return launch<true, true, kCompact>(P, stream);
+  if (with_l4) return launch<true, false, kCompact>(P, stream);
+  if (with_layout) return launch<false, true, kCompact>(P, stream);
+  return launch<false, false, kCompact>(P, stream);
+}
+
+}  // namespace
+
+extern "C" hipError_t gpk_launch_decode(const gpk::KParams* P, int with_l4, int with_layout, hipStream_t stream) {
+  if (P->n == 0) return hipSuccess;
+  return P->ctab ? launch_outputs<true>(P, with_l4, with_layout, stream)
+                 : launch_outputs<false>(P, with_l4, with_layout, stream);
 }
 
 extern "C" hipError_t gpk_launch_list(const gpk::KParams* P, uint64_t index, int64_t* out, uint32_t cap,

@@ -79,6 +79,10 @@ class Context:
             _lib._lib.gpk_ctx_destroy(h)
             self.h = None
 
+    def set_table_mode(self, mode):
+        """_lib.TABLES_AUTO (compact LDS tables when they fit) or TABLES_GLOBAL."""
+        check(lib().gpk_ctx_set_table_mode(self.h, int(mode)))
+
     def decode_host(self, parser, data, offsets, caplens, layouts=False):
         """Host batch in, host results out (copies HtoD, decodes, copies DtoH)."""
         data = np.ascontiguousarray(data, dtype=np.uint8)

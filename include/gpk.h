@@ -227,6 +227,15 @@ int gpk_parser_set_udp_port(gpk_parser* p, uint32_t port, int32_t layer_type);
 typedef struct gpk_ctx gpk_ctx;
 int gpk_ctx_create(gpk_ctx** out, int device_ordinal);
 int gpk_ctx_destroy(gpk_ctx* ctx);
+/* Where the kernels read the parser's next-layer tables (EthernetType /
+ * IPProtocol / TCPPort / UDPPort -> LayerType, layers/enums.go:294-353,
+ * layers/ports.go:54-183). AUTO (default): a compact copy in LDS whenever the
+ * tables fit (a few dozen non-default entries each, as the defaults are),
+ * else the full tables in device memory. GLOBAL: always the full tables.
+ * Results are identical; GLOBAL exists for testing and diagnosis. */
+#define GPK_TABLES_AUTO 0
+#define GPK_TABLES_GLOBAL 1
+int gpk_ctx_set_table_mode(gpk_ctx* ctx, int mode);
 
 /* A packed, offset-indexed packet batch. Packet i is data[offsets[i] ..
  * offsets[i]+caplens[i]). In gpk_decode_batch every pointer is DEVICE memory.

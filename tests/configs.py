@@ -20,6 +20,13 @@ CONFIGS = {
     "overrides": dict(first=17, decoders=[ETH, D1Q, IP4, IP6, TCP, UDP, PAY],
                       ethertype={0x1234: 20}, tcp_port={80: 1234, 443: 2}, udp_port={53: 2},
                       ipprotocol={200: 44}),
+    # 100 extra TCP ports: the compact LDS hash tables with collisions/probing
+    "many_ports": dict(first=17, decoders=[ETH, IP4, IP6, TCP, UDP, PAY],
+                       tcp_port={p: (2 if p % 3 else 1000 + p % 7) for p in range(1, 101)},
+                       udp_port={p * 97 % 65536: 2 for p in range(1, 40)}),
+    # 200 distinct LayerTypes: does not fit the compact tables, global tables used
+    "tables_overflow": dict(first=17, decoders=[ETH, IP4, TCP, UDP, PAY],
+                            tcp_port={p: 3000 + p for p in range(1, 201)}),
 }
 
 

@@ -200,3 +200,36 @@ def test_offsets_beyond_2_and_4_GiB(gpu_ctx, base):
     assert_same(dev, ref, "base %d" % base)
     del data
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("cfg_name", ["statsassembly", "overrides", "many_ports", "tables_overflow", "raw_ip6",
+                                      "first_unregistered"])
+def test_global_table_mode(gpu_ctx, cfg_name):
+    """GPK_TABLES_GLOBAL (full tables in device memory) gives the same results
+    as the oracle, like the default compact LDS tables do."""
+    from gopacket_amd import _lib
+    gpu_ctx.set_table_mode(_lib.TABLES_GLOBAL)
+    try:
+        packets = golden_packets() + pktutil.fuzz_packets(zlib.crc32(cfg_name.encode()) % 1000 + 5, 20000)
+        dev, ref = run_both(gpu_ctx, CONFIGS[cfg_name], packets)
+        assert_same(dev, ref, cfg_name + " global tables")
+    finally:
+        gpu_ctx.set_table_mode(_lib.TABLES_AUTO)
+
+
+def test_port_traffic_hits_table_entries(gpu_ctx):
+    """Packets whose ports/ethertypes are exactly the keys stored in the
+    compact hash tables (every probe depth) decode like the oracle."""
+    import struct
+    cfg = CONFIGS["many_ports"]
+    pk = []
+    for port in list(cfg["tcp_port"]) + [0, 65535, 65534, 101, 4096]:
+        ip = struct.pack(">BBHHHBBH4s4s", 0x45, 0, 40, 0, 0, 64, 6, 0, b"\x01" * 4, b"\x02" * 4)
+        for sp, dp in ((port, 9), (9, port), (port, port)):
+            tcp = struct.pack(">HHIIBBHHH", sp, dp, 1, 2, 0x50, 0x18, 100, 0, 0)
+            pk.append(b"\x02" * 12 + b"\x08\x00" + ip + tcp + b"xyz")
+    for port in list(cfg["udp_port"]) + [53, 4789, 65535, 0]:
+        ip = struct.pack(">BBHHHBBH4s4s", 0x45, 0, 31, 0, 0, 64, 17, 0, b"\x01" * 4, b"\x02" * 4)
+        pk.append(b"\x02" * 12 + b"\x08\x00" + ip + struct.pack(">HHHH", port, 7, 11, 0) + b"abc")
+    dev, ref = run_both(gpu_ctx, cfg, pk)
+    assert_same(dev, ref, "many_ports keys")

@@ -7,8 +7,13 @@ TAG=$1; CFGS=$2; shift 2
 OUT=gpurun_out/ab_$TAG
 mkdir -p $OUT
 for V in "$@"; do
-  if [ "$V" = base ]; then unset GPK_LIB_VARIANT; else export GPK_LIB_VARIANT=$V; fi
-  timeout -k 10 300 python3 bench.py --no-cpu-baseline --no-parity --configs $CFGS --steps 10 --warmup 2 \
+  EXTRA=""
+  case $V in
+    base) unset GPK_LIB_VARIANT ;;
+    global) unset GPK_LIB_VARIANT; EXTRA="--tables global" ;;
+    *) export GPK_LIB_VARIANT=$V ;;
+  esac
+  timeout -k 10 300 python3 bench.py $EXTRA --no-cpu-baseline --no-parity --configs $CFGS --steps 10 --warmup 2 \
     > $OUT/$V.json 2> $OUT/$V.err || { echo "variant $V failed"; exit 1; }
   python3 - "$OUT/$V.json" "$V" <<'PY'
 import json, sys
