@@ -174,14 +174,15 @@ def cpu_baseline(name, seconds=12.0, batch=262144):
                        % (reps, batch, name.upper(), len(data) / 1e6, el, cores))
 
 
-def load_traffic(name):
+def load_traffic(name, n):
+    """HBM bytes per launch of the decode kernel from the committed PMC
+    profile (profiles/hbm_traffic.json, tools/make_profiles.py): measured
+    bytes per packet x packets per launch. None if not profiled."""
     path = os.path.join(ROOT, "profiles", "hbm_traffic.json")
-    if not os.path.exists(path):
-        return None
     try:
-        t = json.load(open(path)).get(name)
-        return t
-    except Exception:
+        t = json.load(open(path))[name]
+        return round((t["fetch_bytes_per_packet"] + t["write_bytes_per_packet"]) * n)
+    except (OSError, KeyError, ValueError):
         return None
 
 
@@ -229,8 +230,8 @@ def main():
                        "payload_bytes_per_gpu": r["payload_bytes"], "parallelism": "shard%d" % world,
                        "parser": "+".join(CONFIGS[head]["decoders"])},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": load_traffic(head),
-                         "kernel": "gpk::decode_kernel<true,false>", "kernel_ms": round(r["kernel_ms"], 4),
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": load_traffic(head, r["n"]),
+                         "kernel": "gpk::decode_kernel<true,false,true>", "traffic_unit": "bytes per launch", "kernel_ms": round(r["kernel_ms"], 4),
                          "algo_bytes_per_launch": r["algo_bytes"],
                          "probe_read_GBps": r["probe_gbs"] and round(r["probe_gbs"], 1)},
             "parity": r["parity"],

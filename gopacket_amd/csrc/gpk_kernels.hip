@@ -36,6 +36,15 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 #ifndef GPK_PB_G
 #define GPK_PB_G 4  // phase B: pending packets per wave pass
 #endif
+#ifndef GPK_LINE_SPLIT
+#define GPK_LINE_SPLIT 0  // 1: phase B on whole lines, partial lines per lane (A/B r01: no gain)
+#endif
+#ifndef GPK_PREFETCH
+#define GPK_PREFETCH 0  // 1: next tile's windows in flight (persistent only; A/B r01: no gain)
+#endif
+#ifndef GPK_PERSISTENT
+#define GPK_PERSISTENT 0  // 1: blocks loop over tiles (A/B r01: +50 VGPRs from hoisting, no gain)
+#endif
 #ifndef GPK_NT_B
 #define GPK_NT_B 1
 #endif
@@ -250,10 +259,48 @@ __device__ __forceinline__ void decode_packet(const KParams& P, const TT& T, uin
           if (ra != fa) edge += chunk_sum(ld16(P.data + (ra & ~15ull)), ra & ~15ull, ra, re, par);
           if (re != fe) edge += chunk_sum(ld16(P.data + fe), fe, ra, re, par);
         }
+#if GPK_LINE_SPLIT
+        // Phase B gets whole 128-byte lines only, [la, lb). The full chunks
+        // of the segment's first and last partial lines, [fa, la) and
+        // [lb, fe), are summed here, right after the header window loads
+        // touched those lines (the window's last line; the last line is
+        // the next packet's first line, which its lane loaded with this
+        // tile's windows) so they are still cached: every line of the
+        // packet is fetched from HBM once.
+        uint64_t la = fa, lb = fa;  // fa >= fe: no full chunk at all
+        if (fa < fe) {
+          la = (fa + 127) & ~127ull;
+          lb = fe & ~127ull;
+          if (la > fe) la = fe;
+          if (lb < la) lb = la;
+        }
+        {
+          uint4 hv[15];
+#pragma unroll
+          for (int k = 0; k < 7; k++)
+            if (fa + 16 * k < la) hv[k] = ld16(P.data + fa + 16 * k);
+#pragma unroll
+          for (int k = 0; k < 8; k++)
+            if (lb + 16 * k < fe) hv[7 + k] = ld16(P.data + lb + 16 * k);
+          uint32_t E2 = 0, O2 = 0;
+#pragma unroll
+          for (int k = 0; k < 7; k++)
+            if (fa + 16 * k < la) chunk_eo(hv[k], E2, O2);
+#pragma unroll
+          for (int k = 0; k < 8; k++)
+            if (lb + 16 * k < fe) chunk_eo(hv[7 + k], E2, O2);
+          edge += par ? (O2 << 8) + E2 : (E2 << 8) + O2;
+        }
+        jsum = init + part + edge;
+        job = la < lb;
+        ja = la;
+        je = lb;
+#else
         jsum = init + part + edge;
         job = fa < fe;
         ja = fa;
         je = fe;
+#endif
         jpar = par;
         if (!job) l4c = fold(jsum - jexist);
       }
@@ -291,54 +338,48 @@ __device__ __forceinline__ void decode_packet(const KParams& P, const TT& T, uin
   if (kL4) {
     uint32_t extra = 0;
     uint64_t pend = __ballot(job);
+    const uint32_t vo = lane * 16;
     while (pend) {
       constexpr int G = GPK_PB_G;
       uint32_t jl[G];
-      uint64_t s0[G], e0[G], b0[G];
+      uint32_t len[G];
+      __amdgpu_buffer_rsrc_t rs[G];
       uint32_t pr[G];
 #pragma unroll
       for (int g = 0; g < G; g++) {
         jl[g] = 64;
-        s0[g] = e0[g] = b0[g] = 0;  // empty slot: every load reads data[0..16), discarded
+        len[g] = 0;  // empty slot: a zero-record descriptor, every load returns 0
         pr[g] = 0;
+        uint64_t b0 = 0;
         if (pend) {
           uint32_t j = (uint32_t)__builtin_ctzll(pend);
           pend &= pend - 1;
           jl[g] = j;
-          s0[g] = readlane64(ja, j);
-          e0[g] = readlane64(je, j);
+          b0 = readlane64(ja, j);
+          len[g] = (uint32_t)(readlane64(je, j) - b0);
           pr[g] = readlane32(jpar, j);
-          b0[g] = s0[g];
         }
+        // [b0, b0+len) as a raw buffer: loads past its end return zeros
+        // (hardware range check), so no lane needs a predicate or a mask
+        rs[g] = __builtin_amdgcn_make_buffer_rsrc((void*)(P.data + b0), 0, len[g], 0x00020000);
       }
       uint32_t E[G], O[G];
 #pragma unroll
       for (int g = 0; g < G; g++) E[g] = O[g] = 0;
-      for (uint64_t rr = 0;; rr += 2048) {
-        uint4 v[G][2];
-        bool ok[G][2];
+      uint32_t maxlen = 0;
+#pragma unroll
+      for (int g = 0; g < G; g++) maxlen = len[g] > maxlen ? len[g] : maxlen;
+      for (uint32_t rr = 0; rr < maxlen; rr += 2048) {
+        u32x4 v[G][2];
 #pragma unroll
         for (int g = 0; g < G; g++)
 #pragma unroll
-          for (int h = 0; h < 2; h++) {
-            // every lane loads (a lane past the end re-reads the packet's
-            // first chunk and discards it): no exec-mask branches
-            uint64_t A = b0[g] + rr + h * 1024 + lane * 16;
-            ok[g][h] = A < e0[g];
-            v[g][h] = ld16b(P.data + (ok[g][h] ? A : b0[g]));
-          }
-        bool more = false;
+          for (int h = 0; h < 2; h++)
+            v[g][h] = __builtin_amdgcn_raw_buffer_load_b128(rs[g], vo + h * 1024, rr, GPK_NT_B ? 2 : 0);
 #pragma unroll
-        for (int g = 0; g < G; g++) {
+        for (int g = 0; g < G; g++)
 #pragma unroll
-          for (int h = 0; h < 2; h++) {
-            uint4 x = v[g][h];
-            if (!ok[g][h]) x = make_uint4(0, 0, 0, 0);
-            chunk_eo(x, E[g], O[g]);
-          }
-          more |= b0[g] + rr + 2048 < e0[g];
-        }
-        if (!more) break;
+          for (int h = 0; h < 2; h++) chunk_eo(make_uint4(v[g][h].x, v[g][h].y, v[g][h].z, v[g][h].w), E[g], O[g]);
       }
 #pragma unroll
       for (int g = 0; g < G; g++) {
@@ -401,11 +442,12 @@ __device__ __forceinline__ void decode_tiles(const KParams& P, const TT& T) {
   const uint32_t lane = tid & 63;
   const uint32_t slot_dw = tid * kSlotDw;
   const uint64_t ntiles = (P.n + kBlock - 1) / kBlock;
-  const uint64_t stride = gridDim.x;
+  [[maybe_unused]] const uint64_t stride = gridDim.x;
   uint64_t t = blockIdx.x;
   if (t >= ntiles) return;  // uniform over the block
 
   uint64_t i = t * kBlock + tid;
+#if GPK_PREFETCH
   Idx cur = load_index(P, i);
   uint32_t nc = win_chunks(cur, i < P.n);
   Win w;
@@ -425,6 +467,30 @@ __device__ __forceinline__ void decode_tiles(const KParams& P, const TT& T) {
     nc = nc1;
     nxt = nn;
   }
+#elif !GPK_PERSISTENT
+  {  // one tile per block
+    const Idx cur = load_index(P, i);
+    const uint32_t nc = win_chunks(cur, i < P.n);
+    Win w;
+    load_window(P, cur, nc, w);
+    store_window(slot_dw, nc, w);
+    decode_packet<kL4, kLayout>(P, T, i, i < P.n, cur.off, cur.cl, slot_dw, lane);
+  }
+#else
+  Idx nxt = load_index(P, i);
+  for (;;) {
+    const Idx cur = nxt;
+    const uint32_t nc = win_chunks(cur, i < P.n);
+    Win w;
+    load_window(P, cur, nc, w);
+    nxt = load_index(P, i + stride * kBlock);  // next tile's offsets/caplens
+    store_window(slot_dw, nc, w);
+    decode_packet<kL4, kLayout>(P, T, i, i < P.n, cur.off, cur.cl, slot_dw, lane);
+    t += stride;
+    if (t >= ntiles) break;
+    i += stride * kBlock;
+  }
+#endif
 }
 
 // kCompact: the parser's lookup tables are copied into LDS once per block
@@ -486,6 +552,7 @@ hipError_t launch(const gpk::KParams* P, hipStream_t stream) {
   const uint64_t ntiles = (P->n + kBlock - 1) / kBlock;
   uint64_t grid = (uint64_t)cached_cus[dev] * cached_bpc[dev] * 8;
   if (ntiles < grid * 8) grid = (ntiles + 7) / 8;
+  if (!GPK_PERSISTENT && !GPK_PREFETCH) grid = ntiles;
   if (grid < 1) grid = 1;
   hipLaunchKernelGGL((decode_kernel<kL4, kLayout, kCompact>), dim3((unsigned)grid), dim3(kBlock), lds, stream, *P);
   return hipGetLastError();
