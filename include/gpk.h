@@ -12,10 +12,13 @@
  *                                          parser.go:222-233, AddDecodingLayer :200,
  *                                          SetDecodingLayerContainer :238-241,
  *                                          DecodingLayerParserOptions :337-351
- *   gpk_tables_default / gpk_tables_set_*  EthernetType/IPProtocol metadata tables
- *                                          layers/enums.go:294-353, enums_generated.go:76-156;
- *                                          RegisterTCPPortLayerType / RegisterUDPPortLayerType
- *                                          layers/ports.go:99-104,178-183
+ *   gpk_parser_set_ethertype / _ipprotocol EthernetType/IPProtocol metadata tables
+ *                                          layers/enums.go:294-353, enums_generated.go:76-156
+ *   gpk_parser_set_tcp_port / _udp_port    RegisterTCPPortLayerType / RegisterUDPPortLayerType
+ *                                          layers/ports.go:99-104,178-183 (defaults: the port
+ *                                          switches :54-93,:121-172 + init overrides)
+ *   gpk_ctx_create / gpk_ctx_destroy       one GPU (there is no reference counterpart: a
+ *                                          DecodingLayerParser is per goroutine, doc.go:211-228)
  *   gpk_decode_batch                       DecodingLayerParser.DecodeLayers (parser.go:303-317)
  *                                          applied to every packet of a batch, plus, per packet,
  *                                          IPv4.VerifyChecksum (layers/ip4.go:323-332),

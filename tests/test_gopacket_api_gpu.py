@@ -1,0 +1,131 @@
+"""The gopacket-shaped Python API (gopacket_amd.gopacket / .layers) on the GPU.
+
+These read like the reference's own DecodingLayerParser tests: build a
+parser from layer structs, DecodeLayers a packet, check `decoded`, the error,
+Truncated, the layer fields, VerifyChecksum and the flows. Every call goes
+through the HIP kernels (C ABI); expectations restate the cited reference
+tests.
+"""
+import struct
+
+import numpy as np
+import pytest
+
+import pktutil
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture()
+def gp(gpu_ctx):
+    from gopacket_amd import gopacket, layers
+    return gopacket, layers, gpu_ctx
+
+
+def _parser(gp, first, *decs):
+    gopacket, layers, ctx = gp
+    return gopacket.DecodingLayerParser(first, *decs, ctx=ctx)
+
+
+# layers/decode_test.go:386-492 TestDecodeSimpleTCPPacket through the parser
+# (the DecodingLayerParser form of decode_test.go:192-205)
+def test_decode_layers_simple_tcp(gp):
+    gopacket, L, _ = gp
+    eth, ip4, tcp, pay = L.Ethernet(), L.IPv4(), L.TCP(), gopacket.Payload()
+    p = _parser(gp, L.LayerTypeEthernet, eth, ip4, tcp, pay)
+    decoded = [L.LayerTypeDot1Q]  # truncated by DecodeLayers
+    pkt = pktutil.golden_bytes("simple_tcp")
+    err = p.DecodeLayers(pkt, decoded)
+    assert err is None and not p.Truncated
+    assert decoded == [L.LayerTypeEthernet, L.LayerTypeIPv4, L.LayerTypeTCP, gopacket.LayerTypePayload]
+    assert eth.SrcMAC == bytes.fromhex("bc305be8d349") and eth.EthernetType == 0x0800
+    assert (ip4.Length, ip4.Id, ip4.TTL, ip4.Protocol) == (420, 14815, 64, 6)
+    assert (tcp.SrcPort, tcp.DstPort, tcp.Seq) == (50679, 80, 0xc57e0e48)
+    assert pay.Payload() == pkt[66:]
+    e, res = ip4.VerifyChecksum()
+    assert e is None and res.Valid and res.Correct == res.Actual == 0x555A
+    e, res = tcp.VerifyChecksum()
+    assert e is None and res.Valid and res.Correct == 0x9a8f
+    assert tcp.TransportFlow().String() == "50679->80"
+    assert ip4.NetworkFlow().FastHash() == ip4.NetworkFlow().Reverse().FastHash()
+
+
+# layers/decode_test.go:549-572 TestDecodeVLANPacket
+def test_decode_layers_vlan(gp):
+    gopacket, L, _ = gp
+    eth, d1q, ip4, tcp, pay = L.Ethernet(), L.Dot1Q(), L.IPv4(), L.TCP(), gopacket.Payload()
+    p = _parser(gp, L.LayerTypeEthernet, eth, d1q, ip4, tcp, pay)
+    decoded = []
+    err = p.DecodeLayers(pktutil.golden_bytes("vlan_tcp"), decoded)
+    assert err is None
+    assert decoded[:4] == [L.LayerTypeEthernet, L.LayerTypeDot1Q, L.LayerTypeIPv4, L.LayerTypeTCP]
+    assert d1q.Type == 0x0800
+
+
+# layers/udp_test.go:39-98 TestUDPPacketDNS: DNS has no decoder -> UnsupportedLayerType
+def test_unsupported_layer_type_error(gp):
+    gopacket, L, _ = gp
+    p = _parser(gp, L.LayerTypeEthernet, L.Ethernet(), L.IPv4(), L.UDP(), gopacket.Payload())
+    decoded = []
+    err = p.DecodeLayers(pktutil.golden_bytes("udp_dns"), decoded)
+    assert isinstance(err, gopacket.UnsupportedLayerType)
+    assert err.Error() == "No decoder for layer type DNS"
+    assert decoded == [L.LayerTypeEthernet, L.LayerTypeIPv4, L.LayerTypeUDP]
+    p.IgnoreUnsupported = True
+    assert p.DecodeLayers(pktutil.golden_bytes("udp_dns"), decoded) is None
+
+
+# layers/decode_test.go:1018-1031 TestDecodeUDPPacketTooSmall: truncated, no error
+def test_truncated_flag(gp):
+    gopacket, L, _ = gp
+    p = _parser(gp, L.LayerTypeEthernet, L.Ethernet(), L.Dot1Q(), L.IPv4(), L.UDP(), gopacket.Payload())
+    decoded = []
+    assert p.DecodeLayers(pktutil.golden_bytes("udp_too_small"), decoded) is None
+    assert p.Truncated
+
+
+# layers/tcp_test.go:159-188 TestMPTCPInvalidLengthAndSubtype: decoder error text
+def test_decoder_error_text(gp):
+    gopacket, L, _ = gp
+    p = _parser(gp, L.LayerTypeIPv4, L.IPv4(), L.TCP(), gopacket.Payload())
+    decoded = []
+    err = p.DecodeLayers(pktutil.golden_bytes("mptcp_bad_len_sll2")[20:], decoded)
+    assert err is not None and err.Error().endswith("MPTCP bad option length 0")
+    assert decoded == [L.LayerTypeIPv4]
+
+
+# parser.go:329-333: a short MPTCP option panics in Go; DecodeLayers returns
+# "panic: runtime error: ..." unless IgnorePanic, which re-raises
+def test_mptcp_panic_error(gp):
+    gopacket, L, _ = gp
+    ip = struct.pack(">BBHHHBBH4s4s", 0x45, 0, 20 + 24, 0, 0, 64, 6, 0, b"\x01" * 4, b"\x02" * 4)
+    # MPTCP ADD_ADDR (subtype 4) claiming 5 bytes in a 4-byte option area: data[4] (tcp.go:414-455)
+    tcp = struct.pack(">HHIIBBHHH", 1, 2, 0, 0, 0x60, 0x10, 0, 0, 0) + bytes([30, 5, 0x40, 0])
+    p = _parser(gp, L.LayerTypeIPv4, L.IPv4(), L.TCP(), gopacket.Payload())
+    decoded = []
+    err = p.DecodeLayers(ip + tcp, decoded)
+    assert err is not None and err.Error() == "panic: runtime error: index out of range [4] with length 4"
+    p.IgnorePanic = True
+    with pytest.raises(gopacket.GoPanic):
+        p.DecodeLayers(ip + tcp, decoded)
+
+
+# pcap/pcap_test.go:50-117 + the doc.go:211-228 batch pattern: DecodeBatch over
+# test_ethernet.pcap, per-packet views agree with per-packet DecodeLayers
+def test_decode_batch_matches_decode_layers(gp):
+    gopacket, L, _ = gp
+    _, pkts = pktutil.read_pcap(pktutil.GOLDEN + "/test_ethernet.pcap")
+    eth, ip4, tcp, pay = L.Ethernet(), L.IPv4(), L.TCP(), gopacket.Payload()
+    p = _parser(gp, L.LayerTypeEthernet, eth, ip4, tcp, pay)
+    res = p.DecodeBatch(gopacket.PacketBatch.from_packets(pkts), layouts=True)
+    assert len(res) == 10
+    for i, pkt in enumerate(pkts):
+        d1, d2 = [], []
+        assert res.Hydrate(i, d1) is None
+        h = res.FlowHashes(i)
+        assert p.DecodeLayers(pkt, d2) is None
+        assert d1 == d2 and d1[:3] == [L.LayerTypeEthernet, L.LayerTypeIPv4, L.LayerTypeTCP]
+        assert res.IPv4Checksum(i)[0] and res.L4Checksum(i)[0]
+        assert h == (eth.LinkFlow().FastHash(), ip4.NetworkFlow().FastHash(), tcp.TransportFlow().FastHash())
+    assert res.FlowHashes(0) == res.FlowHashes(1)  # opposite directions, symmetric hash
+    assert np.count_nonzero([gopacket.LayerTypePayload in res.Decoded(i) for i in range(10)]) == 3
