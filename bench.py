@@ -174,6 +174,41 @@ def cpu_baseline(name, seconds=12.0, batch=262144):
                        % (reps, batch, name.upper(), len(data) / 1e6, el, cores))
 
 
+def pcie_inclusive(name, ctx, n=4 * 2**20, reps=5):
+    """gpk_decode_batch_host over a pinned host batch: HtoD copy of bytes and
+    index, decode, DtoH copy of the results, synchronous. The rate a host
+    source (pcap reader, AF_PACKET ring) sees; never the headline value."""
+    import ctypes
+    from gopacket_amd import _lib, engine
+    cfg = CONFIGS[name]
+    L, S = _lib.lib(), _lib.synth_lib()
+    kinds = [engine.DECODER_KINDS[d] for d in cfg["decoders"]]
+    parser = engine.ParserConfig(17, kinds, outputs=cfg["outputs"])
+    nbytes = S.gpk_synth_batch_host(cfg["synth"], 0, n, None, None, None)
+    bufs = []
+
+    def pinned(sz):
+        p = ctypes.c_void_p()
+        _lib.check(L.gpk_host_alloc(ctypes.byref(p), sz))
+        bufs.append(p)
+        return p.value
+
+    data, off, cap = pinned(nbytes + 16), pinned(8 * n), pinned(4 * n)
+    rec, err, fl = pinned(16 * n), pinned(8 * n), pinned(24 * n)
+    S.gpk_synth_batch_host(cfg["synth"], 0, n, data, off, cap)
+    b = _lib.Batch(data, off, cap, n, nbytes)
+    r = _lib.Results(rec, err, fl if cfg["outputs"] & 4 else None, None)
+    _lib.check(L.gpk_decode_batch_host(ctx.h, parser.h, ctypes.byref(b), ctypes.byref(r)))
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        _lib.check(L.gpk_decode_batch_host(ctx.h, parser.h, ctypes.byref(b), ctypes.byref(r)))
+    el = (time.perf_counter() - t0) / reps
+    for p in bufs:
+        L.gpk_host_free(p)
+    return dict(value=round(n / el / 1e6, 2), unit="Mpkts/s", GBps=round((nbytes + 12 * n) / el / 1e9, 2),
+                packets=n, note="gpk_decode_batch_host from pinned memory: HtoD + decode + DtoH")
+
+
 def load_traffic(name, n):
     """HBM bytes per launch of the decode kernel from the committed PMC
     profile (profiles/hbm_traffic.json, tools/make_profiles.py): measured
@@ -197,6 +232,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--no-probe", action="store_true", help="skip the streaming-read reference kernel")
+    ap.add_argument("--pcie", action="store_true", help="also time the host-buffer path (PCIe-inclusive)")
     ap.add_argument("--tables", default="auto", choices=["auto", "global"],
                     help="next-layer tables: compact LDS copy (auto) or device-memory tables (global)")
     args = ap.parse_args()
@@ -246,6 +282,8 @@ def main():
                 "kernel_ms": round(s["kernel_ms"], 4), "achieved_GBps": round(ach, 1),
                 "frac": round(ach / HBM_PEAK_GBS, 4), "parity": s["parity"],
                 "probe_read_GBps": s["probe_gbs"] and round(s["probe_gbs"], 1)}
+        if args.pcie and world == 1:
+            out["pcie_inclusive"] = pcie_inclusive(head, ctx)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(head, seconds=args.cpu_seconds)
         else:
