@@ -33,6 +33,9 @@ CONFIGS = {
                workload="C3: 64M x 1500B Eth/IPv4/TCP, IPv4+TCP checksum, link/net/transport FastHash"),
     "c2": dict(synth=2, decoders=("Ethernet", "IPv4", "UDP", "Payload"), outputs=1,
                workload="C2: 64M x 64B Eth/IPv4/UDP, header decode + IPv4 checksum"),
+    # diagnostics (not bench lines): C3 bytes with the L4 checksum and flows off
+    "c3h": dict(synth=3, decoders=("Ethernet", "IPv4", "TCP", "Payload"), outputs=1,
+                workload="C3 packets, headers + IPv4 checksum only (diagnostic)"),
     "c4": dict(synth=4, decoders=("Ethernet", "Dot1Q", "IPv4", "IPv6", "IPv6ExtensionSkipper", "TCP", "UDP",
                                   "Payload"), outputs=7,
                workload="C4: 64M IMIX 64/594/1518 7:4:1, 40% Dot1Q/QinQ, 20% IPv6, all checksums + hashes"),

@@ -68,7 +68,10 @@ struct KParams {
 // from 32 lanes hit 32 different banks.
 constexpr int kBlock = 256;
 constexpr int kWaves = kBlock / 64;
-constexpr int kWinChunks = 9;
+#ifndef GPK_WIN_CHUNKS
+#define GPK_WIN_CHUNKS 9
+#endif
+constexpr int kWinChunks = GPK_WIN_CHUNKS;
 constexpr int kSlotDw = kWinChunks * 4 + 1;  // 37 (odd: conflict-free)
 constexpr int kLdsBytes = kBlock * kSlotDw * 4;
 
@@ -640,7 +643,17 @@ __device__ __forceinline__ Outcome run_parser(const KParams& P, const TT& T, con
     Res x;
     // Whole header (the most bytes this decoder may read) inside the LDS
     // window: branch-free LDS reads; otherwise the mixed reader.
-    const bool fast = off + max_header(kind) <= r.win;
+    // IPv4/TCP: the header length field bounds the bytes read (options
+    // included), so only that much has to be in the window.
+    uint32_t need = max_header(kind);
+    if (kind == GPK_DEC_IPV4 && off < r.win) {
+      const uint32_t h = 4 * (lds8(r.lb + off) & 15);
+      need = h > 20 ? h : 20;
+    } else if (kind == GPK_DEC_TCP && off + 12 < r.win) {
+      const uint32_t h = 4 * (lds8(r.lb + off + 12) >> 4);
+      need = h > 20 ? h : 20;
+    }
+    const bool fast = off + need <= r.win;
     const RdL rl{r.lb};
     switch (kind) {
       case GPK_DEC_ETHERNET: x = fast ? dec_ethernet(T, rl, off, len) : dec_ethernet(T, r, off, len); break;

@@ -45,6 +45,15 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 #ifndef GPK_PERSISTENT
 #define GPK_PERSISTENT 0  // 1: blocks loop over tiles (A/B r01: +50 VGPRs from hoisting, no gain)
 #endif
+#ifndef GPK_PB_STREAM
+#define GPK_PB_STREAM 1  // phase B as a continuous stream of 1 KiB wave loads
+#endif
+#ifndef GPK_PB_DEPTH
+#define GPK_PB_DEPTH 8  // phase-B wave loads in flight
+#endif
+#ifndef GPK_PB_NULL
+#define GPK_PB_NULL 0  // timing-only: phase-B loads read nothing (zero-record descriptors)
+#endif
 #ifndef GPK_NT_B
 #define GPK_NT_B 1
 #endif
@@ -338,6 +347,73 @@ __device__ __forceinline__ void decode_packet(const KParams& P, const TT& T, uin
   if (kL4) {
     uint32_t extra = 0;
     uint64_t pend = __ballot(job);
+#if GPK_PB_STREAM
+    // The wave's pending segments as one stream of 1 KiB wave loads (items),
+    // packet after packet, GPK_PB_DEPTH items always in flight: a register
+    // ring, refilled as each item is consumed. Item = one raw-buffer load of
+    // 16 bytes per lane from the packet's remaining whole chunks; bytes past
+    // the packet's end come back as zeros (range check), so no predicates.
+    const uint32_t vo = lane * 16;
+    constexpr int D = GPK_PB_DEPTH;
+    uint32_t p_lane = 64, p_off = 0, p_len = 0;  // producer (wave-uniform)
+    __amdgpu_buffer_rsrc_t p_rs = __builtin_amdgcn_make_buffer_rsrc((void*)P.data, 0, 0, 0x00020000);
+    u32x4 ring[D];
+    uint32_t r_lane[D], r_last[D];
+#pragma unroll
+    for (int k = 0; k < D; k++) {
+      if (p_off >= p_len) {
+        p_lane = 64;
+        p_off = p_len = 0;
+        uint64_t b0 = 0;
+        if (pend) {
+          p_lane = (uint32_t)__builtin_ctzll(pend);
+          pend &= pend - 1;
+          b0 = readlane64(ja, p_lane);
+          p_len = (uint32_t)(readlane64(je, p_lane) - b0);
+        }
+        p_rs = __builtin_amdgcn_make_buffer_rsrc((void*)(P.data + b0), 0, GPK_PB_NULL ? 0 : p_len, 0x00020000);
+      }
+      ring[k] = __builtin_amdgcn_raw_buffer_load_b128(p_rs, vo, p_off, GPK_NT_B ? 2 : 0);
+      r_lane[k] = p_lane;
+      r_last[k] = p_off + 1024 >= p_len;
+      p_off += 1024;
+    }
+    uint32_t E = 0, O = 0;
+    for (;;) {
+      uint32_t live = 0;
+#pragma unroll
+      for (int k = 0; k < D; k++) {
+        if (r_lane[k] < 64) {
+          const u32x4 x = ring[k];
+          chunk_eo(make_uint4(x.x, x.y, x.z, x.w), E, O);
+          if (r_last[k]) {
+            const uint32_t pr = readlane32(jpar, r_lane[k]);
+            const uint32_t t = wave_sum(pr ? (O << 8) + E : (E << 8) + O);
+            if (lane == r_lane[k]) extra += t;
+            E = O = 0;
+          }
+        }
+        if (p_off >= p_len) {
+          p_lane = 64;
+          p_off = p_len = 0;
+          uint64_t b0 = 0;
+          if (pend) {
+            p_lane = (uint32_t)__builtin_ctzll(pend);
+            pend &= pend - 1;
+            b0 = readlane64(ja, p_lane);
+            p_len = (uint32_t)(readlane64(je, p_lane) - b0);
+          }
+          p_rs = __builtin_amdgcn_make_buffer_rsrc((void*)(P.data + b0), 0, GPK_PB_NULL ? 0 : p_len, 0x00020000);
+        }
+        ring[k] = __builtin_amdgcn_raw_buffer_load_b128(p_rs, vo, p_off, GPK_NT_B ? 2 : 0);
+        r_lane[k] = p_lane;
+        r_last[k] = p_off + 1024 >= p_len;
+        p_off += 1024;
+        live |= r_lane[k] < 64;
+      }
+      if (!live) break;
+    }
+#else
     const uint32_t vo = lane * 16;
     while (pend) {
       constexpr int G = GPK_PB_G;
@@ -389,6 +465,7 @@ __device__ __forceinline__ void decode_packet(const KParams& P, const TT& T, uin
         }
       }
     }
+#endif
     if (job) l4c = fold(jsum + extra - jexist);
   }
   if (active && (st & GPK_ST_L4_CSUM)) {

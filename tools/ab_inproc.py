@@ -1,0 +1,90 @@
+#!/usr/bin/env python3
+"""In-process A/B of kernel variants: every variant library is loaded into one
+process (ctypes, RTLD_LOCAL: each keeps its own gpk_* symbols and HIP
+module), the synthetic batch is generated once, and the variants are timed
+in interleaved rounds so clocks and thermals affect them alike.
+
+    python tools/ab_inproc.py --configs c3,c2,c4 --rounds 5 --steps 5 base w6 w7 ...
+
+"base" = gopacket_amd/libgpk.so, NAME = gopacket_amd/build/libgpk_NAME.so.
+Prints, per config and variant, the median and min kernel ms over rounds.
+"""
+import argparse
+import ctypes
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def load(name):
+    import torch  # noqa: F401  (one HIP runtime: torch's)
+    path = os.path.join(ROOT, "gopacket_amd", "libgpk.so" if name == "base" else "build/libgpk_%s.so" % name)
+    L = ctypes.CDLL(path)
+    vp = ctypes.c_void_p
+    L.gpk_ctx_create.argtypes = [ctypes.POINTER(vp), ctypes.c_int]
+    L.gpk_parser_create.argtypes = [ctypes.POINTER(vp), ctypes.c_int64]
+    L.gpk_parser_add_decoder.argtypes = [vp, ctypes.c_int]
+    L.gpk_parser_set_outputs.argtypes = [vp, ctypes.c_uint32]
+    L.gpk_decode_batch.argtypes = [vp, vp, vp, vp, vp]
+    return L
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--configs", default="c3,c2,c4")
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--packets", type=int, default=64 * 2**20)
+    ap.add_argument("variants", nargs="+")
+    a = ap.parse_args()
+    import numpy as np
+    import torch
+    import bench
+    from gopacket_amd import _lib, engine, synth
+    libs = {v: load(v) for v in a.variants}
+    stream = torch.cuda.current_stream()
+    for name in a.configs.split(","):
+        cfg = bench.CONFIGS[name]
+        n = a.packets
+        data, off, cap = synth.device_batch(cfg["synth"], 0, n, stream=stream)
+        rec = torch.empty(n * 16, dtype=torch.uint8, device="cuda")
+        err = torch.zeros(2 * n, dtype=torch.int32, device="cuda")
+        fl = torch.empty(3 * n, dtype=torch.int64, device="cuda")
+        algo = int(cap.sum(dtype=torch.int64).item()) + 12 * n
+        b = _lib.Batch(data.data_ptr(), off.data_ptr(), cap.data_ptr(), n, data.numel())
+        r = _lib.Results(rec.data_ptr(), err.data_ptr(), fl.data_ptr(), None)
+        handles = {}
+        for v, L in libs.items():
+            ctx, p = ctypes.c_void_p(), ctypes.c_void_p()
+            assert L.gpk_ctx_create(ctypes.byref(ctx), 0) == 0
+            assert L.gpk_parser_create(ctypes.byref(p), 17) == 0
+            for d in cfg["decoders"]:
+                assert L.gpk_parser_add_decoder(p, engine.DECODER_KINDS[d]) == 0
+            assert L.gpk_parser_set_outputs(p, cfg["outputs"]) == 0
+            handles[v] = (ctx, p)
+        times = {v: [] for v in libs}
+        for rnd in range(a.rounds + 1):
+            for v, L in libs.items():
+                ctx, p = handles[v]
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+                for _ in range(a.steps):
+                    rc = L.gpk_decode_batch(ctx, p, ctypes.byref(b), ctypes.byref(r), ctypes.c_void_p(stream.cuda_stream))
+                    assert rc == 0
+                e1.record(stream)
+                torch.cuda.synchronize()
+                if rnd:  # round 0 warms every variant up
+                    times[v].append(e0.elapsed_time(e1) / a.steps)
+        for v in libs:
+            t = np.array(times[v])
+            print("%-4s %-10s median %8.3f ms  min %8.3f ms  %7.1f GB/s (%.1f%% of 8 TB/s)" % (
+                name, v, np.median(t), t.min(), algo / (np.median(t) * 1e-3) / 1e9,
+                algo / (np.median(t) * 1e-3) / 8e12 * 100), flush=True)
+        del data, off, cap, rec, err, fl
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()
