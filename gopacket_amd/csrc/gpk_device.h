@@ -69,10 +69,10 @@ struct KParams {
 constexpr int kBlock = 256;
 constexpr int kWaves = kBlock / 64;
 #ifndef GPK_WIN_CHUNKS
-#define GPK_WIN_CHUNKS 9
+#define GPK_WIN_CHUNKS 5  // 80-byte header window: 6 blocks per CU (A/B r01: C2 -21%, C4 -17%, C3 -5% vs 9)
 #endif
 constexpr int kWinChunks = GPK_WIN_CHUNKS;
-constexpr int kSlotDw = kWinChunks * 4 + 1;  // 37 (odd: conflict-free)
+constexpr int kSlotDw = kWinChunks * 4 + 1;  // odd: lanes reading equal positions hit distinct banks
 constexpr int kLdsBytes = kBlock * kSlotDw * 4;
 
 // Dynamic LDS of the decode kernels (one declaration, aliased everywhere).

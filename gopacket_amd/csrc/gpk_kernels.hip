@@ -31,7 +31,7 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 #define GPK_NT_A 0  // A/B (r01): temporal phase-A loads keep lines shared with phase B in L2: C3 +30%
 #endif
 #ifndef GPK_WAVES_PER_EU
-#define GPK_WAVES_PER_EU 4  // <= 128 VGPRs: 4 waves/SIMD, the LDS limit too
+#define GPK_WAVES_PER_EU 6  // <= 80 VGPRs: 6 waves/SIMD, matching the 6 blocks per CU the LDS allows
 #endif
 #ifndef GPK_PB_G
 #define GPK_PB_G 4  // phase B: pending packets per wave pass
