@@ -54,6 +54,9 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 #ifndef GPK_PB_NULL
 #define GPK_PB_NULL 0  // timing-only: phase-B loads read nothing (zero-record descriptors)
 #endif
+#ifndef GPK_PPL
+#define GPK_PPL 1  // packets per lane (tiles per block)
+#endif
 #ifndef GPK_NT_B
 #define GPK_NT_B 1
 #endif
@@ -578,7 +581,41 @@ __device__ __forceinline__ void decode_tiles(const KParams& P, const TT& T) {
 template <bool kL4, bool kLayout, bool kCompact>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GPK_WAVES_PER_EU, 8))) void decode_kernel(
     KParams P) {
-  if ((uint64_t)blockIdx.x * kBlock >= P.n) return;  // uniform over the block
+  if ((uint64_t)blockIdx.x * kBlock * GPK_PPL >= P.n) return;  // uniform over the block
+#if !GPK_PERSISTENT && !GPK_PREFETCH
+  // GPK_PPL tiles per block, one packet of each per lane: every packet's
+  // index, then every header window (the first in LDS, the others held in
+  // registers) and the table blob are in flight together, so the two
+  // dependent memory round trips are paid once for GPK_PPL packets.
+  const uint32_t tid = threadIdx.x;
+  const uint32_t slot_dw = tid * kSlotDw;
+  const uint64_t i0 = (uint64_t)blockIdx.x * (kBlock * GPK_PPL) + tid, i1 = i0 + kBlock;
+  static_assert(GPK_PPL == 1 || GPK_PPL == 2, "GPK_PPL is 1 or 2");
+  const Idx c0 = load_index(P, i0);
+  const Idx c1 = GPK_PPL == 2 ? load_index(P, i1) : Idx{0, 0};
+  const uint32_t n0 = win_chunks(c0, i0 < P.n);
+  const uint32_t n1 = GPK_PPL == 2 ? win_chunks(c1, i1 < P.n) : 0;
+  Win w0, w1;
+  load_window(P, c0, n0, w0);
+  if (GPK_PPL == 2) load_window(P, c1, n1, w1);
+  const uint32_t base = kBlock * kSlotDw;
+  if (kCompact) {
+    for (uint32_t k = tid; k < P.cg.words; k += kBlock) gpk_smem[base + k] = P.ctab[k];
+    __syncthreads();
+  }
+  store_window(slot_dw, n0, w0);
+  if (kCompact)
+    decode_packet<kL4, kLayout>(P, LTab{P.cg, base}, i0, i0 < P.n, c0.off, c0.cl, slot_dw, tid & 63);
+  else
+    decode_packet<kL4, kLayout>(P, GTab{P.tab}, i0, i0 < P.n, c0.off, c0.cl, slot_dw, tid & 63);
+  if (GPK_PPL == 2) {
+    store_window(slot_dw, n1, w1);  // lane-private slot, reused
+    if (kCompact)
+      decode_packet<kL4, kLayout>(P, LTab{P.cg, base}, i1, i1 < P.n, c1.off, c1.cl, slot_dw, tid & 63);
+    else
+      decode_packet<kL4, kLayout>(P, GTab{P.tab}, i1, i1 < P.n, c1.off, c1.cl, slot_dw, tid & 63);
+  }
+#else
   if (kCompact) {
     const uint32_t base = kBlock * kSlotDw;
     for (uint32_t w = threadIdx.x; w < P.cg.words; w += kBlock) gpk_smem[base + w] = P.ctab[w];
@@ -587,6 +624,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GPK_WAVE
   } else {
     decode_tiles<kL4, kLayout>(P, GTab{P.tab});
   }
+#endif
 }
 
 // Full decoded list of one packet (lists longer than the 16 inline codes).
@@ -629,7 +667,7 @@ hipError_t launch(const gpk::KParams* P, hipStream_t stream) {
   const uint64_t ntiles = (P->n + kBlock - 1) / kBlock;
   uint64_t grid = (uint64_t)cached_cus[dev] * cached_bpc[dev] * 8;
   if (ntiles < grid * 8) grid = (ntiles + 7) / 8;
-  if (!GPK_PERSISTENT && !GPK_PREFETCH) grid = ntiles;
+  if (!GPK_PERSISTENT && !GPK_PREFETCH) grid = (ntiles + GPK_PPL - 1) / GPK_PPL;
   if (grid < 1) grid = 1;
   hipLaunchKernelGGL((decode_kernel<kL4, kLayout, kCompact>), dim3((unsigned)grid), dim3(kBlock), lds, stream, *P);
   return hipGetLastError();
