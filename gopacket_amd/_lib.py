@@ -54,7 +54,44 @@ EXPORTS = (
     "gpk_ctx_destroy", "gpk_ctx_set_table_mode", "gpk_decode_batch", "gpk_decode_batch_host", "gpk_decoded_list",
     "gpk_decoded_list_host", "gpk_host_alloc", "gpk_host_free", "gpk_format_error", "gpk_layer_type_name", "gpk_code_layer_type", "gpk_strerror",
     "gpk_last_hip_error", "gpk_abi_version",
+    # include/gpk_capture.h
+    "gpk_capreader_create", "gpk_capreader_destroy", "gpk_capreader_index", "gpk_capreader_error",
+    "gpk_capreader_link_type", "gpk_capreader_pcap_header", "gpk_capreader_nsections", "gpk_capreader_section_info",
+    "gpk_capreader_ninterfaces", "gpk_capreader_interface", "gpk_capreader_interface_str", "gpk_replay_file",
 )
+
+# include/gpk_capture.h constants
+CAP_PCAP, CAP_PCAPNG = 1, 2
+NG_WANT_MIXED_LINKTYPE, NG_ERROR_ON_MISMATCHING_LINKTYPE, NG_SKIP_UNKNOWN_VERSION = 1, 2, 4
+CAP_MORE, CAP_FULL, CAP_END = 0, 1, 2
+CAPINFO_DTYPE = np.dtype([("ts_sec", "<i8"), ("ts_nsec", "<u4"), ("length", "<u4"), ("iface", "<i4"),
+                          ("link_type", "<i4")])
+
+
+class NgInterface(ctypes.Structure):
+    _fields_ = [("link_type", ctypes.c_uint16), ("ts_resolution", ctypes.c_uint8),
+                ("has_statistics", ctypes.c_uint8), ("snap_length", ctypes.c_uint32), ("ts_offset", ctypes.c_uint64),
+                ("last_update_sec", ctypes.c_int64), ("start_time_sec", ctypes.c_int64),
+                ("end_time_sec", ctypes.c_int64), ("last_update_nsec", ctypes.c_uint32),
+                ("start_time_nsec", ctypes.c_uint32), ("end_time_nsec", ctypes.c_uint32), ("_pad", ctypes.c_uint32),
+                ("packets_received", ctypes.c_uint64), ("packets_dropped", ctypes.c_uint64)]
+
+
+class ReplayOpts(ctypes.Structure):
+    _fields_ = [("format", ctypes.c_int), ("ng_flags", ctypes.c_uint32), ("slot_bytes", ctypes.c_uint64),
+                ("slots", ctypes.c_int), ("batch_pkts", ctypes.c_uint64), ("read_threads", ctypes.c_int)]
+
+
+class ReplayStats(ctypes.Structure):
+    _fields_ = [("packets", ctypes.c_uint64), ("packet_bytes", ctypes.c_uint64), ("file_bytes", ctypes.c_uint64),
+                ("stream_bytes", ctypes.c_uint64), ("batches", ctypes.c_uint64), ("slots", ctypes.c_uint64),
+                ("wall_s", ctypes.c_double), ("read_s", ctypes.c_double), ("index_s", ctypes.c_double),
+                ("gpu_s", ctypes.c_double), ("kernel_s", ctypes.c_double), ("deliver_s", ctypes.c_double),
+                ("reader_status", ctypes.c_int), ("error", ctypes.c_char * 160)]
+
+
+REPLAY_CB = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p,
+                             ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p)
 
 
 class GpkError(RuntimeError):
@@ -123,6 +160,18 @@ def lib():
         "gpk_strerror": ([c_int], ctypes.c_char_p),
         "gpk_last_hip_error": ([], ctypes.c_char_p),
         "gpk_abi_version": ([], c_int),
+        "gpk_capreader_create": ([P(vp), c_int, u32], c_int),
+        "gpk_capreader_destroy": ([vp], c_int),
+        "gpk_capreader_index": ([vp, vp, u64, c_int, vp, vp, vp, u64, P(u64), P(u64)], c_int),
+        "gpk_capreader_error": ([vp, ctypes.c_char_p, ctypes.c_size_t, P(c_int), P(c_int)], c_int),
+        "gpk_capreader_link_type": ([vp], c_int),
+        "gpk_capreader_pcap_header": ([vp, P(u32), P(ctypes.c_uint16), P(ctypes.c_uint16), P(c_int)], c_int),
+        "gpk_capreader_nsections": ([vp], c_int),
+        "gpk_capreader_section_info": ([vp, c_int, c_int, ctypes.c_char_p, ctypes.c_size_t], c_int),
+        "gpk_capreader_ninterfaces": ([vp, c_int], c_int),
+        "gpk_capreader_interface": ([vp, c_int, c_int, P(NgInterface)], c_int),
+        "gpk_capreader_interface_str": ([vp, c_int, c_int, c_int, ctypes.c_char_p, ctypes.c_size_t], c_int),
+        "gpk_replay_file": ([vp, vp, ctypes.c_char_p, P(ReplayOpts), REPLAY_CB, vp, P(ReplayStats)], c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)

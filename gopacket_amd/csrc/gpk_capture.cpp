@@ -1,0 +1,840 @@
+// gpk_capture.cpp — pcap / pcapng batch indexer (include/gpk_capture.h).
+//
+// A restatement of pcapgo's readers as a resumable byte-stream machine: the
+// capture arrives in chunks (pinned staging slots), the machine walks the
+// records in place and emits (offset, caplen, CaptureInfo) per packet, so the
+// staging buffer itself is the packed batch the device decodes — no copy of
+// packet bytes on the host.
+//
+// Each "call" below is one ReadPacketData of the reference. The reader's
+// position and state advance exactly as Go's bufio-backed reader does,
+// including its accounting quirks (block length tracked as uint32 and allowed
+// to wrap, the reused option value buffer, the 24-byte EUI address length in
+// name records), so a malformed capture desynchronises the same way. When a
+// call needs bytes beyond the chunk (and the chunk is not the end of the
+// stream) the call is undone — position back to its start, state restored
+// from a snapshot taken lazily at the first mutation — and indexing stops
+// there: the caller re-presents the rest with more bytes appended.
+//
+// Reference functions (pcapgo/): NewNgReader ngread.go:64-106, readBytes
+// :112-126, discard :128-137, readBlock :170-196, readOption :199-236,
+// readSectionHeader :240-305, skipSection :308-320, firstInterface :330-369,
+// readInterfaceDescriptor :372-436, convertTime :439-443,
+// readInterfaceStatistics :446-492, readPacketHeader :497-582,
+// readPacketOptions :584-632, ReadPacketDataWithOptions :642-675,
+// readNameResolutionBlock ngread_nrb.go:63-130, readDecryptionSecretsBlock
+// ngread_dsb.go:17-39; NewReader/readHeader read.go:64-122, ReadPacketData
+// :124-140, readPacketHeader :171-180.
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/gpk_capture.h"
+
+namespace {
+
+constexpr int64_t kZeroTimeSec = -62135596800LL;  // time.Time{}.Unix()
+constexpr uint64_t kNoValue64 = ~0ull;             // NgNoValue64
+constexpr uint32_t kSHB = 0x0A0D0D0A, kIDB = 1, kPB = 2, kSPB = 3, kNRB = 4, kISB = 5, kEPB = 6, kDSB = 0xA;
+constexpr uint32_t kByteOrderMagic = 0x1A2B3C4D;
+
+const char* const kEOF = "EOF";
+const char* const kUnexpectedEOF = "unexpected EOF";
+
+struct NeedMore {};
+struct GoErr {
+  std::string text;
+  bool panic;
+};
+[[noreturn]] void fail(const std::string& s, bool panic = false) { throw GoErr{s, panic}; }
+
+std::string fmt(const char* f, ...) __attribute__((format(printf, 1, 2)));
+std::string fmt(const char* f, ...) {
+  char b[256];
+  va_list ap;
+  va_start(ap, f);
+  vsnprintf(b, sizeof(b), f, ap);
+  va_end(ap);
+  return b;
+}
+
+inline uint16_t ld16(const uint8_t* p, bool be) {
+  return be ? (uint16_t)(p[0] << 8 | p[1]) : (uint16_t)(p[1] << 8 | p[0]);
+}
+inline uint32_t ld32(const uint8_t* p, bool be) {
+  return be ? ((uint32_t)p[0] << 24 | (uint32_t)p[1] << 16 | (uint32_t)p[2] << 8 | p[3])
+            : ((uint32_t)p[3] << 24 | (uint32_t)p[2] << 16 | (uint32_t)p[1] << 8 | p[0]);
+}
+inline uint64_t ld64(const uint8_t* p, bool be) {
+  return be ? ((uint64_t)ld32(p, true) << 32 | ld32(p + 4, true)) : ((uint64_t)ld32(p + 4, false) << 32 | ld32(p, false));
+}
+
+// time.Unix(sec, nsec).UTC() normalisation
+void unix_norm(int64_t sec, int64_t nsec, int64_t* os, uint32_t* ons) {
+  if (nsec < 0 || nsec >= 1000000000LL) {
+    int64_t n = nsec / 1000000000LL;  // truncates toward zero, like Go
+    sec = (int64_t)((uint64_t)sec + (uint64_t)n);
+    nsec -= n * 1000000000LL;
+    if (nsec < 0) {
+      nsec += 1000000000LL;
+      sec = (int64_t)((uint64_t)sec - 1);
+    }
+  }
+  *os = sec;
+  *ons = (uint32_t)nsec;
+}
+
+struct Stats {
+  int64_t lu_s = kZeroTimeSec, st_s = kZeroTimeSec, et_s = kZeroTimeSec;
+  uint32_t lu_ns = 0, st_ns = 0, et_ns = 0;
+  std::string comment;
+  uint64_t received = 0, dropped = 0;
+};
+
+struct Iface {
+  std::string name, comment, description, filter, os;
+  uint16_t link_type = 0;
+  uint8_t tsres = 0;
+  uint64_t tsoff = 0;
+  uint32_t snap = 0;
+  uint64_t second_mask = 0, scale_up = 0, scale_down = 0;
+  bool has_stats = false;
+  Stats stats;
+};
+
+struct Section {
+  std::string comment, hardware, os, application;
+};
+
+struct NgState {  // what a rollback restores
+  bool be = false;
+  std::vector<Iface> ifaces;
+  Section section;
+  uint16_t link_type = 0;
+  bool first_section_found = false, active_section = false;
+  std::vector<std::pair<Section, std::vector<Iface>>> ended;
+};
+
+struct OptBuf {  // NgReader.currentOption.value: backing array + length
+  std::vector<uint8_t> back = std::vector<uint8_t>(1024, 0);
+  uint32_t len = 1024;
+};
+
+}  // namespace
+
+struct gpk_capreader {
+  int format = 0;
+  uint32_t flags = 0;
+  // stream cursor over the current chunk
+  const uint8_t* b = nullptr;
+  uint64_t n = 0, pos = 0;
+  bool eof = false;
+  // life cycle
+  bool opened = false, open_failed = false;
+  std::string err_text;
+  bool err_eof = false, err_panic = false;
+  // pcap
+  bool pbe = false;
+  uint32_t factor = 1, snaplen = 0;
+  uint16_t major = 0, minor = 0;
+  uint32_t plink = 0;
+  // pcapng
+  NgState st, st_snap;
+  bool st_saved = false;
+  OptBuf opt, opt_snap;
+  bool opt_saved = false;
+  uint32_t typ = 0, blen = 0;  // currentBlock
+  uint16_t opt_code = 0;
+  // ci of the current call
+  uint32_t ci_iface = 0, ci_caplen = 0, ci_len = 0;
+  int64_t ci_s = 0;
+  uint32_t ci_ns = 0;
+
+  // ---- primitives (bufio.Reader over the chunk) ----------------------------
+  uint64_t avail() const { return n - pos; }
+  // NgReader.readBytes: reads k <= m bytes; short only at end of stream
+  uint64_t read_into(uint8_t* dst, uint64_t m) {
+    if (m > avail()) {
+      if (!eof) throw NeedMore{};
+      uint64_t k = avail();
+      if (dst && k) memcpy(dst, b + pos, k);
+      pos = n;
+      return k;
+    }
+    if (dst && m) memcpy(dst, b + pos, m);
+    pos += m;
+    return m;
+  }
+  const uint8_t* read_view(uint64_t m) {  // readBytes into a scratch buffer, error on short read
+    if (m > avail()) {
+      if (!eof) throw NeedMore{};
+      pos = n;
+      fail(kUnexpectedEOF);
+    }
+    const uint8_t* p = b + pos;
+    pos += m;
+    return p;
+  }
+  void discard(uint64_t m) {  // NgReader.discard
+    if (m > avail()) {
+      if (!eof) throw NeedMore{};
+      pos = n;
+      fail(kUnexpectedEOF);
+    }
+    pos += m;
+    blen -= (uint32_t)m;
+  }
+  bool be() const { return st.be; }
+  void touch() {
+    if (!st_saved) {
+      st_snap = st;
+      st_saved = true;
+    }
+  }
+  void touch_opt() {
+    if (!opt_saved) {
+      opt_snap = opt;
+      opt_saved = true;
+    }
+  }
+
+  // ---- pcapng --------------------------------------------------------------
+  void read_block() {
+    if (avail() < 8) {
+      if (!eof) throw NeedMore{};
+      uint64_t k = avail();
+      pos = n;
+      fail(k == 0 ? kEOF : kUnexpectedEOF);
+    }
+    const uint8_t* h = b + pos;
+    pos += 8;
+    typ = ld32(h, be());
+    if (typ == kSHB) {
+      const uint8_t* m = read_view(4);
+      bool nbe;
+      if (ld32(m, true) == kByteOrderMagic)
+        nbe = true;
+      else if (ld32(m, false) == kByteOrderMagic)
+        nbe = false;
+      else
+        fail("Wrong byte order value in Section Header");
+      if (nbe != st.be) {
+        touch();
+        st.be = nbe;
+      }
+      blen = ld32(h + 4, be()) - 8 - 4;
+      return;
+    }
+    blen = ld32(h + 4, be()) - 8;
+  }
+
+  void read_option() {
+    if (blen == 4) {
+      opt_code = 0;
+      return;
+    }
+    const uint8_t* h = read_view(4);
+    blen -= 4;
+    opt_code = ld16(h, be());
+    uint16_t olen = ld16(h + 2, be());
+    if (opt_code == 0) {
+      if (olen != 0) fail("End of Options must be zero length");
+      return;
+    }
+    if (olen != 0) {
+      touch_opt();
+      if (olen < opt.back.size()) {
+        opt.len = olen;
+      } else {
+        opt.back.assign(olen, 0);
+        opt.len = olen;
+      }
+      uint64_t k = read_into(opt.back.data(), olen);
+      if (k < olen) fail(kUnexpectedEOF);
+      uint16_t pad = olen % 4;
+      if (pad > 0) discard(4 - pad);
+      blen -= olen;
+    }
+  }
+  std::string opt_str(uint32_t skip = 0) const {
+    return skip >= opt.len ? std::string() : std::string((const char*)opt.back.data() + skip, opt.len - skip);
+  }
+  uint64_t opt_u64() const { return ld64(opt.back.data(), be()); }  // value[:8] (cap >= 1024)
+  uint32_t opt_u32(uint32_t o) const { return ld32(opt.back.data() + o, be()); }
+
+  void read_section_header() {
+    touch();
+    if (st.active_section) st.ended.emplace_back(st.section, st.ifaces);
+    st.ifaces.clear();
+    st.active_section = false;
+    for (;;) {  // RESTART
+      const uint8_t* h = read_view(12);
+      blen -= 12;
+      uint16_t vmaj = ld16(h, be()), vmin = ld16(h + 2, be());
+      if (vmaj != 1 || vmin != 0) {
+        if (!(flags & GPK_NG_SKIP_UNKNOWN_VERSION)) fail("Unknown pcapng Version in Section Header");
+        discard(blen);
+        skip_section();
+        continue;
+      }
+      break;
+    }
+    Section sec;
+    for (;;) {
+      read_option();
+      if (opt_code == 0) break;
+      switch (opt_code) {
+        case 1: sec.comment = opt_str(); break;
+        case 2: sec.hardware = opt_str(); break;
+        case 3: sec.os = opt_str(); break;
+        case 4: sec.application = opt_str(); break;
+      }
+    }
+    discard(blen);
+    st.active_section = true;
+    st.section = sec;
+    if (!(flags & GPK_NG_WANT_MIXED_LINKTYPE)) first_interface();
+  }
+
+  void skip_section() {
+    for (;;) {
+      read_block();
+      if (typ == kSHB) return;
+      discard(blen);
+    }
+  }
+
+  void first_interface() {
+    for (;;) {
+      read_block();
+      switch (typ) {
+        case kIDB:
+          read_interface_descriptor();
+          if (!st.first_section_found) {
+            st.link_type = st.ifaces[0].link_type;
+            st.first_section_found = true;
+          } else if (st.link_type != st.ifaces[0].link_type) {
+            if (flags & GPK_NG_ERROR_ON_MISMATCHING_LINKTYPE)
+              fail("Link type of current interface is different from first one");
+            continue;
+          }
+          return;
+        case kPB:
+        case kEPB:
+        case kSPB:
+        case kISB:
+          fail("A section must have an interface before a packet block");
+        case kDSB:
+          read_decryption_secrets();
+          break;
+        case kNRB:
+          read_name_resolution();
+          break;
+      }
+      discard(blen);
+    }
+  }
+
+  void read_interface_descriptor() {
+    const uint8_t* h = read_view(8);
+    blen -= 8;
+    Iface it;
+    it.link_type = ld16(h, be());
+    it.snap = ld32(h + 4, be());
+    for (;;) {
+      read_option();
+      if (opt_code == 0) break;
+      switch (opt_code) {
+        case 2: it.name = opt_str(); break;
+        case 1: it.comment = opt_str(); break;
+        case 3: it.description = opt_str(); break;
+        case 11: it.filter = opt_str(1); break;
+        case 12: it.os = opt_str(); break;
+        case 14: it.tsoff = opt_u64(); break;
+        case 9: it.tsres = opt.back[0]; break;
+      }
+    }
+    discard(blen);
+    if (it.tsres == 0) it.tsres = 6;
+    const uint32_t e = it.tsres & 0x7f;
+    if (it.tsres & 0x80) {
+      it.second_mask = e < 64 ? (1ull << e) : 0;  // Go: shifts >= 64 give 0
+    } else {
+      it.second_mask = 1;
+      for (uint32_t j = 0; j < e; j++) it.second_mask *= 10;
+    }
+    it.scale_down = 1;
+    it.scale_up = 1;
+    if (it.second_mask < 1000000000ull) {
+      if (it.second_mask == 0) fail("runtime error: integer divide by zero", true);
+      it.scale_up = 1000000000ull / it.second_mask;
+    } else {
+      it.scale_down = it.second_mask / 1000000000ull;
+    }
+    touch();
+    st.ifaces.push_back(std::move(it));
+  }
+
+  void convert_time(uint32_t idx, uint64_t ts, int64_t* s, uint32_t* ns) const {
+    const Iface& it = st.ifaces[idx];
+    int64_t sec = (int64_t)(ts / it.second_mask + it.tsoff);
+    int64_t nsec = (int64_t)(ts % it.second_mask * it.scale_up / it.scale_down);
+    unix_norm(sec, nsec, s, ns);
+  }
+
+  void read_interface_statistics() {
+    const uint8_t* h = read_view(12);
+    blen -= 12;
+    uint32_t idx = ld32(h, be());
+    uint64_t ts = (uint64_t)ld32(h + 4, be()) << 32 | ld32(h + 8, be());
+    if (idx >= st.ifaces.size())
+      fail(fmt("Interface id %u not present in section (have only %zu interfaces)", idx, st.ifaces.size()));
+    touch();
+    Iface& it = st.ifaces[idx];
+    it.has_stats = true;
+    it.stats = Stats();
+    it.stats.received = it.stats.dropped = kNoValue64;
+    convert_time(idx, ts, &it.stats.lu_s, &it.stats.lu_ns);
+    for (;;) {
+      read_option();
+      if (opt_code == 0) break;
+      Stats& S = st.ifaces[idx].stats;
+      switch (opt_code) {
+        case 1: S.comment = opt_str(); break;
+        case 2: convert_time(idx, (uint64_t)opt_u32(0) << 32 | opt_u32(4), &S.st_s, &S.st_ns); break;
+        case 3: convert_time(idx, (uint64_t)opt_u32(0) << 32 | opt_u32(4), &S.et_s, &S.et_ns); break;
+        case 4: S.received = opt_u64(); break;
+        case 5: S.dropped = opt_u64(); break;
+      }
+    }
+    discard(blen);
+  }
+
+  void read_decryption_secrets() {
+    uint8_t h[8];
+    if (read_into(h, 8) < 8) fail(fmt("could not read DecryptionSecret Header block length: %s", kUnexpectedEOF));
+    blen -= 8;
+    uint32_t slen = ld32(h + 4, be());
+    if (read_into(nullptr, slen) < slen)
+      fail(fmt("could not read %u bytes from DecryptionSecret payload: %s", slen, kUnexpectedEOF));
+    blen -= slen;
+  }
+
+  void read_name_resolution() {
+    while (blen > 0) {
+      uint8_t h[4];
+      if (read_into(h, 4) < 4) fail(fmt("could not read NameRecord Header block length: %s", kUnexpectedEOF));
+      blen -= 4;
+      uint16_t rtype = ld16(h, be()), rlen = ld16(h + 2, be());
+      int64_t length = rlen < (int64_t)blen ? (int64_t)rlen : (int64_t)blen;
+      int64_t padding = length % 4 ? 4 - length % 4 : 0;
+      int64_t alen;
+      if (rtype == 1 || rtype == 2) {
+        uint64_t m = rtype == 1 ? 4 : 16;
+        if (read_into(nullptr, m) < m)
+          fail(fmt("could not read %s address: could not read IP address: %s", rtype == 1 ? "IPv4" : "IPv6",
+                   kUnexpectedEOF));
+        alen = (int64_t)m;
+      } else if (rtype == 3 || rtype == 4) {
+        uint64_t m = rtype == 3 ? 6 : 8;
+        if (read_into(nullptr, m) < m)
+          fail(fmt("could not read %s address: could not read EUI address: %s", rtype == 3 ? "EUI-48" : "EUI-64",
+                   kUnexpectedEOF));
+        alen = 24;  // newHWAddress(r.buf[:]) clones the whole 24-byte buffer
+      } else if (rtype == 0) {
+        break;
+      } else {
+        uint64_t m = (uint64_t)(length + padding);
+        if (m > avail()) {
+          if (!eof) throw NeedMore{};
+          pos = n;
+          fail(fmt("could not discard unknown name record: %s", kUnexpectedEOF));
+        }
+        pos += m;
+        blen -= (uint32_t)m;
+        continue;
+      }
+      blen -= (uint32_t)length;
+      length -= alen;
+      while (length > 0) {  // bufio.Reader.ReadBytes(0)
+        const void* z = memchr(b + pos, 0, avail());
+        if (!z) {
+          if (!eof) throw NeedMore{};
+          pos = n;
+          fail(fmt("could not read name: %s", kEOF));
+        }
+        uint64_t k = (const uint8_t*)z - (b + pos) + 1;
+        pos += k;
+        length -= (int64_t)k;
+      }
+      discard((uint64_t)padding);
+    }
+    discard(blen);
+  }
+
+  void read_packet_header() {
+    for (;;) {  // RESTART
+      for (;;) {  // FIND_PACKET
+        read_block();
+        if (typ == kEPB) {
+          const uint8_t* h = read_view(20);
+          blen -= 20;
+          uint32_t idx = ld32(h, be());
+          if (idx >= st.ifaces.size())
+            fail(fmt("Interface id %u not present in section (have only %zu interfaces)", idx, st.ifaces.size()));
+          ci_iface = idx;
+          convert_time(idx, (uint64_t)ld32(h + 4, be()) << 32 | ld32(h + 8, be()), &ci_s, &ci_ns);
+          ci_caplen = ld32(h + 12, be());
+          ci_len = ld32(h + 16, be());
+          break;
+        } else if (typ == kSPB) {
+          const uint8_t* h = read_view(4);
+          blen -= 4;
+          ci_s = kZeroTimeSec;
+          ci_ns = 0;
+          ci_iface = 0;
+          ci_len = ld32(h, be());
+          ci_caplen = ci_len;
+          if (st.ifaces.empty()) fail("At least one Interface is needed for a packet");
+          if (st.ifaces[0].snap != 0 && ci_caplen > st.ifaces[0].snap) ci_caplen = st.ifaces[0].snap;
+          break;
+        } else if (typ == kIDB) {
+          read_interface_descriptor();
+        } else if (typ == kISB) {
+          read_interface_statistics();
+        } else if (typ == kSHB) {
+          read_section_header();
+        } else if (typ == kPB) {
+          const uint8_t* h = read_view(20);
+          blen -= 20;
+          uint32_t idx = ld16(h, be());
+          if (idx >= st.ifaces.size())
+            fail(fmt("Interface id %u not present in section (have only %zu interfaces)", idx, st.ifaces.size()));
+          ci_iface = idx;
+          convert_time(idx, (uint64_t)ld32(h + 4, be()) << 32 | ld32(h + 8, be()), &ci_s, &ci_ns);
+          ci_caplen = ld32(h + 12, be());
+          ci_len = ld32(h + 16, be());
+          break;
+        } else if (typ == kNRB) {
+          read_name_resolution();
+        } else {
+          discard(blen);
+        }
+      }
+      if (!(flags & GPK_NG_WANT_MIXED_LINKTYPE)) {
+        if (st.ifaces[ci_iface].link_type != st.link_type) {
+          discard(blen);
+          if (flags & GPK_NG_ERROR_ON_MISMATCHING_LINKTYPE)
+            fail("Link type of current interface is different from first one");
+          continue;
+        }
+      }
+      return;
+    }
+  }
+
+  void read_packet_options() {
+    for (;;) {
+      read_option();
+      if (opt_code == 0) return;
+      if ((opt_code == 2 || opt_code == 6) && opt.len < 4)  // binary.LittleEndian.Uint32: _ = b[3]
+        fail(fmt("runtime error: index out of range [3] with length %u", opt.len), true);
+      if ((opt_code == 4 || opt_code == 5) && opt.len < 8)  // binary.LittleEndian.Uint64: _ = b[7]
+        fail(fmt("runtime error: index out of range [7] with length %u", opt.len), true);
+    }
+  }
+
+  // One ReadPacketDataWithOptions; returns the data offset in the chunk.
+  uint64_t ng_read_packet() {
+    read_packet_header();
+    const uint64_t off = pos;
+    if (ci_caplen > avail()) {
+      if (!eof) throw NeedMore{};
+      pos = n;
+      fail(kUnexpectedEOF);
+    }
+    pos += ci_caplen;
+    blen -= ci_caplen;
+    uint32_t pad = (4 - (ci_caplen & 3)) & 3;
+    if (pad > 0) discard(pad);
+    if (typ == kEPB) read_packet_options();
+    discard(blen);
+    return off;
+  }
+
+  void ng_open() {
+    if (avail() < 2) {  // reader.r.Peek(2)
+      if (!eof) throw NeedMore{};
+      fail(avail() > 0 ? kUnexpectedEOF : kEOF);
+    }
+    read_block();
+    if (typ != kSHB) fail(fmt("Unknown magic %x", typ));
+    read_section_header();
+  }
+
+  // ---- pcap ------------------------------------------------------------------
+  void pcap_open() {
+    if (avail() < 2) {  // br.Peek(2)
+      if (!eof) throw NeedMore{};
+      fail(kEOF);
+    }
+    if (avail() < 24) {  // io.ReadFull(r.r, buf[24])
+      if (!eof) throw NeedMore{};
+      pos = n;
+      fail(kUnexpectedEOF);
+    }
+    const uint8_t* h = b + pos;
+    pos += 24;
+    uint32_t magic = ld32(h, false);
+    if (magic == 0xA1B23C4D) {
+      pbe = false, factor = 1;
+    } else if (magic == 0x4D3CB2A1) {
+      pbe = true, factor = 1;
+    } else if (magic == 0xA1B2C3D4) {
+      pbe = false, factor = 1000;
+    } else if (magic == 0xD4C3B2A1) {
+      pbe = true, factor = 1000;
+    } else {
+      fail(fmt("Unknown magic %x", magic));
+    }
+    major = ld16(h + 4, pbe);
+    if (major != 2) fail(fmt("Unknown major version %u", major));
+    minor = ld16(h + 6, pbe);
+    if (minor != 4) fail(fmt("Unknown minor version %u", minor));
+    snaplen = ld32(h + 16, pbe);
+    plink = ld32(h + 20, pbe) & 0xFFFF;  // layers.LinkType is uint16
+  }
+
+  uint64_t pcap_read_packet() {
+    if (avail() < 16) {  // io.ReadFull(r.r, r.buf[:16])
+      if (!eof) throw NeedMore{};
+      uint64_t k = avail();
+      pos = n;
+      fail(k == 0 ? kEOF : kUnexpectedEOF);
+    }
+    const uint8_t* h = b + pos;
+    pos += 16;
+    uint32_t sec = ld32(h, pbe), usec = ld32(h + 4, pbe);
+    unix_norm((int64_t)sec, (int64_t)(uint32_t)(usec * factor), &ci_s, &ci_ns);  // uint32 product wraps
+    ci_caplen = ld32(h + 8, pbe);
+    ci_len = ld32(h + 12, pbe);
+    ci_iface = 0;
+    if (ci_caplen > snaplen) fail(fmt("capture length exceeds snap length: %u > %u", ci_caplen, snaplen));
+    if (ci_caplen > ci_len) fail(fmt("capture length exceeds original packet length: %u > %u", ci_caplen, ci_len));
+    const uint64_t off = pos;
+    if (ci_caplen > avail()) {  // io.ReadFull(r.r, data)
+      if (!eof) throw NeedMore{};
+      uint64_t k = avail();
+      pos = n;
+      fail(k == 0 ? kEOF : kUnexpectedEOF);
+    }
+    pos += ci_caplen;
+    return off;
+  }
+};
+
+extern "C" {
+
+int gpk_capreader_create(gpk_capreader** out, int format, uint32_t flags) {
+  if (!out || (format != GPK_CAP_PCAP && format != GPK_CAP_PCAPNG)) return GPK_EINVAL;
+  if (flags & ~7u) return GPK_EINVAL;
+  gpk_capreader* r = new (std::nothrow) gpk_capreader();
+  if (!r) return GPK_ENOMEM;
+  r->format = format;
+  r->flags = format == GPK_CAP_PCAPNG ? flags : 0;
+  *out = r;
+  return GPK_OK;
+}
+
+int gpk_capreader_destroy(gpk_capreader* r) {
+  delete r;
+  return GPK_OK;
+}
+
+int gpk_capreader_index(gpk_capreader* r, const uint8_t* buf, uint64_t len, int eof, uint64_t* offsets,
+                        uint32_t* caplens, gpk_capture_info* ci, uint64_t max_pkts, uint64_t* n_pkts,
+                        uint64_t* consumed) {
+  if (!r || (!buf && len) || !offsets || !caplens || !n_pkts || !consumed) return GPK_EINVAL;
+  *n_pkts = 0;
+  *consumed = 0;
+  if (r->open_failed) return GPK_CAP_END;  // NewReader/NewNgReader failed: no reader
+  r->b = buf;
+  r->n = len;
+  r->pos = 0;
+  r->eof = eof != 0;
+  const bool ng = r->format == GPK_CAP_PCAPNG;
+  const bool mixed = (r->flags & GPK_NG_WANT_MIXED_LINKTYPE) != 0;
+  uint64_t k = 0;
+  int status = GPK_CAP_MORE;
+  try {
+    if (!r->opened) {
+      r->st_saved = r->opt_saved = false;
+      try {
+        if (ng)
+          r->ng_open();
+        else
+          r->pcap_open();
+      } catch (NeedMore&) {
+        r->st = NgState();
+        r->opt = OptBuf();
+        r->pos = 0;
+        throw;
+      } catch (GoErr& e) {
+        r->open_failed = true;
+        r->err_text = e.text;
+        r->err_eof = e.text == kEOF;
+        r->err_panic = e.panic;
+        *consumed = r->pos;
+        return GPK_CAP_END;
+      }
+      r->opened = true;
+    }
+    for (;;) {
+      if (k == max_pkts) {
+        status = GPK_CAP_FULL;
+        break;
+      }
+      const uint64_t start = r->pos;
+      r->st_saved = r->opt_saved = false;
+      try {
+        const uint64_t off = ng ? r->ng_read_packet() : r->pcap_read_packet();
+        offsets[k] = off;
+        caplens[k] = r->ci_caplen;
+        if (ci) {
+          ci[k].ts_sec = r->ci_s;
+          ci[k].ts_nsec = r->ci_ns;
+          ci[k].length = r->ci_len;
+          ci[k].iface = (int32_t)r->ci_iface;
+          ci[k].link_type = (ng && mixed) ? (int32_t)r->st.ifaces[r->ci_iface].link_type : -1;
+        }
+        k++;
+      } catch (NeedMore&) {
+        if (r->st_saved) r->st = std::move(r->st_snap);
+        if (r->opt_saved) r->opt = std::move(r->opt_snap);
+        r->pos = start;
+        status = GPK_CAP_MORE;
+        break;
+      } catch (GoErr& e) {
+        r->err_text = e.text;
+        r->err_eof = e.text == kEOF;
+        r->err_panic = e.panic;
+        status = GPK_CAP_END;
+        break;
+      }
+    }
+  } catch (NeedMore&) {
+    status = GPK_CAP_MORE;
+  } catch (...) {
+    return GPK_ENOMEM;
+  }
+  *n_pkts = k;
+  *consumed = r->pos;
+  return status;
+}
+
+int gpk_capreader_error(const gpk_capreader* r, char* buf, size_t cap, int* is_eof, int* is_panic) {
+  if (!r) return GPK_EINVAL;
+  if (is_eof) *is_eof = r->err_eof;
+  if (is_panic) *is_panic = r->err_panic;
+  if (buf && cap) snprintf(buf, cap, "%s", r->err_text.c_str());
+  return (int)r->err_text.size();
+}
+
+int gpk_capreader_link_type(const gpk_capreader* r) {
+  if (!r) return GPK_EINVAL;
+  return r->format == GPK_CAP_PCAP ? (int)r->plink : (int)r->st.link_type;
+}
+
+int gpk_capreader_pcap_header(const gpk_capreader* r, uint32_t* snaplen, uint16_t* major, uint16_t* minor,
+                              int* nanosecond) {
+  if (!r || r->format != GPK_CAP_PCAP) return GPK_EINVAL;
+  if (snaplen) *snaplen = r->snaplen;
+  if (major) *major = r->major;
+  if (minor) *minor = r->minor;
+  if (nanosecond) *nanosecond = r->factor == 1;
+  return GPK_OK;
+}
+
+int gpk_capreader_nsections(const gpk_capreader* r) {
+  if (!r) return GPK_EINVAL;
+  return (int)r->st.ended.size();
+}
+
+static const Section* section_at(const gpk_capreader* r, int s, const std::vector<Iface>** ifaces) {
+  if (!r || r->format != GPK_CAP_PCAPNG || s < 0 || s > (int)r->st.ended.size()) return nullptr;
+  if (s == (int)r->st.ended.size()) {
+    *ifaces = &r->st.ifaces;
+    return &r->st.section;
+  }
+  *ifaces = &r->st.ended[s].second;
+  return &r->st.ended[s].first;
+}
+
+static int put_str(const std::string& s, char* buf, size_t cap) {
+  if (buf && cap) {
+    size_t m = s.size() < cap - 1 ? s.size() : cap - 1;
+    memcpy(buf, s.data(), m);
+    buf[m] = 0;
+  }
+  return (int)s.size();
+}
+
+int gpk_capreader_section_info(const gpk_capreader* r, int s, int field, char* buf, size_t cap) {
+  const std::vector<Iface>* ifs;
+  const Section* sec = section_at(r, s, &ifs);
+  if (!sec) return GPK_EINVAL;
+  switch (field) {
+    case GPK_SECTION_COMMENT: return put_str(sec->comment, buf, cap);
+    case GPK_SECTION_HARDWARE: return put_str(sec->hardware, buf, cap);
+    case GPK_SECTION_OS: return put_str(sec->os, buf, cap);
+    case GPK_SECTION_APPLICATION: return put_str(sec->application, buf, cap);
+  }
+  return GPK_EINVAL;
+}
+
+int gpk_capreader_ninterfaces(const gpk_capreader* r, int s) {
+  const std::vector<Iface>* ifs;
+  if (!section_at(r, s, &ifs)) return GPK_EINVAL;
+  return (int)ifs->size();
+}
+
+int gpk_capreader_interface(const gpk_capreader* r, int s, int i, gpk_ng_interface* out) {
+  const std::vector<Iface>* ifs;
+  if (!section_at(r, s, &ifs) || i < 0 || i >= (int)ifs->size() || !out) return GPK_EINVAL;
+  const Iface& it = (*ifs)[i];
+  memset(out, 0, sizeof(*out));
+  out->link_type = it.link_type;
+  out->ts_resolution = it.tsres;
+  out->has_statistics = it.has_stats;
+  out->snap_length = it.snap;
+  out->ts_offset = it.tsoff;
+  out->last_update_sec = it.stats.lu_s;
+  out->last_update_nsec = it.stats.lu_ns;
+  out->start_time_sec = it.stats.st_s;
+  out->start_time_nsec = it.stats.st_ns;
+  out->end_time_sec = it.stats.et_s;
+  out->end_time_nsec = it.stats.et_ns;
+  out->packets_received = it.stats.received;
+  out->packets_dropped = it.stats.dropped;
+  return GPK_OK;
+}
+
+int gpk_capreader_interface_str(const gpk_capreader* r, int s, int i, int field, char* buf, size_t cap) {
+  const std::vector<Iface>* ifs;
+  if (!section_at(r, s, &ifs) || i < 0 || i >= (int)ifs->size()) return GPK_EINVAL;
+  const Iface& it = (*ifs)[i];
+  switch (field) {
+    case GPK_IFACE_NAME: return put_str(it.name, buf, cap);
+    case GPK_IFACE_COMMENT: return put_str(it.comment, buf, cap);
+    case GPK_IFACE_DESCRIPTION: return put_str(it.description, buf, cap);
+    case GPK_IFACE_FILTER: return put_str(it.filter, buf, cap);
+    case GPK_IFACE_OS: return put_str(it.os, buf, cap);
+    case GPK_IFACE_STATS_COMMENT: return put_str(it.stats.comment, buf, cap);
+  }
+  return GPK_EINVAL;
+}
+
+}  // extern "C"

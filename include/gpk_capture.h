@@ -1,0 +1,161 @@
+/*
+ * gpk_capture.h — capture-file ingest for the batch decoder.
+ *
+ * The path of BASELINE config C5: a pcap / pcapng file is read into pinned
+ * staging buffers, indexed IN PLACE (a packet's bytes stay where the file put
+ * them: the staging buffer is the packed batch, offsets point into it), copied
+ * to HBM and decoded. This header replaces, for a Go caller binding it through
+ * cgo:
+ *
+ *   gpk_capreader_create(GPK_CAP_PCAPNG)  pcapgo.NewNgReader(r, NgReaderOptions)
+ *                                         pcapgo/ngread.go:64-106; options :23-37
+ *   gpk_capreader_create(GPK_CAP_PCAP)    pcapgo.NewReader(r)            pcapgo/read.go:64-122
+ *   gpk_capreader_index                   a loop of ReadPacketData calls
+ *                                         pcapgo/ngread.go:642-675 (ReadPacketDataWithOptions,
+ *                                         reached through ReadPacketData :636-640 and the
+ *                                         ZeroCopy variants :683-716), pcapgo/read.go:124-140
+ *   gpk_capreader_link_type               NgReader.LinkType() ngread.go:719 / Reader.LinkType() read.go:183
+ *   gpk_capreader_section_* / _interface* NgReader.SectionInfo() :724, Interface(i) :729,
+ *                                         NInterfaces() :737, SectionEndCallback (:33)
+ *   gpk_replay_file                       the C5 loop: NgReader/Reader + DecodingLayerParser
+ *                                         over a whole file, pipelined through HBM
+ *
+ * Semantics are the reference's byte for byte, including its accounting
+ * quirks: the indexer is a restatement of pcapgo's
+ * bufio-stream reader, fed in chunks. Gzip-compressed files are inflated by
+ * the file layer (gpk_replay_file) before indexing, as pcapgo does
+ * transparently (read.go:74-84, ngread.go:80-95).
+ */
+#ifndef GPK_CAPTURE_H
+#define GPK_CAPTURE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "gpk.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GPK_CAP_PCAP 1
+#define GPK_CAP_PCAPNG 2
+
+/* NgReaderOptions (ngread.go:23-37) */
+#define GPK_NG_WANT_MIXED_LINKTYPE 0x1u
+#define GPK_NG_ERROR_ON_MISMATCHING_LINKTYPE 0x2u
+#define GPK_NG_SKIP_UNKNOWN_VERSION 0x4u
+
+/* gopacket.CaptureInfo (packet.go) of one packet. Timestamp = time.Unix(ts_sec,
+ * ts_nsec).UTC(); the zero time.Time (simple packet blocks) is ts_sec =
+ * -62135596800, ts_nsec = 0, which is what Time{}.Unix() returns. */
+typedef struct gpk_capture_info {
+  int64_t ts_sec;
+  uint32_t ts_nsec;
+  uint32_t length;    /* Length (original packet length)                      */
+  int32_t iface;      /* InterfaceIndex                                       */
+  int32_t link_type;  /* AncillaryData[0] with WantMixedLinkType, else -1     */
+} gpk_capture_info;
+
+typedef struct gpk_capreader gpk_capreader;
+
+int gpk_capreader_create(gpk_capreader** out, int format, uint32_t ng_flags);
+int gpk_capreader_destroy(gpk_capreader* r);
+
+/* gpk_capreader_index return values (>= 0) */
+#define GPK_CAP_MORE 0 /* every whole record of buf was read: feed buf[consumed..] + more bytes */
+#define GPK_CAP_FULL 1 /* max_pkts packets written: call again with buf[consumed..]       */
+#define GPK_CAP_END 2  /* ReadPacketData returned an error (io.EOF included): see
+                          gpk_capreader_error. Calling again continues like another
+                          ReadPacketData call after that error would.                 */
+
+/* Index the packets of buf[0, len) — the capture stream from the reader's
+ * current position on; eof != 0 when no byte follows buf[len-1]. Writes up to
+ * max_pkts packets: data of packet i is buf[offsets[i], offsets[i]+caplens[i]),
+ * its CaptureInfo is ci[i] (ci may be NULL). *consumed = the stream bytes the
+ * reader is done with; every written packet lies in buf[0, *consumed). The
+ * next call must pass the stream from buf + *consumed on. A record longer
+ * than the bytes available returns GPK_CAP_MORE with *consumed possibly 0:
+ * pass a longer buffer. Packets the reference returns together with an error
+ * (a failed ReadPacketData) are not written. */
+int gpk_capreader_index(gpk_capreader* r, const uint8_t* buf, uint64_t len, int eof, uint64_t* offsets,
+                        uint32_t* caplens, gpk_capture_info* ci, uint64_t max_pkts, uint64_t* n_pkts,
+                        uint64_t* consumed);
+
+/* The error that ended the last GPK_CAP_END: the Go error text (io.EOF is
+ * "EOF"); *is_eof = it is io.EOF; *is_panic = the reference panics there
+ * (a runtime error its code does not recover). Returns the text length. */
+int gpk_capreader_error(const gpk_capreader* r, char* buf, size_t cap, int* is_eof, int* is_panic);
+
+/* Reader.LinkType() / NgReader.LinkType() (0 with WantMixedLinkType). */
+int gpk_capreader_link_type(const gpk_capreader* r);
+/* pcap header fields: snaplen, version, nanosecond resolution (read.go:96-121). */
+int gpk_capreader_pcap_header(const gpk_capreader* r, uint32_t* snaplen, uint16_t* major, uint16_t* minor,
+                              int* nanosecond);
+
+/* pcapng sections: sections 0 .. nsections-1 ended (the SectionEndCallback
+ * calls, ngread.go:241-248); section == nsections is the current one. */
+int gpk_capreader_nsections(const gpk_capreader* r);
+#define GPK_SECTION_COMMENT 0
+#define GPK_SECTION_HARDWARE 1
+#define GPK_SECTION_OS 2
+#define GPK_SECTION_APPLICATION 3
+/* NgSectionInfo string field; returns its length (bytes may include NUL). */
+int gpk_capreader_section_info(const gpk_capreader* r, int section, int field, char* buf, size_t cap);
+int gpk_capreader_ninterfaces(const gpk_capreader* r, int section);
+
+/* NgInterface (pcapgo/pcapng.go) numeric fields and statistics. */
+typedef struct gpk_ng_interface {
+  uint16_t link_type;
+  uint8_t ts_resolution;
+  uint8_t has_statistics;
+  uint32_t snap_length;
+  uint64_t ts_offset;
+  int64_t last_update_sec, start_time_sec, end_time_sec;
+  uint32_t last_update_nsec, start_time_nsec, end_time_nsec, _pad;
+  uint64_t packets_received, packets_dropped;
+} gpk_ng_interface;
+int gpk_capreader_interface(const gpk_capreader* r, int section, int index, gpk_ng_interface* out);
+#define GPK_IFACE_NAME 0
+#define GPK_IFACE_COMMENT 1
+#define GPK_IFACE_DESCRIPTION 2
+#define GPK_IFACE_FILTER 3
+#define GPK_IFACE_OS 4
+#define GPK_IFACE_STATS_COMMENT 5
+int gpk_capreader_interface_str(const gpk_capreader* r, int section, int index, int field, char* buf, size_t cap);
+
+/* ---- whole-file replay through the GPU (BASELINE config C5) -------------- */
+typedef struct gpk_replay_opts {
+  int format;            /* GPK_CAP_PCAP / GPK_CAP_PCAPNG, 0 = from the magic */
+  uint32_t ng_flags;     /* GPK_NG_* */
+  uint64_t slot_bytes;   /* file bytes per pinned staging slot (default 256 MiB) */
+  int slots;             /* staging slots in flight (default 4)                 */
+  uint64_t batch_pkts;   /* packets per device launch (default 2 Mi)            */
+  int read_threads;      /* pread threads per slot (default 8)                  */
+} gpk_replay_opts;
+
+typedef struct gpk_replay_stats {
+  uint64_t packets, packet_bytes, file_bytes, stream_bytes, batches, slots;
+  double wall_s;         /* open .. last result delivered                        */
+  double read_s;         /* file -> pinned staging (read threads, busy time)     */
+  double index_s;        /* record walk (gpk_capreader_index)                    */
+  double gpu_s;          /* HtoD + decode + DtoH, summed over batches            */
+  double kernel_s;       /* decode kernels alone                                 */
+  double deliver_s;      /* result callback                                      */
+  int reader_status;     /* the GPK_CAP_END error: 0 = io.EOF (clean end)        */
+  char error[160];
+} gpk_replay_stats;
+
+/* Results of one device launch, in packet order, delivered on the calling
+ * thread: host arrays valid during the call only. */
+typedef void (*gpk_replay_cb)(void* user, uint64_t first_packet, uint64_t n, const gpk_record* records,
+                              const uint32_t* err_args, const uint64_t* flows, const gpk_capture_info* ci,
+                              const uint32_t* caplens);
+
+int gpk_replay_file(gpk_ctx* ctx, const gpk_parser* p, const char* path, const gpk_replay_opts* opts,
+                    gpk_replay_cb cb, void* user, gpk_replay_stats* stats);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GPK_CAPTURE_H */

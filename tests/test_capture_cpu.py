@@ -1,0 +1,321 @@
+"""Native capture indexer (libgpk gpk_capreader_*, host code, no GPU) against the
+pcapgo oracle (oracle/pcapgo_oracle.py, pinned by tests/test_pcapgo_oracle.py).
+
+Bit-exact on every packet (stream offset, caplen, CaptureInfo), the error
+that ends the stream (Go text and panic flag) and the section/interface
+metadata; fed whole and in chunks of many sizes (the resumable walk must not
+depend on where a chunk ends); on the reference's fixtures, on generated
+edge-case captures and on mutated (fuzzed) captures.
+"""
+import ctypes
+import gzip
+import os
+import random
+
+import numpy as np
+import pytest
+
+import pcapgen
+from gopacket_amd import _lib, pcapgo
+from oracle import pcapgo_oracle as PO
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "pcapgo")
+FILES = sorted([os.path.join(be, f) for be in ("le", "be") for f in os.listdir(os.path.join(GOLD, be))]) + ["epb.pcapng"]
+FLAG_SETS = [0, 1, 2, 4, 6, 7]
+
+
+def native_events(stream, fmt, flags, chunk=None, max_pkts=1 << 30, errors=1, max_events=100000):
+    """Drive gpk_capreader_index like a ReadPacketData loop; returns events:
+    ("pkt", abs_offset, caplen, ts_sec, ts_nsec, length, iface, ancil) or ("err", text, panic)."""
+    L = _lib.lib()
+    h = ctypes.c_void_p()
+    _lib.check(L.gpk_capreader_create(ctypes.byref(h), fmt, flags))
+    ev = []
+    base, have = 0, (len(stream) if chunk is None else min(len(stream), chunk))
+    nerr = 0
+    try:
+        while len(ev) < max_events:
+            buf = np.frombuffer(stream[base:have], np.uint8) if have > base else np.zeros(1, np.uint8)
+            m = max(1, min(max_pkts, 4096))
+            off = np.empty(m, np.uint64)
+            cap = np.empty(m, np.uint32)
+            ci = np.empty(m, _lib.CAPINFO_DTYPE)
+            n, used = ctypes.c_uint64(), ctypes.c_uint64()
+            eof = have >= len(stream)
+            rc = L.gpk_capreader_index(h, buf.ctypes.data, have - base, int(eof), off.ctypes.data, cap.ctypes.data,
+                                       ci.ctypes.data, m, ctypes.byref(n), ctypes.byref(used))
+            assert rc >= 0, rc
+            for i in range(n.value):
+                r = ci[i]
+                assert int(off[i]) + int(cap[i]) <= used.value
+                ev.append(("pkt", base + int(off[i]), int(cap[i]), int(r["ts_sec"]), int(r["ts_nsec"]),
+                           int(r["length"]), int(r["iface"]), None if int(r["link_type"]) < 0 else int(r["link_type"])))
+            base += used.value
+            if rc == _lib.CAP_END:
+                b = ctypes.create_string_buffer(512)
+                e, p = ctypes.c_int(), ctypes.c_int()
+                k = L.gpk_capreader_error(h, b, 512, ctypes.byref(e), ctypes.byref(p))
+                ev.append(("err", b.raw[:k].decode("latin-1"), bool(p.value)))
+                nerr += 1
+                if bool(e.value) or nerr >= errors:
+                    break
+            elif rc == _lib.CAP_MORE:
+                assert not eof
+                have = len(stream) if chunk is None else min(len(stream), have + chunk)
+        meta = native_meta(L, h, fmt)
+    finally:
+        L.gpk_capreader_destroy(h)
+    return ev, meta
+
+
+def native_meta(L, h, fmt):
+    if fmt != _lib.CAP_PCAPNG:
+        return None
+
+    def s(fn, *a):
+        n = fn(h, *a, None, 0)
+        if n < 0:
+            return None
+        b = ctypes.create_string_buffer(n + 1)
+        fn(h, *a, b, n + 1)
+        return b.raw[:n]
+
+    out = []
+    for sec in range(L.gpk_capreader_nsections(h) + 1):
+        info = dict(comment=s(L.gpk_capreader_section_info, sec, 0), hardware=s(L.gpk_capreader_section_info, sec, 1),
+                    os=s(L.gpk_capreader_section_info, sec, 2), application=s(L.gpk_capreader_section_info, sec, 3))
+        ifs = []
+        for i in range(L.gpk_capreader_ninterfaces(h, sec)):
+            x = _lib.NgInterface()
+            assert L.gpk_capreader_interface(h, sec, i, ctypes.byref(x)) == 0
+            f = L.gpk_capreader_interface_str
+            ifs.append(dict(name=s(f, sec, i, 0), comment=s(f, sec, i, 1), description=s(f, sec, i, 2),
+                            filter=s(f, sec, i, 3), os=s(f, sec, i, 4), link_type=x.link_type,
+                            ts_resolution=x.ts_resolution, ts_offset=x.ts_offset, snap_length=x.snap_length,
+                            stats=dict(last_update=(x.last_update_sec, x.last_update_nsec),
+                                       start_time=(x.start_time_sec, x.start_time_nsec),
+                                       end_time=(x.end_time_sec, x.end_time_nsec), comment=s(f, sec, i, 5),
+                                       received=x.packets_received, dropped=x.packets_dropped)))
+        out.append((info, ifs))
+    return out
+
+
+def oracle_events(stream, fmt, flags, errors=1, max_events=100000):
+    kw = dict(want_mixed=bool(flags & 1), error_on_mismatch=bool(flags & 2), skip_unknown_version=bool(flags & 4))
+    try:
+        r = PO.NgReader(stream, **kw) if fmt == _lib.CAP_PCAPNG else PO.Reader(stream)
+    except PO.GoError as e:
+        return [("err", e.text, e.panic)], "open"
+    ev = []
+    nerr = 0
+    while len(ev) < max_events:
+        try:
+            p = r.read_packet()
+            ev.append(("pkt",) + p.key())
+        except PO.GoError as e:
+            ev.append(("err", e.text, e.panic))
+            nerr += 1
+            if e.text == "EOF" or nerr >= errors:
+                break
+    meta = None
+    if fmt == _lib.CAP_PCAPNG:
+        meta = list(r.ended_sections) + [r.section_state()]
+    return ev, meta
+
+
+def compare(stream, fmt, flags, chunk=None, errors=1):
+    want, wmeta = oracle_events(stream, fmt, flags, errors=errors)
+    if wmeta == "open":  # NewReader failed: there is no reader to call again
+        errors = 1
+    got, gmeta = native_events(stream, fmt, flags, chunk=chunk, errors=errors)
+    assert got == want
+    if wmeta != "open" and fmt == _lib.CAP_PCAPNG:
+        assert gmeta == wmeta
+    return want
+
+
+@pytest.mark.parametrize("f", FILES)
+@pytest.mark.parametrize("flags", FLAG_SETS)
+def test_fixtures_match_oracle(f, flags):
+    data = open(os.path.join(GOLD, f), "rb").read()
+    ev = compare(data, _lib.CAP_PCAPNG, flags)
+    assert ev[-1][0] == "err"
+    for chunk in (1, 13, 64, 333, 4096):
+        if len(data) // chunk > 3000:
+            continue
+        compare(data, _lib.CAP_PCAPNG, flags, chunk=chunk)
+
+
+def test_errors_can_be_read_past():
+    """After an error, the next ReadPacketData continues from where Go's reader stands."""
+    for f in ("le/test006.pcapng", "be/test006.pcapng", "le/test901.pcapng"):
+        data = open(os.path.join(GOLD, f), "rb").read()
+        for flags in (2, 0):
+            compare(data, _lib.CAP_PCAPNG, flags, errors=5)
+
+
+def edge_captures():
+    bo_cases = []
+    for bo in ("<", ">"):
+        shb = pcapgen.shb(bo, options=pcapgen.opt(1, b"c", bo) + pcapgen.opt(2, b"hw", bo) + pcapgen.end_opt(bo))
+        idb = pcapgen.idb(1, 0, bo, options=pcapgen.opt(2, b"eth0", bo) + pcapgen.opt(9, b"\x89", bo) +
+                          pcapgen.opt(14, (5).to_bytes(8, "big" if bo == ">" else "little"), bo) + pcapgen.end_opt(bo))
+        pk = [bytes(range(i % 256)) * 3 for i in range(20)]
+        bo_cases += [
+            shb + idb + b"".join(pcapgen.epb(p, ts=i * 7777777, bo=bo) for i, p in enumerate(pk)),
+            shb + idb + b"".join(pcapgen.spb(p, bo=bo) for p in pk),
+            shb + idb + b"".join(pcapgen.pb(p, ts=i, bo=bo) for i, p in enumerate(pk)),
+            # name resolution + decryption secrets + statistics between packets
+            shb + pcapgen.nrb([(1, b"\x0a\x00\x00\x01host\x00"), (3, b"\x01\x02\x03\x04\x05\x06mac\x00"),
+                               (9, b"xyz")], bo) + pcapgen.dsb(0x544c534b, b"secret", bo) + idb +
+            pcapgen.epb(pk[5], bo=bo) + pcapgen.isb(0, 99, bo, options=pcapgen.opt(4, (3).to_bytes(8, "little"), bo) +
+                                                  pcapgen.end_opt(bo)) + pcapgen.epb(pk[6], bo=bo),
+            # EPB options, including ones the reference panics on
+            shb + idb + pcapgen.epb(pk[7], bo=bo, options=pcapgen.opt(2, b"\x01\x00\x00\x00", bo) + pcapgen.end_opt(bo)),
+            shb + idb + pcapgen.epb(pk[7], bo=bo, options=pcapgen.opt(2, b"\x01", bo) + pcapgen.end_opt(bo)),
+            shb + idb + pcapgen.epb(pk[7], bo=bo, options=pcapgen.opt(4, b"\x01\x02", bo) + pcapgen.end_opt(bo)),
+            # second section with another byte order, an unknown block, a bad interface id
+            shb + idb + pcapgen.epb(pk[3], bo=bo) + pcapgen.shb(">" if bo == "<" else "<") +
+            pcapgen.idb(0, 0, ">" if bo == "<" else "<") + pcapgen.block(0x777, b"abcd", bo) +
+            pcapgen.epb(pk[4], bo=">" if bo == "<" else "<"),
+            shb + idb + pcapgen.epb(pk[3], iface=3, bo=bo),
+            # resolution exponent 64: the reference panics (divide by zero)
+            shb + pcapgen.idb(1, 0, bo, options=pcapgen.opt(9, b"\x40", bo) + pcapgen.end_opt(bo)),
+            shb + pcapgen.idb(1, 0, bo, options=pcapgen.opt(9, b"\x86", bo) + pcapgen.end_opt(bo)) +
+            pcapgen.epb(pk[9], ts=(1 << 40) + 12345, bo=bo),
+            # zero-length options keep the previous option value
+            shb + pcapgen.idb(1, 0, bo, options=pcapgen.opt(2, b"name", bo) + pcapgen.opt(1, b"", bo) +
+                              pcapgen.end_opt(bo)) + pcapgen.epb(pk[2], bo=bo),
+            # packet blocks before any interface, version mismatch
+            shb + pcapgen.epb(pk[2], bo=bo),
+            pcapgen.shb(bo, major=2) + idb + pcapgen.epb(pk[2], bo=bo) + shb + idb + pcapgen.epb(pk[3], bo=bo),
+        ]
+    return bo_cases
+
+
+@pytest.mark.parametrize("k", range(len(edge_captures())))
+def test_edge_captures(k):
+    data = edge_captures()[k]
+    for flags in FLAG_SETS:
+        compare(data, _lib.CAP_PCAPNG, flags)
+        compare(data, _lib.CAP_PCAPNG, flags, chunk=17)
+        compare(data, _lib.CAP_PCAPNG, flags, errors=4)
+
+
+def mutate(rng, data):
+    d = bytearray(data)
+    kind = rng.randrange(4)
+    if kind == 0:  # flip bytes
+        for _ in range(rng.randrange(1, 4)):
+            i = rng.randrange(len(d))
+            d[i] = rng.randrange(256)
+    elif kind == 1:  # truncate
+        d = d[:rng.randrange(len(d) + 1)]
+    elif kind == 2:  # small length-field perturbation
+        i = rng.randrange(0, max(1, len(d) - 4)) & ~3
+        d[i] = (d[i] + rng.choice((1, 3, 4, 252, 255))) & 0xFF
+    else:  # splice a random slice elsewhere
+        a = rng.randrange(len(d))
+        b = min(len(d), a + rng.randrange(1, 64))
+        j = rng.randrange(len(d))
+        d = d[:j] + d[a:b] + d[j:]
+    return bytes(d)
+
+
+def test_fuzz_pcapng_matches_oracle():
+    rng = random.Random(1234)
+    seeds = [open(os.path.join(GOLD, f), "rb").read() for f in FILES if os.path.getsize(os.path.join(GOLD, f)) < 3000]
+    seeds += [e for e in edge_captures()]
+    for it in range(1500):
+        data = mutate(rng, rng.choice(seeds))
+        flags = rng.choice(FLAG_SETS)
+        compare(data, _lib.CAP_PCAPNG, flags, errors=3)
+        if it % 10 == 0:
+            compare(data, _lib.CAP_PCAPNG, flags, chunk=rng.randrange(1, 200), errors=3)
+
+
+def pcap_cases():
+    pk = [bytes([i]) * (i * 5 % 97) for i in range(30)]
+    out = []
+    for bo in ("<", ">"):
+        for nano in (False, True):
+            out.append(pcapgen.pcap_file(pk, bo=bo, nano=nano))
+        out.append(pcapgen.pcap_file(pk, bo=bo, snaplen=50))  # "capture length exceeds snap length"
+    return out
+
+
+def test_pcap_matches_oracle():
+    rng = random.Random(99)
+    cases = pcap_cases()
+    for c in cases:
+        for chunk in (None, 1, 7, 100):
+            compare(c, _lib.CAP_PCAP, 0, chunk=chunk, errors=6)
+    for _ in range(800):
+        data = mutate(rng, rng.choice(cases))
+        compare(data, _lib.CAP_PCAP, 0, errors=4)
+    # usec * 1000 wraps in uint32 (read.go:176): usec = 4294968 -> 4294968000 mod 2^32
+    hdr = pcapgen.pcap_file([])
+    rec = (5).to_bytes(4, "little") + (4294968).to_bytes(4, "little") + (2).to_bytes(4, "little") * 2 + b"ab"
+    ev = compare(hdr + rec, _lib.CAP_PCAP, 0)
+    assert ev[0][3:5] == (5, (4294968000 - (1 << 32)))
+
+
+def test_python_mirror_reads_like_pcapgo():
+    """gopacket_amd.pcapgo on the harvested test table (the same checks as ngRunFileReadTest)."""
+    import json
+    exp = json.load(open(os.path.join(GOLD, "expect.json")))
+    from test_pcapgo_oracle import b, want_iface
+    for t in exp["tests"]:
+        for be in ("le", "be"):
+            raw = open(os.path.join(GOLD, be, b(t["testName"]).decode() + ".pcapng"), "rb").read()
+            opts = pcapgo.NgReaderOptions(t["wantMixedLinkType"], t["errorOnMismatchingLinkType"],
+                                          t["skipUnknownVersion"])
+            r = pcapgo.NewNgReader(raw, opts)
+            assert r.LinkType() == (0 if t["wantMixedLinkType"] else t["linkType"])
+            for p in t["packets"]:
+                if "err" in p:
+                    with pytest.raises(pcapgo.PcapgoError) as e:
+                        r.ReadPacketData()
+                    assert e.value.text == p["err"]["err"]
+                    break
+                data, ci = r.ReadPacketData()
+                assert data == b(p["data"])
+                w = p["ci"]
+                assert ci.Timestamp == tuple(w["Timestamp"]["time"])
+                assert (ci.CaptureLength, ci.Length, ci.InterfaceIndex) == (w["CaptureLength"], w["Length"],
+                                                                           w.get("InterfaceIndex", 0))
+                assert ci.AncillaryData == (w.get("AncillaryData") or [])
+            else:
+                with pytest.raises(EOFError):
+                    r.ReadPacketData()
+                secs = r.SectionEnds() + [(r.SectionInfo(), [r.Interface(i) for i in range(r.NInterfaces())])]
+                assert len(secs) == len(t["sections"])
+                for (info, ifs), w in zip(secs, t["sections"]):
+                    wi = w["sectionInfo"]
+                    assert info.Comment == b(wi.get("Comment", {"str": ""}))
+                    assert info.Hardware == b(wi.get("Hardware", {"str": ""}))
+                    assert [i.Name for i in ifs] == [want_iface(x)["name"] for x in w.get("ifaces", [])]
+                    assert [i.Statistics.PacketsDropped for i in ifs] == \
+                        [want_iface(x)["stats"]["dropped"] for x in w.get("ifaces", [])]
+
+
+def test_python_mirror_gzip_and_batches():
+    raw = pcapgen.ng_file([bytes([i & 0xFF]) * (60 + i) for i in range(1000)])
+    for src in (raw, gzip.compress(raw)):
+        r = pcapgo.NewNgReader(src)
+        total = 0
+        while True:
+            try:
+                bt = r.ReadBatch(300)
+            except EOFError:
+                break
+            for i in range(len(bt)):
+                o, c = int(bt.offsets[i]), int(bt.caplens[i])
+                assert bytes(bt.data[o:o + c]) == bytes([(total + i) & 0xFF]) * (60 + total + i)
+            total += len(bt)
+        assert total == 1000
+    with pytest.raises(pcapgo.PcapgoError) as e:
+        pcapgo.NewNgReader(b"\x1f\x8b\x08")
+    assert e.value.text == "unexpected EOF"
+    with pytest.raises(EOFError):
+        pcapgo.NewNgReader(b"")

@@ -1,4 +1,4 @@
-"""libgpk.so on the CPU side only: it loads, exports every symbol include/gpk.h
+"""libgpk.so on the CPU side only: it loads, exports every symbol include/*.h
 declares, and its host-side pieces (parser configuration, error text, layer
 names) match the oracle. No GPU call is made here."""
 import ctypes
@@ -14,8 +14,11 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def header_functions():
-    src = open(os.path.join(ROOT, "include", "gpk.h")).read()
-    return sorted(set(re.findall(r"^(?:int|int64_t|const char\*)\s+(gpk_\w+)\(", src, re.M)))
+    names = set()
+    for h in sorted(os.listdir(os.path.join(ROOT, "include"))):
+        src = open(os.path.join(ROOT, "include", h)).read()
+        names |= set(re.findall(r"^(?:int|int64_t|const char\*)\s+(gpk_\w+)\(", src, re.M))
+    return sorted(names)
 
 
 def test_exports_every_declared_symbol():
