@@ -212,6 +212,70 @@ def pcie_inclusive(name, ctx, n=4 * 2**20, reps=5):
                 packets=n, note="gpk_decode_batch_host from pinned memory: HtoD + decode + DtoH")
 
 
+def c5_replay(ctx, gib=10.0, reps=2, threads=16):
+    """BASELINE config C5: a pcapng of the C4 IMIX mix (~gib GiB, written once
+    to $TMPDIR, in the page cache) replayed end to end by gpk_replay_file:
+    file -> pinned staging slots -> record walk -> HtoD -> decode -> DtoH ->
+    per-launch result callback (which counts valid checksums, as a consumer
+    would touch the results). Sampled packets are checked against the oracle."""
+    from gopacket_amd import _lib, engine, synth
+    from oracle import oracle as O
+    S = _lib.synth_lib()
+    cfg = CONFIGS["c4"]
+    parser = engine.ParserConfig(17, [engine.DECODER_KINDS[d] for d in cfg["decoders"]], outputs=cfg["outputs"])
+    per = S.gpk_synth_bytes(4, 0, 1 << 20) / (1 << 20) + 32 + 1.5  # frame + EPB header/trailer + padding
+    n = int(gib * 2**30 / per)
+    path = os.path.join(os.environ.get("TMPDIR", "/tmp"), "gpk_c5_%d.pcapng" % os.getpid())
+    t0 = time.perf_counter()
+    size = S.gpk_synth_write_pcapng(path.encode(), 4, 0, n, threads)
+    gen_s = time.perf_counter() - t0
+    if not size:
+        raise RuntimeError("could not write %s" % path)
+    rng = np.random.default_rng(5)
+    sample = sorted(set(int(x) for x in rng.integers(0, n, 2048)) | {0, n - 1})
+    picked = {}
+    valid = [0]
+
+    def on_batch(first, k, rec, err, fl, ci, cap):
+        valid[0] += int(np.count_nonzero(rec["status"] & _lib.ST_L4_VALID))
+        lo, hi = np.searchsorted(sample, first), np.searchsorted(sample, first + k)
+        for i in sample[lo:hi]:
+            j = i - first
+            picked[i] = (rec[j].copy(), fl[[j, k + j, 2 * k + j]].copy())
+
+    runs = []
+    try:
+        for _ in range(reps):
+            picked.clear()
+            valid[0] = 0
+            _, st = ctx.replay_file(parser, path, collect=False, on_batch=on_batch)
+            runs.append(st)
+    finally:
+        os.unlink(path)
+    st = min(runs, key=lambda x: x["wall_s"])
+    idx = sorted(picked)
+    pk = [synth.packet(4, i) for i in idx]
+    cap = np.array([len(x) for x in pk], np.uint32)
+    off = np.concatenate([[0], np.cumsum(cap[:-1], dtype=np.uint64)]).astype(np.uint64)
+    ref = O.OracleParser(17, ["ETHERNET", "DOT1Q", "IPV4", "IPV6", "IPV6_EXT", "TCP", "UDP", "PAYLOAD"]).decode(
+        np.frombuffer(b"".join(pk) + bytes(16), np.uint8), off, cap, layouts=False)
+    got = np.array([picked[i][0] for i in idx], _lib.RECORD_DTYPE)
+    gfl = np.stack([picked[i][1] for i in idx], axis=1).reshape(-1)
+    ok = (st["packets"] == n and st["error"] == "EOF" and len(idx) == len(sample)
+          and np.array_equal(got, ref["records"]) and np.array_equal(gfl, ref["flows"]))
+    w = st["wall_s"]
+    return dict(workload="C5: pcapng replay of the C4 IMIX mix, end to end incl. HtoD/DtoH",
+                packets=st["packets"], file_bytes=st["file_bytes"], value=round(st["packets"] / w / 1e6, 2),
+                unit="Mpkts/s", GBps=round(st["file_bytes"] / w / 1e9, 2), wall_s=round(w, 4),
+                runs_wall_s=[round(r["wall_s"], 4) for r in runs],
+                breakdown_s=dict(read=round(st["read_s"], 4), index=round(st["index_s"], 4),
+                                 gpu_copy_decode=round(st["gpu_s"], 4), kernel=round(st["kernel_s"], 4),
+                                 deliver=round(st["deliver_s"], 4)),
+                batches=st["batches"], slots=st["slots"], l4_valid=valid[0], write_s=round(gen_s, 2),
+                parity="%s (%d sampled packets vs oracle)" % ("bit-exact" if ok else "MISMATCH", len(idx)),
+                source="page-cached file in %s" % os.path.dirname(path))
+
+
 def load_traffic(name, n):
     """HBM bytes per launch of the decode kernel from the committed PMC
     profile (profiles/hbm_traffic.json, tools/make_profiles.py): measured
@@ -236,6 +300,8 @@ def main():
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--no-probe", action="store_true", help="skip the streaming-read reference kernel")
     ap.add_argument("--pcie", action="store_true", help="also time the host-buffer path (PCIe-inclusive)")
+    ap.add_argument("--c5", type=float, default=0.0, metavar="GIB",
+                    help="also run config C5: replay a GIB-GiB pcapng end to end (gpk_replay_file)")
     ap.add_argument("--tables", default="auto", choices=["auto", "global"],
                     help="next-layer tables: compact LDS copy (auto) or device-memory tables (global)")
     args = ap.parse_args()
@@ -287,6 +353,8 @@ def main():
                 "probe_read_GBps": s["probe_gbs"] and round(s["probe_gbs"], 1)}
         if args.pcie and world == 1:
             out["pcie_inclusive"] = pcie_inclusive(head, ctx)
+        if args.c5 > 0 and world == 1:
+            out["c5"] = c5_replay(ctx, gib=args.c5)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(head, seconds=args.cpu_seconds)
         else:

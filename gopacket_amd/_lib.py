@@ -211,6 +211,9 @@ def synth_lib():
         S.gpk_synth_device.restype = ctypes.c_int
         S.gpk_synth_bytes.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64]
         S.gpk_synth_bytes.restype = ctypes.c_uint64
+        S.gpk_synth_write_pcapng.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64,
+                                             ctypes.c_int]
+        S.gpk_synth_write_pcapng.restype = ctypes.c_uint64
         S.gpk_probe_read.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int,
                                      ctypes.c_void_p]
         S.gpk_probe_read.restype = ctypes.c_int

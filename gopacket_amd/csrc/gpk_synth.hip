@@ -3,6 +3,13 @@
 // never linked into libgpk.so. Packets are generated in HBM directly (C3 is
 // ~100 GB at 64 M packets, far more than is worth copying over PCIe).
 #include <hip/hip_runtime.h>
+#include <fcntl.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cstring>
+#include <thread>
+#include <vector>
 #include <hipcub/hipcub.hpp>
 
 #include <cstring>
@@ -162,6 +169,69 @@ uint64_t gpk_synth_bytes(int cfg, uint64_t first, uint64_t n) {
   uint64_t t = 0;
   for (uint64_t k = 0; k < n; k++) t += frame_len(cfg, first + k);
   return t;
+}
+
+// C5 capture file: SHB + one IDB (LinkType 1 = Ethernet, snaplen 65535,
+// microsecond timestamps) + one EPB per packet [first, first+n) of config cfg
+// (little endian; ts = 1.6e9 s + i microseconds). T threads generate disjoint
+// ranges and pwrite them at offsets from a prefix sum of the record sizes.
+// Returns the file size, or 0 on error.
+uint64_t gpk_synth_write_pcapng(const char* path, int cfg, uint64_t first, uint64_t n, int T) {
+  if (T < 1) T = 1;
+  int fd = open(path, O_WRONLY | O_CREAT | O_TRUNC, 0644);
+  if (fd < 0) return 0;
+  uint8_t head[28 + 20];
+  auto p32 = [](uint8_t* b, uint32_t v) { memcpy(b, &v, 4); };
+  auto p16 = [](uint8_t* b, uint16_t v) { memcpy(b, &v, 2); };
+  p32(head, 0x0A0D0D0A); p32(head + 4, 28); p32(head + 8, 0x1A2B3C4D); p16(head + 12, 1); p16(head + 14, 0);
+  uint64_t minus1 = ~0ull;
+  memcpy(head + 16, &minus1, 8);
+  p32(head + 24, 28);
+  p32(head + 28, 1); p32(head + 32, 20); p16(head + 36, 1); p16(head + 38, 0); p32(head + 40, 65535); p32(head + 44, 20);
+  bool ok = pwrite(fd, head, sizeof(head), 0) == (ssize_t)sizeof(head);
+  auto rec = [&](uint64_t i) { return 32ull + ((frame_len(cfg, i) + 3u) & ~3u); };
+  std::vector<uint64_t> start(T + 1, 0);
+  const uint64_t per = (n + T - 1) / T;
+  std::vector<std::thread> th;
+  for (int t = 0; t < T; t++)  // bytes of each range
+    th.emplace_back([&, t] {
+      uint64_t a = first + std::min<uint64_t>(n, t * per), e = first + std::min<uint64_t>(n, (t + 1) * per), s = 0;
+      for (uint64_t i = a; i < e; i++) s += rec(i);
+      start[t + 1] = s;
+    });
+  for (auto& x : th) x.join();
+  th.clear();
+  start[0] = sizeof(head);
+  for (int t = 0; t < T; t++) start[t + 1] += start[t];
+  std::vector<int> good(T, 1);
+  for (int t = 0; t < T; t++)
+    th.emplace_back([&, t] {
+      uint64_t a = first + std::min<uint64_t>(n, t * per), e = first + std::min<uint64_t>(n, (t + 1) * per);
+      std::vector<uint8_t> buf(8u << 20);
+      uint64_t fill = 0, at = start[t];
+      for (uint64_t i = a; i <= e; i++) {
+        const uint64_t r = i < e ? rec(i) : 0;
+        if (i == e || fill + r > buf.size()) {
+          if (fill && pwrite(fd, buf.data(), fill, (off_t)at) != (ssize_t)fill) good[t] = 0;
+          at += fill;
+          fill = 0;
+          if (i == e) break;
+        }
+        uint8_t* b = buf.data() + fill;
+        const uint32_t cl = frame_len(cfg, i);
+        const uint64_t ts = 1600000000000000ull + i;
+        memset(b + 28 + (cl & ~3u), 0, 4);
+        p32(b, 6); p32(b + 4, (uint32_t)r); p32(b + 8, 0); p32(b + 12, (uint32_t)(ts >> 32)); p32(b + 16, (uint32_t)ts);
+        p32(b + 20, cl); p32(b + 24, cl);
+        gpk_synth_fill(cfg, i, b + 28);
+        p32(b + r - 4, (uint32_t)r);
+        fill += r;
+      }
+    });
+  for (auto& x : th) x.join();
+  for (int t = 0; t < T; t++) ok = ok && good[t];
+  close(fd);
+  return ok ? start[T] : 0;
 }
 
 // Launch the streaming-read probe over data[0, nbytes & ~15) on `stream`.

@@ -120,6 +120,52 @@ class Context:
             sp = stream.cuda_stream
         check(lib().gpk_decode_batch(self.h, parser.h, ctypes.byref(b), ctypes.byref(r), sp))
 
+    def replay_file(self, parser, path, fmt=0, ng_flags=0, slot_bytes=0, slots=0, batch_pkts=0, read_threads=0,
+                    collect=True, on_batch=None):
+        """gpk_replay_file: the whole capture through HBM (BASELINE config C5).
+        collect=True gathers every result (records, err_args, flows SoA, ci,
+        caplens) in packet order; on_batch(first, n, records, err_args, flows,
+        ci, caplens) sees each launch's numpy views instead (valid during the
+        call). Returns (results-or-None, stats dict)."""
+        parts = []
+
+        def cb(user, first, n, rec, err, fl, ci, cap):
+            if not n:
+                return
+            views = (np.ctypeslib.as_array(ctypes.cast(rec, ctypes.POINTER(ctypes.c_uint8)), (n * 16,)).view(
+                         _lib.RECORD_DTYPE),
+                     np.ctypeslib.as_array(ctypes.cast(err, ctypes.POINTER(ctypes.c_uint32)), (2 * n,)),
+                     np.ctypeslib.as_array(ctypes.cast(fl, ctypes.POINTER(ctypes.c_uint64)), (3 * n,)),
+                     np.ctypeslib.as_array(ctypes.cast(ci, ctypes.POINTER(ctypes.c_uint8)), (n * 24,)).view(
+                         _lib.CAPINFO_DTYPE),
+                     np.ctypeslib.as_array(ctypes.cast(cap, ctypes.POINTER(ctypes.c_uint32)), (n,)))
+            if on_batch is not None:
+                on_batch(first, n, *views)
+            if collect:
+                parts.append(tuple(v.copy() for v in views))
+
+        c_cb = _lib.REPLAY_CB(cb)
+        o = _lib.ReplayOpts(fmt, ng_flags, slot_bytes, slots, batch_pkts, read_threads)
+        st = _lib.ReplayStats()
+        rc = lib().gpk_replay_file(self.h, parser.h, path.encode() if isinstance(path, str) else path,
+                                   ctypes.byref(o), c_cb, None, ctypes.byref(st))
+        if rc != _lib.GPK_OK:
+            raise _lib.GpkError("gpk_replay_file: %d %s %s" % (rc, st.error.decode(errors="replace"),
+                                                               lib().gpk_last_hip_error().decode()))
+        stats = {k: getattr(st, k) for k, _ in _lib.ReplayStats._fields_}
+        stats["error"] = st.error.decode(errors="replace")
+        res = None
+        if collect:
+            if parts:
+                fl = np.concatenate([p[2].reshape(3, -1) for p in parts], axis=1).reshape(-1)
+                res = dict(records=np.concatenate([p[0] for p in parts]), err_args=np.concatenate([p[1] for p in parts]),
+                           flows=fl, ci=np.concatenate([p[3] for p in parts]), caplens=np.concatenate([p[4] for p in parts]))
+            else:
+                res = dict(records=np.zeros(0, _lib.RECORD_DTYPE), err_args=np.zeros(0, np.uint32),
+                           flows=np.zeros(0, np.uint64), ci=np.zeros(0, _lib.CAPINFO_DTYPE),
+                           caplens=np.zeros(0, np.uint32))
+        return res, stats
+
     def decoded_list_host(self, parser, pkt, cap=65536):
         out = (ctypes.c_int64 * cap)()
         n = ctypes.c_uint32()

@@ -1,0 +1,87 @@
+"""gpk_replay_file (BASELINE config C5: capture file -> pinned staging -> HBM ->
+decode -> results) against the oracles: the pcapgo reader oracle for the
+packet stream and CaptureInfo, the decode oracle for every result. Small
+staging slots and batches force records across slot boundaries and many
+launches per slot.
+"""
+import gzip
+import os
+
+import numpy as np
+import pytest
+
+import pcapgen
+from configs import CONFIGS, assert_same, device_parser, oracle_parser
+from oracle import pcapgo_oracle as PO
+
+pytestmark = pytest.mark.gpu
+
+
+def packets_and_expect(raw, fmt="ng", **kw):
+    res = PO.read_all(raw, kind=fmt, **kw)  # the oracle inflates gzip input itself
+    s = res["stream"]
+    pk = [bytes(s[p.offset:p.offset + p.caplen]) for p in res["packets"]]
+    return res, pk
+
+
+def check(gpu_ctx, path, raw, cfg_name="statsassembly", fmt="ng", **opts):
+    res, pk = packets_and_expect(raw, fmt)
+    got, st = gpu_ctx.replay_file(device_parser(CONFIGS[cfg_name]), path, **opts)
+    assert st["packets"] == len(pk)
+    assert st["error"] == res["err"]
+    import pktutil
+    data, off, cap = pktutil.pack(pk)
+    ref = oracle_parser(CONFIGS[cfg_name]).decode(data, off, cap, nthreads=8, layouts=False)
+    assert_same(got, ref, "replay")
+    assert np.array_equal(got["caplens"], cap)
+    ci = got["ci"]
+    assert [(int(a), int(b), int(c), int(d)) for a, b, c, d in zip(ci["ts_sec"], ci["ts_nsec"], ci["length"], ci["iface"])] \
+        == [(p.ts_sec, p.ts_nsec, p.length, p.iface) for p in res["packets"]]
+    return st
+
+
+@pytest.fixture(scope="module")
+def capture(tmp_path_factory):
+    from gopacket_amd import _lib
+    d = tmp_path_factory.mktemp("cap")
+    path = str(d / "imix.pcapng")
+    size = _lib.synth_lib().gpk_synth_write_pcapng(path.encode(), 4, 777, 30000, 4)
+    assert size > 0
+    return path, open(path, "rb").read()
+
+
+@pytest.mark.parametrize("slot_bytes,slots,batch", [(4096, 2, 7), (65536, 3, 1000), (1 << 20, 4, 1 << 16), (0, 0, 0)])
+def test_replay_imix(gpu_ctx, capture, slot_bytes, slots, batch):
+    path, raw = capture
+    st = check(gpu_ctx, path, raw, slot_bytes=slot_bytes, slots=slots, batch_pkts=batch)
+    assert st["reader_status"] == 0 and st["file_bytes"] == len(raw)
+
+
+def test_replay_gzip_and_pcap(gpu_ctx, tmp_path, capture):
+    _, raw = capture
+    gz = gzip.compress(raw[:3_000_000], compresslevel=1)
+    p = tmp_path / "imix.pcapng.gz"
+    p.write_bytes(gz)
+    st = check(gpu_ctx, str(p), gz, slot_bytes=1 << 16, slots=3, batch_pkts=999)
+    assert st["error"] == "unexpected EOF"  # the 3 MB cut ends inside a record
+    from gopacket_amd import synth
+    pk = [synth.packet(4, i) for i in range(5000)]
+    pc = pcapgen.pcap_file(pk)
+    q = tmp_path / "imix.pcap"
+    q.write_bytes(pc)
+    check(gpu_ctx, str(q), pc, fmt="pcap", slot_bytes=8192, slots=2, batch_pkts=300)
+
+
+def test_replay_mixed_blocks(gpu_ctx, tmp_path):
+    """SPB/PB/EPB, statistics, name records, a second section in the other byte order."""
+    import pktutil
+    g = pktutil.golden()
+    pk = [bytes.fromhex(v["hex"]) for k, v in sorted(g.items()) if "hex" in v][:40]
+    raw = pcapgen.shb() + pcapgen.idb(1, 0) + b"".join(pcapgen.epb(p, ts=i) for i, p in enumerate(pk[:10]))
+    raw += pcapgen.nrb([(1, b"\x0a\x00\x00\x01x\x00")]) + b"".join(pcapgen.spb(p) for p in pk[10:20])
+    raw += pcapgen.isb(0, 5) + pcapgen.shb(">") + pcapgen.idb(1, 0, ">") + b"".join(
+        pcapgen.pb(p, bo=">") for p in pk[20:])
+    path = tmp_path / "mixed.pcapng"
+    path.write_bytes(raw)
+    st = check(gpu_ctx, str(path), raw, slot_bytes=4096, slots=2, batch_pkts=3)
+    assert st["error"] == "EOF"
