@@ -378,11 +378,32 @@ struct gpk_capreader {
     st.ifaces.push_back(std::move(it));
   }
 
+  // convertTime (ngread.go:439-443) in uint64 arithmetic. The common
+  // resolutions divide by constants (multiply-shift) or shift: a 64-bit
+  // hardware divide per packet would dominate the record walk.
   void convert_time(uint32_t idx, uint64_t ts, int64_t* s, uint32_t* ns) const {
     const Iface& it = st.ifaces[idx];
-    int64_t sec = (int64_t)(ts / it.second_mask + it.tsoff);
-    int64_t nsec = (int64_t)(ts % it.second_mask * it.scale_up / it.scale_down);
-    unix_norm(sec, nsec, s, ns);
+    const uint64_t m = it.second_mask;
+    uint64_t q, r;
+    if (m == 1000000ull) {
+      q = ts / 1000000ull;
+      r = ts - q * 1000000ull;
+    } else if (m == 1000000000ull) {
+      q = ts / 1000000000ull;
+      r = ts - q * 1000000000ull;
+    } else if (m == 1000ull) {
+      q = ts / 1000ull;
+      r = ts - q * 1000ull;
+    } else if ((m & (m - 1)) == 0) {
+      q = ts >> __builtin_ctzll(m);
+      r = ts & (m - 1);
+    } else {
+      q = ts / m;
+      r = ts % m;
+    }
+    uint64_t nsec = r * it.scale_up;
+    if (it.scale_down != 1) nsec /= it.scale_down;
+    unix_norm((int64_t)(q + it.tsoff), (int64_t)nsec, s, ns);
   }
 
   void read_interface_statistics() {
