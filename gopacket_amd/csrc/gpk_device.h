@@ -61,7 +61,20 @@ struct KParams {
   int32_t first_kind;       // decoder registered for `first` (GPK_DEC_NONE if none)
   const uint32_t* ctab;     // compact blob in device memory, or null: global tables
   CompactGeom cg;
+  uint32_t fast;            // GPK_FAST_* : which transitions the straight-line path may take
 };
+
+// Straight-line common-case parse (fast_parser below). Each bit says the
+// parser's container and tables make this transition go to the expected
+// decoder, so the fast path may take it without the generic dispatch; the
+// host derives them from the parser (gpk_host.cpp fast_flags).
+#define GPK_FAST_ON 0x1u       // first decoder is Ethernet
+#define GPK_FAST_IP4 0x2u      // EtherType 0x0800 -> IPv4 decoder
+#define GPK_FAST_IP6 0x4u      // EtherType 0x86DD -> IPv6 decoder
+#define GPK_FAST_D1Q 0x8u      // EtherType 0x8100 -> Dot1Q decoder
+#define GPK_FAST_QINQ 0x10u    // EtherType 0x88A8 -> Dot1Q decoder
+#define GPK_FAST_TCP 0x20u     // IPProtocol 6 -> TCP decoder
+#define GPK_FAST_UDP 0x40u     // IPProtocol 17 -> UDP decoder
 
 // LDS geometry: per lane a header window of WIN_CHUNKS 16-byte chunks.
 // Slot stride is odd in dwords so byte/dword reads at equal packet positions
@@ -72,7 +85,14 @@ constexpr int kWaves = kBlock / 64;
 #define GPK_WIN_CHUNKS 5  // 80-byte header window: 6 blocks per CU (A/B r01: C2 -21%, C4 -17%, C3 -5% vs 9)
 #endif
 constexpr int kWinChunks = GPK_WIN_CHUNKS;
-constexpr int kSlotDw = kWinChunks * 4 + 1;  // odd: lanes reading equal positions hit distinct banks
+#ifndef GPK_LINE_OWN
+#define GPK_LINE_OWN 0  // 1: each 128-byte line read from HBM once (LineOwn; A/B r01: FETCH -12%, time +4%)
+#endif
+// odd: lanes reading equal positions hit distinct banks. With line ownership
+// the three dwords after the window hold the lane's LineOwn sums (still 6
+// blocks of 256 lanes per CU: 23.5 KB + 2.9 KB of tables).
+constexpr int kSlotDw = kWinChunks * 4 + (GPK_LINE_OWN ? 3 : 1);
+constexpr int kOwnDw = kWinChunks * 4;  // LineOwn h, t, hx at slot + kOwnDw + 0..2
 constexpr int kLdsBytes = kBlock * kSlotDw * 4;
 
 // Dynamic LDS of the decode kernels (one declaration, aliased everywhere).
@@ -693,6 +713,132 @@ __device__ __forceinline__ Outcome run_parser(const KParams& P, const TT& T, con
       return out;
     }
   }
+}
+
+// The common case of DecodeLayers as straight-line code: Ethernet, up to two
+// Dot1Q tags, IPv4 without options/fragmentation or IPv6 without HopByHop,
+// TCP (options other than MPTCP) or UDP, then Payload or an unregistered
+// port type. Every header byte must sit in the LDS window. It fills Parse and
+// Outcome exactly as run_parser would (same layer list, slices, last
+// writers); anything else (errors, truncation, options that need the general
+// decoders, other types) returns false and the lane runs run_parser.
+#ifndef GPK_FAST
+#define GPK_FAST 1
+#endif
+template <class TT>
+__device__ __forceinline__ bool fast_parser(const KParams& P, const TT& T, const Rd& r, uint32_t caplen, Parse& q,
+                                            Outcome& out) {
+  const RdL rl{r.lb};
+  const uint32_t W = r.win, F = P.fast;
+  q.init();
+  if (caplen < 15 || W < 14) return false;
+  uint32_t et = rd16(rl, 12);
+  uint32_t off = 14, len = caplen - 14, n = 1;
+  uint64_t codes = GPK_CODE_ETHERNET;
+  q.s_eth = 0;
+  q.e_eth = caplen;
+#pragma unroll
+  for (int v = 0; v < 2; v++) {  // Dot1Q / QinQ tags (dot1q.go:30-41)
+    const bool tag = (et == 0x8100 && (F & GPK_FAST_D1Q)) || (et == 0x88a8 && (F & GPK_FAST_QINQ));
+    if (!tag) break;
+    if (len < 5 || off + 4 > W) return false;
+    codes |= (uint64_t)GPK_CODE_DOT1Q << (4 * n++);
+    q.s_d1q = off;
+    q.e_d1q = off + len;
+    et = rd16(rl, off + 2);
+    off += 4;
+    len -= 4;
+  }
+  uint32_t proto;
+  if (et == 0x0800 && (F & GPK_FAST_IP4)) {  // ip4.go:178-271, no options
+    if (len < 20 || off + 20 > W) return false;
+    const uint32_t b0 = rd8(rl, off), length = rd16(rl, off + 2), ff = rd16(rl, off + 6);
+    if ((b0 & 15) != 5 || length < 20 || length > len || (ff & 0x3fff)) return false;
+    proto = rd8(rl, off + 9);
+    codes |= (uint64_t)GPK_CODE_IPV4 << (4 * n++);
+    q.s_ip4 = off;
+    q.e_ip4 = off + len;
+    q.last_net = GPK_DEC_IPV4;
+    off += 20;
+    len = length - 20;
+  } else if (et == 0x86dd && (F & GPK_FAST_IP6)) {  // ip6.go:221-278, no HopByHop
+    if (len < 40 || off + 40 > W) return false;
+    const uint32_t length = rd16(rl, off + 4);
+    proto = rd8(rl, off + 6);
+    if (proto == 0 || length == 0 || length > len - 40) return false;
+    codes |= (uint64_t)GPK_CODE_IPV6 << (4 * n++);
+    q.s_ip6 = off;
+    q.e_ip6 = off + len;
+    q.last_net = GPK_DEC_IPV6;
+    off += 40;
+    len = length;
+  } else {
+    return false;
+  }
+  if (len == 0) return false;
+  int32_t h;
+  uint32_t poff, plen;
+  if (proto == 6 && (F & GPK_FAST_TCP)) {  // tcp.go:291-551
+    if (len < 20 || off + 20 > W) return false;
+    const uint32_t ds = (rd8(rl, off + 12) >> 4) * 4;
+    if (ds < 20 || ds > len || off + ds > W) return false;
+    for (uint32_t p = off + 20, e = off + ds; p < e;) {  // options: EOL, NOP, TLV
+      const uint32_t t = rd8(rl, p);
+      if (t == 0) break;
+      if (t == 1) {
+        p++;
+        continue;
+      }
+      if (t == 30 || p + 2 > e) return false;  // MPTCP / short: the general decoder
+      const uint32_t ol = rd8(rl, p + 1);
+      if (ol < 2 || p + ol > e) return false;
+      p += ol;
+    }
+    codes |= (uint64_t)GPK_CODE_TCP << (4 * n++);
+    q.s_tcp = off;
+    q.e_tcp = off + len;
+    q.transport = GPK_DEC_TCP;
+    h = T.tcp(rd32(rl, off));
+    poff = off + ds;
+    plen = len - ds;
+  } else if (proto == 17 && (F & GPK_FAST_UDP)) {  // udp.go:30-56
+    if (len < 8 || off + 8 > W) return false;
+    const uint32_t length = rd16(rl, off + 4);
+    uint32_t hlen = len;
+    if (length >= 8) {
+      if (length > len) return false;
+      hlen = length;
+    } else if (length != 0) {
+      return false;
+    }
+    codes |= (uint64_t)GPK_CODE_UDP << (4 * n++);
+    q.s_udp = off;
+    q.e_udp = off + len;
+    q.transport = GPK_DEC_UDP;
+    q.udp_hlen = hlen;
+    h = T.udp(rd32(rl, off));
+    poff = off + 8;
+    plen = hlen - 8;
+  } else {
+    return false;
+  }
+  if (plen != 0) {  // layers_decoder.go:71-79
+    const int k = T.kind(h);
+    if (k == GPK_DEC_PAYLOAD) {  // gopacket.Payload (base.go:61-70)
+      codes |= (uint64_t)GPK_CODE_PAYLOAD << (4 * n++);
+      q.s_app = poff;
+      q.e_app = poff + plen;
+      q.app_kind = GPK_DEC_PAYLOAD;
+    } else if (k == GPK_DEC_NONE) {  // (typ, nil): UnsupportedLayerType unless typ == 0
+      const int32_t lt = T.lt(h);
+      if (lt != GPK_LT_ZERO && !P.ignore_unsupported) out.err = GPK_ERR_UNSUPPORTED, out.a0 = (uint32_t)lt;
+    } else {
+      return false;
+    }
+  }
+  q.layers = codes;
+  q.nlayers = n;
+  return true;
 }
 
 __device__ __forceinline__ bool clean(const Parse& q, uint32_t kind) {

@@ -319,6 +319,22 @@ int gpk_ctx_set_table_mode(gpk_ctx* c, int mode) {
   return GPK_OK;
 }
 
+// Transitions the kernels' straight-line path may take for this parser
+// (gpk_device.h fast_parser): each is allowed when the tables send it to the
+// decoder the path hard-codes.
+static uint32_t fast_flags(const gpk_parser* p) {
+  auto kind = [&](int32_t lt) { return (lt >= 0 && lt < GPK_MAX_LAYER_TYPE) ? (int)p->tab.dispatch[lt] : GPK_DEC_NONE; };
+  if (p->first != GPK_LT_ETHERNET || kind(GPK_LT_ETHERNET) != GPK_DEC_ETHERNET) return 0;
+  uint32_t f = GPK_FAST_ON;
+  if (kind(p->tab.ethertype[0x0800]) == GPK_DEC_IPV4) f |= GPK_FAST_IP4;
+  if (kind(p->tab.ethertype[0x86dd]) == GPK_DEC_IPV6) f |= GPK_FAST_IP6;
+  if (kind(p->tab.ethertype[0x8100]) == GPK_DEC_DOT1Q) f |= GPK_FAST_D1Q;
+  if (kind(p->tab.ethertype[0x88a8]) == GPK_DEC_DOT1Q) f |= GPK_FAST_QINQ;
+  if (kind(p->tab.ipprotocol[6]) == GPK_DEC_TCP) f |= GPK_FAST_TCP;
+  if (kind(p->tab.ipprotocol[17]) == GPK_DEC_UDP) f |= GPK_FAST_UDP;
+  return f;
+}
+
 static int upload(gpk_ctx* c, const gpk_parser* p, hipStream_t s, gpk::KParams& P) {
   if (c->uploaded_version != p->version) {
     static thread_local uint32_t blob[gpk::kCtDwords];
@@ -333,6 +349,7 @@ static int upload(gpk_ctx* c, const gpk_parser* p, hipStream_t s, gpk::KParams& 
   P.ctab = c->compact ? c->dctab : nullptr;
   P.cg = c->cg;
   P.first_kind = (p->first >= 0 && p->first < GPK_MAX_LAYER_TYPE) ? p->tab.dispatch[p->first] : GPK_DEC_NONE;
+  P.fast = fast_flags(p);
   return GPK_OK;
 }
 
@@ -356,6 +373,7 @@ static int make_params(gpk_ctx* c, const gpk_parser* p, const gpk_batch* b, cons
   P.tab = nullptr;  // upload()
   P.ctab = nullptr;
   P.first_kind = GPK_DEC_NONE;
+  P.fast = 0;
   P.first = p->first;
   P.outputs = p->outputs;
   P.ignore_unsupported = p->ignore_unsupported;

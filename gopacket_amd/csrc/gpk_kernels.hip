@@ -36,9 +36,6 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 #ifndef GPK_PB_G
 #define GPK_PB_G 4  // phase B: pending packets per wave pass
 #endif
-#ifndef GPK_LINE_SPLIT
-#define GPK_LINE_SPLIT 0  // 1: phase B on whole lines, partial lines per lane (A/B r01: no gain)
-#endif
 #ifndef GPK_PREFETCH
 #define GPK_PREFETCH 0  // 1: next tile's windows in flight (persistent only; A/B r01: no gain)
 #endif
@@ -210,6 +207,97 @@ __device__ __forceinline__ void store_window(uint32_t slot_dw, uint32_t nchunk, 
     }
 }
 
+// Line ownership (GPK_LINE_OWN). Phase B streams a packet's L4 bytes long
+// after its header window was read, by which time L2 has evicted the window's
+// lines: without care, the window's last 128-byte line and the packet's last
+// line (which holds the next packet's header) are each fetched from HBM twice.
+// So right after the window arrives (its lines are in L2) every lane also
+// loads the other chunks of the lines the window touched:
+//   head: [wend, he)  this packet's bytes after the window, up to the end of
+//         the window's last line: even/odd byte sums (hE, hO);
+//   tail: [L0, off)   the start of the window's first line, which is the END
+//         of the previous packet when packets are contiguous: even/odd sums
+//         (tE, tO) handed to lane-1, which then never touches that line.
+// Phase B then streams whole lines [he, L0 of the next packet) only. Sums
+// are by absolute byte parity, so the owner combines them with its segment
+// parity like every other partial sum.
+struct LineOwn {  // packed: three registers live across the parse
+  uint32_t h;    // head sums: even | odd << 16 (<= 112 bytes: each < 2^16)
+  uint32_t t;    // tail sums: even | odd << 16 (<= 127 bytes)
+  uint32_t hx;   // (he - off) | tok << 8: head end relative to the packet, tail valid
+};
+
+__device__ __forceinline__ void chunk_eo_masked(uint4 v, uint32_t lo, uint32_t hi, uint32_t& E, uint32_t& O) {
+  uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int d = 0; d < 4; d++) {
+    int l = (int)lo - 4 * d, h = (int)hi - 4 * d;
+    l = l < 0 ? 0 : (l > 4 ? 4 : l);
+    h = h < 0 ? 0 : (h > 4 ? 4 : h);
+    uint32_t m = h > l ? ((0xffffffffu >> (8 * (4 - (h - l)))) << (8 * l)) : 0u;
+    E = dot_even(w[d] & m, E);
+    O = dot_odd(w[d] & m, O);
+  }
+}
+
+// Round 2 of the header loads: issued after the window chunks arrived, so
+// these chunks (same lines) are L2 hits. prev_ok: the previous packet (lane-1)
+// ends exactly at this packet's start and covers [off & ~127, off).
+__device__ __forceinline__ LineOwn line_own(const KParams& P, uint64_t off, uint32_t cl, uint32_t nchunk,
+                                            const uint4& chunk0, bool active, bool prev_ok) {
+  const uint64_t A0 = off & ~15ull, wend = A0 + 16ull * nchunk, L0 = off & ~127ull;
+  const uint64_t pend = (off + cl) & ~15ull;
+  uint64_t he = (wend + 127) & ~127ull;
+  if (he > pend) he = pend;
+  if (he < wend || !active) he = wend;
+  const uint32_t nh = (uint32_t)((he - wend) >> 4);
+  const bool tok = active && prev_ok;
+  const uint32_t nt = tok ? (uint32_t)((A0 - L0) >> 4) : 0u;
+  uint32_t tE = 0, tO = 0, hE = 0, hO = 0;
+  if (tok) chunk_eo_masked(chunk0, 0, (uint32_t)(off & 15), tE, tO);  // [A0, off) of chunk 0
+  // the <= 11 non-window chunks of the <= 2 lines a window touches, in two
+  // batches (7 + 4) so the loads in flight fit the 80-VGPR budget
+#ifndef GPK_OWN_B2
+#define GPK_OWN_B2 1  // two load batches (7 + 4) instead of one of 11
+#endif
+  constexpr int kB1 = GPK_OWN_B2 ? 7 : 11, kB2 = GPK_OWN_B2 ? 4 : 0;
+#pragma unroll
+  for (int b = 0; b < (kB2 ? 2 : 1); b++) {
+    uint4 v[kB1];
+    const int j0 = b ? kB1 : 0, nb = b ? kB2 : kB1;
+    // batch 2 depends on batch 1's sums (an opaque zero): its loads cannot be
+    // hoisted next to batch 1's, which would double the registers in flight
+    uint32_t dep = 0;
+    if (b) asm volatile("v_and_b32 %0, 0, %1" : "=v"(dep) : "v"(hE + tE));
+#pragma unroll
+    for (int k = 0; k < nb; k++) {
+      const uint32_t j = (uint32_t)(j0 + k);
+      const uint64_t a = (j < nt ? L0 + 16ull * j : wend + 16ull * (j - nt)) + dep;
+      v[k] = j < nt + nh ? ld16(P.data + a) : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int k = 0; k < nb; k++) {
+      uint32_t e = 0, od = 0;
+      chunk_eo(v[k], e, od);
+      if ((uint32_t)(j0 + k) < nt) {
+        tE += e;
+        tO += od;
+      } else {
+        hE += e;
+        hO += od;
+      }
+    }
+  }
+  return LineOwn{hE | hO << 16, tE | tO << 16, (uint32_t)(he - off) | (tok ? 256u : 0u)};
+}
+
+__device__ __forceinline__ uint64_t shfl_up64(uint64_t v, int d) {
+  return ((uint64_t)(uint32_t)__shfl_up((int)(uint32_t)(v >> 32), d) << 32) | (uint32_t)__shfl_up((int)(uint32_t)v, d);
+}
+__device__ __forceinline__ uint64_t shfl_down64(uint64_t v, int d) {
+  return ((uint64_t)(uint32_t)__shfl_down((int)(uint32_t)(v >> 32), d) << 32) | (uint32_t)__shfl_down((int)(uint32_t)v, d);
+}
+
 template <bool kL4, bool kLayout, class TT>
 __device__ __forceinline__ void decode_packet(const KParams& P, const TT& T, uint64_t i, bool active, uint64_t off,
                                               uint32_t cl, uint32_t slot_dw, uint32_t lane) {
@@ -222,7 +310,13 @@ __device__ __forceinline__ void decode_packet(const KParams& P, const TT& T, uin
   Parse q;
   q.init();
   Outcome s{0, 0, 0, 0};
+#if GPK_FAST
+  bool done = false;
+  if (active && P.fast) done = fast_parser(P, T, r, cl, q, s);
+  if (active && !done) s = run_parser<false>(P, T, r, cl, q);
+#else
   if (active) s = run_parser<false>(P, T, r, cl, q);
+#endif
 
   uint32_t st = (s.err & GPK_ST_ERR_MASK) | (s.trunc ? GPK_ST_TRUNCATED : 0u) |
                 ((q.nlayers > GPK_ST_NLAYERS_MASK ? GPK_ST_NLAYERS_MASK : q.nlayers) << GPK_ST_NLAYERS_SHIFT);
@@ -265,49 +359,40 @@ __device__ __forceinline__ void decode_packet(const KParams& P, const TT& T, uin
         const uint32_t par = (uint32_t)((off + t0) & 1);
         const uint64_t fa = (ra + 15) & ~15ull, fe = re & ~15ull;
         uint32_t edge = 0;
+#if GPK_LINE_OWN
+        // head: the window's last line after the window, summed at load time
+        // (LineOwn sums in this lane's LDS slot; the next packet's in lane+1's,
+        // written by that lane of this wave before the parse)
+        const uint32_t own_h = gpk_smem[slot_dw + kOwnDw], own_hx = gpk_smem[slot_dw + kOwnDw + 2];
+        const uint32_t nx_t = gpk_smem[slot_dw + kSlotDw + kOwnDw + 1];
+        const bool nx_tok = lane < 63 && (gpk_smem[slot_dw + kSlotDw + kOwnDw + 2] & 256u);
+        const uint64_t he = off + (own_hx & 255u);
+        const bool head_ok = t0 <= win && he > ra && he <= re;
+        const uint64_t bs = head_ok ? he : fa;
+        if (head_ok) edge += par ? ((own_h >> 16) << 8) + (own_h & 0xffff) : ((own_h & 0xffff) << 8) + (own_h >> 16);
+        // tail: the next packet's line head, summed by lane+1 (which saw this
+        // packet end exactly at its start)
+        const uint64_t nl0 = re & ~127ull;
+        const bool tail_ok = nx_tok && re == off + cl && nl0 >= bs && fa <= fe;
+        const uint64_t be = tail_ok ? nl0 : fe;
+        if (tail_ok) edge += par ? ((nx_t >> 16) << 8) + (nx_t & 0xffff) : ((nx_t & 0xffff) << 8) + (nx_t >> 16);
+        if (fa > fe) {  // remainder inside a single chunk
+          edge = chunk_sum(ld16(P.data + (ra & ~15ull)), ra & ~15ull, ra, re, par);
+        } else {
+          if (!head_ok && ra != fa) edge += chunk_sum(ld16(P.data + (ra & ~15ull)), ra & ~15ull, ra, re, par);
+          if (!tail_ok && re != fe) edge += chunk_sum(ld16(P.data + fe), fe, ra, re, par);
+        }
+        jsum = init + part + edge;
+        job = bs < be;
+        ja = bs;
+        je = be;
+#else
         if (fa > fe) {  // remainder inside a single chunk
           edge = chunk_sum(ld16(P.data + (ra & ~15ull)), ra & ~15ull, ra, re, par);
         } else {
           if (ra != fa) edge += chunk_sum(ld16(P.data + (ra & ~15ull)), ra & ~15ull, ra, re, par);
           if (re != fe) edge += chunk_sum(ld16(P.data + fe), fe, ra, re, par);
         }
-#if GPK_LINE_SPLIT
-        // Phase B gets whole 128-byte lines only, [la, lb). The full chunks
-        // of the segment's first and last partial lines, [fa, la) and
-        // [lb, fe), are summed here, right after the header window loads
-        // touched those lines (the window's last line; the last line is
-        // the next packet's first line, which its lane loaded with this
-        // tile's windows) so they are still cached: every line of the
-        // packet is fetched from HBM once.
-        uint64_t la = fa, lb = fa;  // fa >= fe: no full chunk at all
-        if (fa < fe) {
-          la = (fa + 127) & ~127ull;
-          lb = fe & ~127ull;
-          if (la > fe) la = fe;
-          if (lb < la) lb = la;
-        }
-        {
-          uint4 hv[15];
-#pragma unroll
-          for (int k = 0; k < 7; k++)
-            if (fa + 16 * k < la) hv[k] = ld16(P.data + fa + 16 * k);
-#pragma unroll
-          for (int k = 0; k < 8; k++)
-            if (lb + 16 * k < fe) hv[7 + k] = ld16(P.data + lb + 16 * k);
-          uint32_t E2 = 0, O2 = 0;
-#pragma unroll
-          for (int k = 0; k < 7; k++)
-            if (fa + 16 * k < la) chunk_eo(hv[k], E2, O2);
-#pragma unroll
-          for (int k = 0; k < 8; k++)
-            if (lb + 16 * k < fe) chunk_eo(hv[7 + k], E2, O2);
-          edge += par ? (O2 << 8) + E2 : (E2 << 8) + O2;
-        }
-        jsum = init + part + edge;
-        job = la < lb;
-        ja = la;
-        je = lb;
-#else
         jsum = init + part + edge;
         job = fa < fe;
         ja = fa;
@@ -603,7 +688,32 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GPK_WAVE
     for (uint32_t k = tid; k < P.cg.words; k += kBlock) gpk_smem[base + k] = P.ctab[k];
     __syncthreads();
   }
+#ifndef GPK_OWN_EARLY
+#define GPK_OWN_EARLY 0  // 1: issue the line-ownership loads with the window loads
+#endif
+#if GPK_LINE_OWN && GPK_OWN_EARLY
+  LineOwn own{0, 0, 0};
+  if (kL4) {
+    const uint64_t poff = shfl_up64(c0.off, 1);
+    const uint32_t pcl = (uint32_t)__shfl_up((int)c0.cl, 1);
+    const bool prev_ok = (tid & 63) > 0 && poff + pcl == c0.off && poff <= (c0.off & ~127ull);
+    own = line_own(P, c0.off, c0.cl, n0, w0.v[0], i0 < P.n, prev_ok);
+  }
+#endif
   store_window(slot_dw, n0, w0);
+#if GPK_LINE_OWN
+  if (kL4) {
+#if !GPK_OWN_EARLY
+    const uint64_t poff = shfl_up64(c0.off, 1);
+    const uint32_t pcl = (uint32_t)__shfl_up((int)c0.cl, 1);
+    const bool prev_ok = (tid & 63) > 0 && poff + pcl == c0.off && poff <= (c0.off & ~127ull);
+    const LineOwn own = line_own(P, c0.off, c0.cl, n0, w0.v[0], i0 < P.n, prev_ok);
+#endif
+    gpk_smem[slot_dw + kOwnDw] = own.h;
+    gpk_smem[slot_dw + kOwnDw + 1] = own.t;
+    gpk_smem[slot_dw + kOwnDw + 2] = own.hx;
+  }
+#endif
   if (kCompact)
     decode_packet<kL4, kLayout>(P, LTab{P.cg, base}, i0, i0 < P.n, c0.off, c0.cl, slot_dw, tid & 63);
   else
