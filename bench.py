@@ -248,7 +248,7 @@ def c5_replay(ctx, gib=10.0, reps=2, threads=16):
         for _ in range(reps):
             picked.clear()
             valid[0] = 0
-            _, st = ctx.replay_file(parser, path, collect=False, on_batch=on_batch)
+            _, st = ctx.replay_file(parser, path, collect=False, on_batch=on_batch, read_threads=threads)
             runs.append(st)
     finally:
         os.unlink(path)

@@ -58,6 +58,7 @@ EXPORTS = (
     "gpk_capreader_create", "gpk_capreader_destroy", "gpk_capreader_index", "gpk_capreader_error",
     "gpk_capreader_link_type", "gpk_capreader_pcap_header", "gpk_capreader_nsections", "gpk_capreader_section_info",
     "gpk_capreader_ninterfaces", "gpk_capreader_interface", "gpk_capreader_interface_str", "gpk_replay_file",
+    "gpk_capreader_index_all", "gpk_capindex_free",
 )
 
 # include/gpk_capture.h constants
@@ -66,6 +67,11 @@ NG_WANT_MIXED_LINKTYPE, NG_ERROR_ON_MISMATCHING_LINKTYPE, NG_SKIP_UNKNOWN_VERSIO
 CAP_MORE, CAP_FULL, CAP_END = 0, 1, 2
 CAPINFO_DTYPE = np.dtype([("ts_sec", "<i8"), ("ts_nsec", "<u4"), ("length", "<u4"), ("iface", "<i4"),
                           ("link_type", "<i4")])
+
+
+class CapIndex(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_uint64), ("offsets", ctypes.c_void_p), ("caplens", ctypes.c_void_p),
+                ("ci", ctypes.c_void_p)]
 
 
 class NgInterface(ctypes.Structure):
@@ -172,6 +178,8 @@ def lib():
         "gpk_capreader_interface": ([vp, c_int, c_int, P(NgInterface)], c_int),
         "gpk_capreader_interface_str": ([vp, c_int, c_int, c_int, ctypes.c_char_p, ctypes.c_size_t], c_int),
         "gpk_replay_file": ([vp, vp, ctypes.c_char_p, P(ReplayOpts), REPLAY_CB, vp, P(ReplayStats)], c_int),
+        "gpk_capreader_index_all": ([vp, vp, u64, c_int, c_int, P(CapIndex), P(u64)], c_int),
+        "gpk_capindex_free": ([P(CapIndex)], c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)

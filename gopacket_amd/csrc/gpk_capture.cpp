@@ -28,8 +28,10 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <cstdlib>
 #include <new>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/gpk_capture.h"
@@ -381,8 +383,8 @@ struct gpk_capreader {
   // convertTime (ngread.go:439-443) in uint64 arithmetic. The common
   // resolutions divide by constants (multiply-shift) or shift: a 64-bit
   // hardware divide per packet would dominate the record walk.
-  void convert_time(uint32_t idx, uint64_t ts, int64_t* s, uint32_t* ns) const {
-    const Iface& it = st.ifaces[idx];
+  void convert_time(uint32_t idx, uint64_t ts, int64_t* s, uint32_t* ns) const { iface_time(st.ifaces[idx], ts, s, ns); }
+  static void iface_time(const Iface& it, uint64_t ts, int64_t* s, uint32_t* ns) {
     const uint64_t m = it.second_mask;
     uint64_t q, r;
     if (m == 1000000ull) {
@@ -859,3 +861,221 @@ int gpk_capreader_interface_str(const gpk_capreader* r, int s, int i, int field,
 }
 
 }  // extern "C"
+
+// ---- parallel record walk (gpk_capreader_index_all) -------------------------
+// The record walk is a pointer chase through the capture: one DRAM stream per
+// thread, ~4-5 GB/s. To walk a large staging slot with T threads, segments
+// 1..T-1 are walked speculatively: each worker finds a plausible chain of
+// plain Enhanced Packet Blocks after its segment's start and walks it. The
+// exact walk (the restated reader) then runs up to each worker's start; where
+// it lands exactly there with the reader state unchanged since the workers'
+// snapshot, the worker's packets are what ReadPacketData would return (a plain
+// EPB changes no reader state, see plain_epb) and the exact walk resumes after
+// them. Anywhere else the exact walk simply continues: the result is always
+// the sequential one.
+namespace {
+
+struct PktVec {  // growable, uninitialised arrays (malloc: gpk_capindex_free)
+  uint64_t* off = nullptr;
+  uint32_t* cap = nullptr;
+  gpk_capture_info* ci = nullptr;
+  uint64_t n = 0, room = 0;
+  bool reserve(uint64_t m) {
+    if (m <= room) return true;
+    uint64_t r = room ? room : 4096;
+    while (r < m) r *= 2;
+    void* a = realloc(off, r * 8);
+    if (!a) return false;
+    off = (uint64_t*)a;
+    void* c = realloc(cap, r * 4);
+    if (!c) return false;
+    cap = (uint32_t*)c;
+    void* d = realloc(ci, r * sizeof(gpk_capture_info));
+    if (!d) return false;
+    ci = (gpk_capture_info*)d;
+    room = r;
+    return true;
+  }
+  void release() {
+    free(off);
+    free(cap);
+    free(ci);
+    off = nullptr;
+    cap = nullptr;
+    ci = nullptr;
+    n = room = 0;
+  }
+};
+
+// What ReadPacketData does on a plain EPB at b[p] (ngread.go:497-527, 642-675):
+// block header; 20-byte EPB header; interface known (else an error) and, without
+// WantMixedLinkType, of the first interface's link type (else the block is
+// skipped); data + padding; the 4 bytes left make readOption return end of
+// options at once (ngread.go:201-204); discard(4). No state changes. "Plain":
+// total length == 32 + caplen + padding (no options) and the block inside
+// b[p, end). Returns the block length, 0 for anything else.
+uint32_t plain_epb(const NgState& st, uint32_t flags, const uint8_t* b, uint64_t p, uint64_t end, uint64_t* off,
+                   uint32_t* cap, gpk_capture_info* ci) {
+  if (end - p < 32) return 0;
+  const bool be = st.be;
+  const uint8_t* h = b + p;
+  if (ld32(h, be) != kEPB) return 0;
+  const uint32_t L = ld32(h + 4, be), idx = ld32(h + 8, be), cl = ld32(h + 20, be);
+  if (idx >= st.ifaces.size()) return 0;
+  if ((uint64_t)L != 32ull + cl + ((4u - (cl & 3u)) & 3u) || L > end - p) return 0;
+  const Iface& it = st.ifaces[idx];
+  const bool mixed = (flags & GPK_NG_WANT_MIXED_LINKTYPE) != 0;
+  if (!mixed && it.link_type != st.link_type) return 0;
+  if (ci) {
+    gpk_capreader::iface_time(it, (uint64_t)ld32(h + 12, be) << 32 | ld32(h + 16, be), &ci->ts_sec, &ci->ts_nsec);
+    ci->length = ld32(h + 24, be);
+    ci->iface = (int32_t)idx;
+    ci->link_type = mixed ? (int32_t)it.link_type : -1;
+  }
+  *off = p + 28;
+  *cap = cl;
+  return L;
+}
+
+// First p in [from, to), p = ref (mod 4) (blocks are 4-byte multiples), where
+// four plain EPBs with matching trailers follow each other.
+uint64_t find_sync(const NgState& st, uint32_t flags, const uint8_t* b, uint64_t from, uint64_t to, uint64_t end,
+                   uint64_t ref) {
+  for (uint64_t p = from + ((ref - from) & 3); p < to; p += 4) {
+    uint64_t q = p, o;
+    uint32_t c;
+    int k = 0;
+    for (; k < 4; k++) {
+      const uint32_t L = plain_epb(st, flags, b, q, end, &o, &c, nullptr);
+      if (!L || ld32(b + q + L - 4, st.be) != L) break;
+      q += L;
+    }
+    if (k == 4) return p;
+  }
+  return ~0ull;
+}
+
+struct Seg {
+  uint64_t sync = ~0ull, end = 0;
+  PktVec v;
+};
+
+void walk_seg(const NgState& st, uint32_t flags, const uint8_t* b, uint64_t p, uint64_t seg_end, uint64_t end,
+              Seg& s) {
+  s.sync = p;
+  while (p < seg_end && s.v.reserve(s.v.n + 1)) {
+    const uint32_t L = plain_epb(st, flags, b, p, end, &s.v.off[s.v.n], &s.v.cap[s.v.n], &s.v.ci[s.v.n]);
+    if (!L) break;
+    s.v.n++;
+    p += L;
+  }
+  s.end = p;
+}
+
+// Exact walk: ReadPacketData calls over b[from, to); *stop = where the next
+// call starts. Returns GPK_CAP_MORE / GPK_CAP_END or a negative status.
+int seq_walk(gpk_capreader* r, const uint8_t* b, uint64_t from, uint64_t to, int eof, PktVec& v, uint64_t* stop) {
+  uint64_t pos = from;
+  for (;;) {
+    const uint64_t room = 1u << 16;
+    if (!v.reserve(v.n + room)) return GPK_ENOMEM;
+    uint64_t k = 0, used = 0;
+    const int st = gpk_capreader_index(r, b + pos, to - pos, eof, v.off + v.n, v.cap + v.n, v.ci + v.n, room, &k, &used);
+    if (st < 0) return st;
+    for (uint64_t i = 0; i < k; i++) v.off[v.n + i] += pos;
+    v.n += k;
+    pos += used;
+    if (st != GPK_CAP_FULL) {
+      *stop = pos;
+      return st;
+    }
+  }
+}
+
+uint64_t state_version(const gpk_capreader* r) {  // anything plain_epb depends on changes one of these
+  return (uint64_t)r->st.ended.size() << 32 | r->st.ifaces.size();
+}
+
+}  // namespace
+
+extern "C" int gpk_capreader_index_all(gpk_capreader* r, const uint8_t* buf, uint64_t len, int eof, int threads,
+                                       gpk_capindex* out, uint64_t* consumed) {
+  if (!r || (!buf && len) || !out || !consumed) return GPK_EINVAL;
+  memset(out, 0, sizeof(*out));
+  *consumed = 0;
+  PktVec v;
+  uint64_t pos = 0, stop = 0;
+  int st = GPK_CAP_MORE;
+  bool done = false;
+  try {
+    if (r->format == GPK_CAP_PCAPNG && threads > 1 && len >= (1u << 20) && !r->open_failed) {
+      if (!r->opened) {  // NewNgReader (section header, first interface) first
+        const uint64_t pre = len < (1u << 16) ? len : (1u << 16);
+        st = seq_walk(r, buf, 0, pre, pre == len ? eof : 0, v, &stop);
+        pos = stop;
+        done = st != GPK_CAP_MORE || pre == len;
+      }
+      if (!done && r->opened) {
+        const NgState snap = r->st;
+        const uint64_t ver = state_version(r), span = len - pos, base = pos;
+        const int T = threads > 64 ? 64 : threads;
+        std::vector<Seg> seg(T);
+        std::vector<std::thread> th;
+        for (int k = 1; k < T; k++)
+          th.emplace_back([&, k] {
+            const uint64_t s0 = base + span * k / T, s1 = k + 1 < T ? base + span * (k + 1) / T : len;
+            const uint64_t to = s1 < s0 + (1u << 20) ? s1 : s0 + (1u << 20);
+            const uint64_t p = find_sync(snap, r->flags, buf, s0, to, len, base);
+            if (p != ~0ull) walk_seg(snap, r->flags, buf, p, s1, len, seg[k]);
+          });
+        for (auto& t : th) t.join();
+        for (int k = 1; k < T && !done; k++) {
+          Seg& s = seg[k];
+          if (s.sync == ~0ull || s.sync < pos) {
+            s.v.release();
+            continue;
+          }
+          st = seq_walk(r, buf, pos, s.sync, 0, v, &stop);
+          pos = stop;
+          if (st != GPK_CAP_MORE) {
+            done = true;
+          } else if (pos == s.sync && state_version(r) == ver && v.reserve(v.n + s.v.n)) {
+            memcpy(v.off + v.n, s.v.off, s.v.n * 8);
+            memcpy(v.cap + v.n, s.v.cap, s.v.n * 4);
+            memcpy(v.ci + v.n, s.v.ci, s.v.n * sizeof(gpk_capture_info));
+            v.n += s.v.n;
+            pos = s.end;
+          }
+          s.v.release();
+        }
+        for (auto& s : seg) s.v.release();
+      }
+    }
+    if (!done) {
+      st = seq_walk(r, buf, pos, len, eof, v, &stop);
+      pos = stop;
+    }
+  } catch (...) {
+    v.release();
+    return GPK_ENOMEM;
+  }
+  if (st < 0) {
+    v.release();
+    return st;
+  }
+  out->n = v.n;
+  out->offsets = v.off;
+  out->caplens = v.cap;
+  out->ci = v.ci;
+  *consumed = pos;
+  return st;
+}
+
+extern "C" int gpk_capindex_free(gpk_capindex* x) {
+  if (!x) return GPK_EINVAL;
+  free(x->offsets);
+  free(x->caplens);
+  free(x->ci);
+  memset(x, 0, sizeof(*x));
+  return GPK_OK;
+}

@@ -321,75 +321,74 @@ extern "C" int gpk_replay_file(gpk_ctx* ctx, const gpk_parser* parser, const cha
       }
       if (good) start_fill(N);
     }
-    // walk the records of [start, start+len) into batches
-    uint64_t pos = start;
+    // walk the records of [start, start+len) (parallel, gpk_capreader_index_all)
+    gpk_capindex xi;
+    uint64_t used = 0;
+    double t_ix = now_s();
+    int st = gpk_capreader_index_all(rd, S.host + start, len, eof ? 1 : 0, opt.read_threads, &xi, &used);
+    stats->index_s += now_s() - t_ix;
+    if (st < 0) {
+      rc = st;
+      finished = true;
+      break;
+    }
+    const uint64_t pos = start + used;
     bool copied = false;
-    for (;;) {
+    for (uint64_t first = 0; first < xi.n && good;) {  // batches of up to P packets
+      const uint64_t n = std::min<uint64_t>(P, xi.n - first);
       const int b = pl.acquire();
       if (b < 0) {
         good = false;
         break;
       }
       Bat& B = pl.bats[b];
-      uint64_t n = 0, used = 0;
-      double t = now_s();
-      int st = gpk_capreader_index(rd, S.host + pos, start + len - pos, eof ? 1 : 0, B.h_off, B.h_cap, B.h_ci, P, &n,
-                                   &used);
-      stats->index_s += now_s() - t;
-      if (st < 0) {
-        rc = st;
-        finished = true;
+      memcpy(B.h_off, xi.offsets + first, n * 8);  // relative to the slot's device copy (start)
+      memcpy(B.h_cap, xi.caplens + first, n * 4);
+      memcpy(B.h_ci, xi.ci + first, n * sizeof(gpk_capture_info));
+      if (!copied) {  // the whole slot, once, before its first kernel
+        good = pl.ok(hipMemcpyAsync(S.dev, S.host + start, len + 16, hipMemcpyHostToDevice, S.stream), "HtoD slot") &&
+               pl.ok(hipEventRecord(S.h2d, S.stream), "hipEventRecord");
+        S.h2d_pending = true;
+        copied = true;
+      }
+      B.first = packet_index;
+      B.n = n;
+      good = good && pl.ok(hipEventRecord(B.e0, S.stream), "hipEventRecord") &&
+             pl.ok(hipMemcpyAsync(B.d_off, B.h_off, n * 8, hipMemcpyHostToDevice, S.stream), "HtoD offsets") &&
+             pl.ok(hipMemcpyAsync(B.d_cap, B.h_cap, n * 4, hipMemcpyHostToDevice, S.stream), "HtoD caplens") &&
+             pl.ok(hipMemsetAsync(B.d_err, 0, n * 8, S.stream), "hipMemsetAsync") &&
+             pl.ok(hipEventRecord(B.k0, S.stream), "hipEventRecord");
+      if (!good) {
         pl.free_bats.push_back(b);
         break;
       }
-      if (n) {
-        const uint64_t shift = pos - start;  // offsets relative to the slot's device copy
-        for (uint64_t i = 0; i < n; i++) B.h_off[i] += shift;
-        if (!copied) {  // the whole slot, once, before its first kernel
-          good = pl.ok(hipMemcpyAsync(S.dev, S.host + start, len + 16, hipMemcpyHostToDevice, S.stream), "HtoD slot") &&
-                 pl.ok(hipEventRecord(S.h2d, S.stream), "hipEventRecord");
-          S.h2d_pending = true;
-          copied = true;
-        }
-        B.first = packet_index;
-        B.n = n;
-        good = good && pl.ok(hipEventRecord(B.e0, S.stream), "hipEventRecord") &&
-               pl.ok(hipMemcpyAsync(B.d_off, B.h_off, n * 8, hipMemcpyHostToDevice, S.stream), "HtoD offsets") &&
-               pl.ok(hipMemcpyAsync(B.d_cap, B.h_cap, n * 4, hipMemcpyHostToDevice, S.stream), "HtoD caplens") &&
-               pl.ok(hipMemsetAsync(B.d_err, 0, n * 8, S.stream), "hipMemsetAsync") &&
-               pl.ok(hipEventRecord(B.k0, S.stream), "hipEventRecord");
-        if (!good) break;
-        gpk_batch db{S.dev, B.d_off, B.d_cap, n, len + 16};
-        gpk_results dr{B.d_rec, B.d_err, B.d_flow, nullptr};
-        int drc = gpk_decode_batch(ctx, parser, &db, &dr, S.stream);
-        if (drc) {
-          rc = drc;
-          finished = true;
-          good = false;
-          break;
-        }
-        good = pl.ok(hipEventRecord(B.k1, S.stream), "hipEventRecord") &&
-               pl.ok(hipMemcpyAsync(B.h_rec, B.d_rec, n * sizeof(gpk_record), hipMemcpyDeviceToHost, S.stream), "DtoH") &&
-               pl.ok(hipMemcpyAsync(B.h_err, B.d_err, n * 8, hipMemcpyDeviceToHost, S.stream), "DtoH") &&
-               pl.ok(hipMemcpyAsync(B.h_flow, B.d_flow, n * 24, hipMemcpyDeviceToHost, S.stream), "DtoH") &&
-               pl.ok(hipEventRecord(B.done, S.stream), "hipEventRecord");
-        pl.inflight.push_back(b);
-        packet_index += n;
-        stats->batches++;
-        for (uint64_t i = 0; i < n; i++) stats->packet_bytes += B.h_cap[i];
-      } else {
-        pl.free_bats.push_back(b);
-      }
-      pos += used;
-      if (!good) break;
-      if (st == GPK_CAP_FULL) continue;
-      if (st == GPK_CAP_END) {
-        int is_eof = 0, is_panic = 0;
-        gpk_capreader_error(rd, stats->error, sizeof(stats->error), &is_eof, &is_panic);
-        stats->reader_status = is_eof ? 0 : (is_panic ? 2 : 1);
+      gpk_batch db{S.dev, B.d_off, B.d_cap, n, len + 16};
+      gpk_results dr{B.d_rec, B.d_err, B.d_flow, nullptr};
+      int drc = gpk_decode_batch(ctx, parser, &db, &dr, S.stream);
+      if (drc) {
+        rc = drc;
         finished = true;
+        good = false;
+        pl.free_bats.push_back(b);
+        break;
       }
-      break;  // GPK_CAP_MORE: the rest is carried into the next slot
+      good = pl.ok(hipEventRecord(B.k1, S.stream), "hipEventRecord") &&
+             pl.ok(hipMemcpyAsync(B.h_rec, B.d_rec, n * sizeof(gpk_record), hipMemcpyDeviceToHost, S.stream), "DtoH") &&
+             pl.ok(hipMemcpyAsync(B.h_err, B.d_err, n * 8, hipMemcpyDeviceToHost, S.stream), "DtoH") &&
+             pl.ok(hipMemcpyAsync(B.h_flow, B.d_flow, n * 24, hipMemcpyDeviceToHost, S.stream), "DtoH") &&
+             pl.ok(hipEventRecord(B.done, S.stream), "hipEventRecord");
+      pl.inflight.push_back(b);
+      packet_index += n;
+      stats->batches++;
+      for (uint64_t i = 0; i < n; i++) stats->packet_bytes += B.h_cap[i];
+      first += n;
+    }
+    gpk_capindex_free(&xi);
+    if (st == GPK_CAP_END) {
+      int is_eof = 0, is_panic = 0;
+      gpk_capreader_error(rd, stats->error, sizeof(stats->error), &is_eof, &is_panic);
+      stats->reader_status = is_eof ? 0 : (is_panic ? 2 : 1);
+      finished = true;
     }
     stats->slots++;
     carry = S.host + pos;

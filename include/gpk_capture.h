@@ -82,6 +82,24 @@ int gpk_capreader_index(gpk_capreader* r, const uint8_t* buf, uint64_t len, int 
                         uint32_t* caplens, gpk_capture_info* ci, uint64_t max_pkts, uint64_t* n_pkts,
                         uint64_t* consumed);
 
+/* The same result as gpk_capreader_index called until it stops (unbounded
+ * output), over buf[0, len), with the record walk split over `threads`
+ * threads: segments after the first are walked speculatively from a plausible
+ * chain of plain Enhanced Packet Blocks, and a segment's packets are kept
+ * only where the exact walk lands on its start with unchanged reader state,
+ * so the output is always the sequential one. Returns GPK_CAP_MORE or
+ * GPK_CAP_END (never FULL); the arrays are malloc'd by the library (release
+ * with gpk_capindex_free); offsets are relative to buf. */
+typedef struct gpk_capindex {
+  uint64_t n;
+  uint64_t* offsets;
+  uint32_t* caplens;
+  gpk_capture_info* ci;
+} gpk_capindex;
+int gpk_capreader_index_all(gpk_capreader* r, const uint8_t* buf, uint64_t len, int eof, int threads,
+                            gpk_capindex* out, uint64_t* consumed);
+int gpk_capindex_free(gpk_capindex* x);
+
 /* The error that ended the last GPK_CAP_END: the Go error text (io.EOF is
  * "EOF"); *is_eof = it is io.EOF; *is_panic = the reference panics there
  * (a runtime error its code does not recover). Returns the text length. */

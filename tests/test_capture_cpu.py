@@ -319,3 +319,81 @@ def test_python_mirror_gzip_and_batches():
     assert e.value.text == "unexpected EOF"
     with pytest.raises(EOFError):
         pcapgo.NewNgReader(b"")
+
+
+def index_all_events(stream, flags, threads, chunk=None):
+    """gpk_capreader_index_all over the stream (whole or in chunks), as events."""
+    L = _lib.lib()
+    h = ctypes.c_void_p()
+    _lib.check(L.gpk_capreader_create(ctypes.byref(h), _lib.CAP_PCAPNG, flags))
+    ev = []
+    base, have = 0, (len(stream) if chunk is None else min(len(stream), chunk))
+    try:
+        while True:
+            buf = np.frombuffer(stream[base:have], np.uint8) if have > base else np.zeros(1, np.uint8)
+            eof = have >= len(stream)
+            out, used = _lib.CapIndex(), ctypes.c_uint64()
+            rc = L.gpk_capreader_index_all(h, buf.ctypes.data, have - base, int(eof), threads, ctypes.byref(out),
+                                           ctypes.byref(used))
+            assert rc in (_lib.CAP_MORE, _lib.CAP_END), rc
+            n = out.n
+            if n:
+                off = np.ctypeslib.as_array(ctypes.cast(out.offsets, ctypes.POINTER(ctypes.c_uint64)), (n,))
+                cap = np.ctypeslib.as_array(ctypes.cast(out.caplens, ctypes.POINTER(ctypes.c_uint32)), (n,))
+                ci = np.ctypeslib.as_array(ctypes.cast(out.ci, ctypes.POINTER(ctypes.c_uint8)), (n * 24,)).view(
+                    _lib.CAPINFO_DTYPE)
+                for i in range(n):
+                    r = ci[i]
+                    ev.append(("pkt", base + int(off[i]), int(cap[i]), int(r["ts_sec"]), int(r["ts_nsec"]),
+                               int(r["length"]), int(r["iface"]),
+                               None if int(r["link_type"]) < 0 else int(r["link_type"])))
+            L.gpk_capindex_free(ctypes.byref(out))
+            base += used.value
+            if rc == _lib.CAP_END:
+                b = ctypes.create_string_buffer(512)
+                e, p = ctypes.c_int(), ctypes.c_int()
+                k = L.gpk_capreader_error(h, b, 512, ctypes.byref(e), ctypes.byref(p))
+                ev.append(("err", b.raw[:k].decode("latin-1"), bool(p.value)))
+                break
+            assert not eof
+            have = len(stream) if chunk is None else min(len(stream), have + chunk)
+    finally:
+        L.gpk_capreader_destroy(h)
+    return ev
+
+
+def big_capture(n=60000, seed=3):
+    from gopacket_amd import synth
+    rng = random.Random(seed)
+    pk = [synth.packet(4, i) for i in range(n)]
+    blocks = [pcapgen.epb(p, ts=i * 1000) for i, p in enumerate(pk)]
+    return pcapgen.shb() + pcapgen.idb(1, 0) + pcapgen.idb(1, 0), blocks, rng
+
+
+def test_parallel_walk_equals_sequential():
+    head, blocks, rng = big_capture()
+    variants = {"plain": blocks}
+    # state changes, non-plain blocks and a fake block chain inside packet data
+    v = list(blocks)
+    v.insert(20000, pcapgen.idb(0, 0))  # a Null-link interface: later packets on it are skipped
+    v[25000] = pcapgen.epb(bytes(100), iface=2)
+    v.insert(30000, pcapgen.epb(bytes(70), options=pcapgen.opt(1, b"comment") + pcapgen.end_opt()))
+    v.insert(35000, pcapgen.spb(bytes(90)))
+    v.insert(41000, pcapgen.shb(">") + pcapgen.idb(1, 0, ">"))
+    v[41001:] = [pcapgen.epb(pcapgen_payload(b), bo=">") for b in v[41001:]]
+    fake = b"".join(pcapgen.epb(bytes([7]) * 40, ts=5) for _ in range(6))
+    v.insert(15000, pcapgen.epb(bytes(3) + fake + bytes(5)))
+    variants["mixed"] = v
+    for name, bl in variants.items():
+        data = head + b"".join(bl)
+        for flags in (0, 1, 2):
+            want, _ = native_events(data, _lib.CAP_PCAPNG, flags, errors=1, max_events=10 ** 7)
+            for threads in (1, 3, 8):
+                assert index_all_events(data, flags, threads) == want, (name, flags, threads)
+            assert index_all_events(data, flags, 8, chunk=(5 << 20) + 13) == want, (name, flags)
+
+
+def pcapgen_payload(block):
+    """The packet bytes of a little-endian plain EPB built by pcapgen.epb."""
+    cl = int.from_bytes(block[20:24], "little")
+    return block[28:28 + cl]
