@@ -253,7 +253,7 @@ def test_pcap_matches_oracle():
     for _ in range(800):
         data = mutate(rng, rng.choice(cases))
         compare(data, _lib.CAP_PCAP, 0, errors=4)
-    # usec * 1000 wraps in uint32 (read.go:176): usec = 4294968 -> 4294968000 mod 2^32
+    # usec * 1000 wraps in uint32 (read.go:173): usec = 4294968 -> 4294968000 mod 2^32
     hdr = pcapgen.pcap_file([])
     rec = (5).to_bytes(4, "little") + (4294968).to_bytes(4, "little") + (2).to_bytes(4, "little") * 2 + b"ab"
     ev = compare(hdr + rec, _lib.CAP_PCAP, 0)

@@ -6,7 +6,8 @@ in interleaved rounds so clocks and thermals affect them alike.
 
     python tools/ab_inproc.py --configs c3,c2,c4 --rounds 5 --steps 5 base w6 w7 ...
 
-"base" = gopacket_amd/libgpk.so, NAME = gopacket_amd/build/libgpk_NAME.so.
+"base" = gopacket_amd/libgpk.so, NAME = gopacket_amd/build/libgpk_NAME.so;
+NAME@global runs that library with gpk_ctx_set_table_mode(GPK_TABLES_GLOBAL).
 Prints, per config and variant, the median and min kernel ms over rounds.
 """
 import argparse
@@ -43,7 +44,7 @@ def main():
     import torch
     import bench
     from gopacket_amd import _lib, engine, synth
-    libs = {v: load(v) for v in a.variants}
+    libs = {v: load(v.split("@")[0]) for v in a.variants}
     stream = torch.cuda.current_stream()
     for name in a.configs.split(","):
         cfg = bench.CONFIGS[name]
@@ -59,6 +60,8 @@ def main():
         for v, L in libs.items():
             ctx, p = ctypes.c_void_p(), ctypes.c_void_p()
             assert L.gpk_ctx_create(ctypes.byref(ctx), 0) == 0
+            if v.endswith("@global"):
+                assert L.gpk_ctx_set_table_mode(ctx, 1) == 0
             assert L.gpk_parser_create(ctypes.byref(p), 17) == 0
             for d in cfg["decoders"]:
                 assert L.gpk_parser_add_decoder(p, engine.DECODER_KINDS[d]) == 0
