@@ -59,7 +59,42 @@ EXPORTS = (
     "gpk_capreader_link_type", "gpk_capreader_pcap_header", "gpk_capreader_nsections", "gpk_capreader_section_info",
     "gpk_capreader_ninterfaces", "gpk_capreader_interface", "gpk_capreader_interface_str", "gpk_replay_file",
     "gpk_capreader_index_all", "gpk_capindex_free",
+    # include/gpk_afpacket.h
+    "gpk_tp_default_opts", "gpk_tp_check_opts", "gpk_tpacket_new", "gpk_tpacket_attach", "gpk_tpacket_close",
+    "gpk_tpacket_ring", "gpk_tpacket_index", "gpk_tpacket_defer", "gpk_tpacket_release_seq", "gpk_tpacket_release",
+    "gpk_tpacket_take_new_headers", "gpk_tpacket_geometry", "gpk_tpacket_error", "gpk_tpacket_stats",
+    "gpk_tpacket_socket_stats", "gpk_tpacket_set_bpf", "gpk_tpacket_set_fanout", "gpk_tpacket_pump",
 )
+
+# include/gpk_afpacket.h constants
+TPACKET_V1, TPACKET_V2, TPACKET_V3, TPACKET_HIGHEST = 0, 1, 2, -1
+TP_WAIT, TP_FULL, TP_ERROR = 0, 1, 2
+TPINFO_DTYPE = np.dtype([("ts_sec", "<i8"), ("ts_nsec", "<u4"), ("length", "<u4"), ("iface", "<i4"),
+                         ("vlan", "<i4")])
+
+
+class TpOpts(ctypes.Structure):
+    _fields_ = [("version", ctypes.c_int32), ("socktype", ctypes.c_int32), ("frame_size", ctypes.c_int32),
+                ("block_size", ctypes.c_int32), ("num_blocks", ctypes.c_int32), ("frames_per_block", ctypes.c_int32),
+                ("add_vlan_header", ctypes.c_int32), ("vnet_hdr_size", ctypes.c_int32),
+                ("block_timeout_ns", ctypes.c_int64), ("poll_timeout_ns", ctypes.c_int64),
+                ("protocol", ctypes.c_uint16), ("_pad", ctypes.c_uint16 * 3), ("iface", ctypes.c_char * 64)]
+
+
+class PumpOpts(ctypes.Structure):
+    _fields_ = [("batch_pkts", ctypes.c_uint64), ("max_packets", ctypes.c_uint64), ("wait", ctypes.c_int),
+                ("inflight", ctypes.c_int)]
+
+
+class PumpStats(ctypes.Structure):
+    _fields_ = [("packets", ctypes.c_uint64), ("packet_bytes", ctypes.c_uint64), ("batches", ctypes.c_uint64),
+                ("ring_bytes_copied", ctypes.c_uint64), ("waits", ctypes.c_uint64), ("wall_s", ctypes.c_double),
+                ("index_s", ctypes.c_double), ("gpu_s", ctypes.c_double), ("kernel_s", ctypes.c_double),
+                ("status", ctypes.c_int), ("error", ctypes.c_char * 160)]
+
+
+PUMP_CB = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p,
+                           ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p)
 
 # include/gpk_capture.h constants
 CAP_PCAP, CAP_PCAPNG = 1, 2
@@ -180,6 +215,24 @@ def lib():
         "gpk_replay_file": ([vp, vp, ctypes.c_char_p, P(ReplayOpts), REPLAY_CB, vp, P(ReplayStats)], c_int),
         "gpk_capreader_index_all": ([vp, vp, u64, c_int, c_int, P(CapIndex), P(u64)], c_int),
         "gpk_capindex_free": ([P(CapIndex)], c_int),
+        "gpk_tp_default_opts": ([P(TpOpts)], None),
+        "gpk_tp_check_opts": ([P(TpOpts), ctypes.c_char_p, ctypes.c_size_t], c_int),
+        "gpk_tpacket_new": ([P(vp), P(TpOpts), ctypes.c_char_p, ctypes.c_size_t], c_int),
+        "gpk_tpacket_attach": ([P(vp), vp, u64, c_int, P(TpOpts)], c_int),
+        "gpk_tpacket_close": ([vp], c_int),
+        "gpk_tpacket_ring": ([vp, P(vp), P(u64), P(c_int), P(c_int)], c_int),
+        "gpk_tpacket_index": ([vp, c_int, vp, vp, vp, u64, P(u64), vp, u64, P(u64)], c_int),
+        "gpk_tpacket_defer": ([vp, c_int], c_int),
+        "gpk_tpacket_release_seq": ([vp, P(u64)], c_int),
+        "gpk_tpacket_release": ([vp, u64], c_int),
+        "gpk_tpacket_take_new_headers": ([vp, P(u64), P(u64)], c_int),
+        "gpk_tpacket_geometry": ([vp, P(u64), P(u64)], c_int),
+        "gpk_tpacket_error": ([vp, ctypes.c_char_p, ctypes.c_size_t, P(c_int)], c_int),
+        "gpk_tpacket_stats": ([vp, P(i64), P(i64)], c_int),
+        "gpk_tpacket_socket_stats": ([vp, P(u32), P(u32), P(u32)], c_int),
+        "gpk_tpacket_set_bpf": ([vp, vp, u32], c_int),
+        "gpk_tpacket_set_fanout": ([vp, c_int, ctypes.c_uint16], c_int),
+        "gpk_tpacket_pump": ([vp, vp, vp, P(PumpOpts), PUMP_CB, vp, P(PumpStats)], c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -225,5 +278,12 @@ def synth_lib():
         S.gpk_probe_read.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int,
                                      ctypes.c_void_p]
         S.gpk_probe_read.restype = ctypes.c_int
+        S.gpk_synth_tpacket_v3.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int,
+                                           ctypes.c_uint64, ctypes.c_int32, ctypes.c_uint32, ctypes.c_void_p]
+        S.gpk_synth_tpacket_v3.restype = ctypes.c_uint64
+        S.gpk_synth_tp_producer_start.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32]
+        S.gpk_synth_tp_producer_start.restype = ctypes.c_void_p
+        S.gpk_synth_tp_producer_stop.argtypes = [ctypes.c_void_p]
+        S.gpk_synth_tp_producer_stop.restype = ctypes.c_uint64
         _synth = S
     return _synth

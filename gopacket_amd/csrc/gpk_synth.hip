@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <cstring>
+#include <atomic>
 #include <thread>
 #include <vector>
 #include <hipcub/hipcub.hpp>
@@ -232,6 +233,117 @@ uint64_t gpk_synth_write_pcapng(const char* path, int cfg, uint64_t first, uint6
   for (int t = 0; t < T; t++) ok = ok && good[t];
   close(fd);
   return ok ? start[T] : 0;
+}
+
+// ---- AF_PACKET TPACKET_V3 rings (bench / test infrastructure) -------------
+// Blocks laid out the way the Linux kernel fills them for a SOCK_RAW socket on
+// an Ethernet device (measured on lo, tests/golden/afpacket/lo_v3.ring):
+// tpacket_block_desc {version 2, offset_to_priv 48, hdr_v1 {block_status,
+// num_pkts, offset_to_first_pkt 48, blk_len, seq_num, ts}}; packets chained
+// from offset 48 with tp_mac 82, tp_net 96, tp_next_offset =
+// TPACKET_ALIGN(82 + snaplen) (0 on the block's last packet), a sockaddr_ll at
+// +48. Packet k of the ring is synth packet first+k of config cfg. Every
+// vlan_every-th packet (0 = none) carries TP_STATUS_VLAN_VALID and a TCI.
+// Returns the packet count; counts[b] (optional) = packets of block b.
+static inline uint32_t tp_al(uint32_t x) { return (x + 15u) & ~15u; }
+
+uint64_t gpk_synth_tpacket_v3(uint8_t* ring, uint32_t block_size, uint32_t nblocks, int cfg, uint64_t first,
+                              int32_t ifindex, uint32_t vlan_every, uint64_t* counts) {
+  std::vector<uint64_t> start(nblocks + 1, first);
+  for (uint32_t b = 0; b < nblocks; b++) {  // packets per block from the lengths alone
+    uint64_t i = start[b];
+    uint32_t pos = 48;
+    while (pos + tp_al(82 + frame_len(cfg, i)) <= block_size) pos += tp_al(82 + frame_len(cfg, i++));
+    start[b + 1] = i;
+  }
+  const int T = (int)std::min<uint32_t>(16, std::max<uint32_t>(1, nblocks));
+  std::vector<std::thread> th;
+  for (int t = 0; t < T; t++)
+    th.emplace_back([&, t] {
+      for (uint32_t b = (uint32_t)t; b < nblocks; b += (uint32_t)T) {
+        uint8_t* B = ring + (uint64_t)b * block_size;
+        memset(B, 0, 48);
+        const uint64_t n = start[b + 1] - start[b];
+        uint32_t pos = 48, last = 48;
+        for (uint64_t k = 0; k < n; k++) {
+          const uint64_t i = start[b] + k;
+          uint8_t* P = B + pos;
+          memset(P, 0, 82);
+          const uint32_t snap = gpk_synth_fill(cfg, i, P + 82);
+          const uint32_t step = tp_al(82 + snap);
+          const bool vl = vlan_every && (i % vlan_every) == 0;
+          const uint32_t sec = 1600000000u + (uint32_t)(i / 1000000u), nsec = (uint32_t)(i % 1000000u) * 1000u;
+          const uint32_t status = 1u | (vl ? 0x10u : 0u), tci = vl ? (uint32_t)((i * 37u) & 0xfffu) | 0x2000u : 0u;
+          const uint32_t nxt = k + 1 < n ? step : 0u;
+          memcpy(P + 0, &nxt, 4);
+          memcpy(P + 4, &sec, 4);
+          memcpy(P + 8, &nsec, 4);
+          memcpy(P + 12, &snap, 4);
+          memcpy(P + 16, &snap, 4);
+          memcpy(P + 20, &status, 4);
+          const uint16_t mac = 82, net = 96;
+          memcpy(P + 24, &mac, 2);
+          memcpy(P + 26, &net, 2);
+          memcpy(P + 32, &tci, 4);
+          const uint16_t tpid = vl ? 0x8100 : 0;
+          memcpy(P + 36, &tpid, 2);
+          const uint16_t fam = 17, proto = 0x0008, hatype = 1;  // AF_PACKET, htons(ETH_P_IP), ARPHRD_ETHER
+          memcpy(P + 48, &fam, 2);
+          memcpy(P + 50, &proto, 2);
+          memcpy(P + 52, &ifindex, 4);
+          memcpy(P + 56, &hatype, 2);
+          P[58] = 0;  // PACKET_HOST
+          P[59] = 6;
+          memcpy(P + 60, P + 82 + 6, 6);  // source MAC
+          last = pos + 82 + snap;
+          pos += step;
+        }
+        const uint32_t hdr[6] = {2u, 48u, 0u, (uint32_t)n, 48u, (last + 7u) & ~7u};
+        memcpy(B, hdr, sizeof(hdr));
+        const uint64_t seq = b + 1;
+        memcpy(B + 24, &seq, 8);
+        __atomic_store_n(reinterpret_cast<uint32_t*>(B + 8), 1u, __ATOMIC_RELEASE);  // TP_STATUS_USER: hand it over
+        if (counts) counts[b] = n;
+      }
+    });
+  for (auto& x : th) x.join();
+  return start[nblocks] - first;
+}
+
+// Emulated kernel side of a ring for the capture benchmark: a thread that
+// hands every released block (block_status == 0) straight back to user space
+// (TP_STATUS_USER), in ring order, with its contents unchanged.
+struct TpProducer {
+  std::atomic<bool> stop{false};
+  std::atomic<uint64_t> rearmed{0};
+  std::thread th;
+};
+
+void* gpk_synth_tp_producer_start(uint8_t* ring, uint32_t block_size, uint32_t nblocks) {
+  TpProducer* p = new TpProducer();
+  p->th = std::thread([p, ring, block_size, nblocks] {
+    uint32_t b = 0;
+    while (!p->stop.load(std::memory_order_relaxed)) {
+      uint32_t* st = reinterpret_cast<uint32_t*>(ring + (uint64_t)b * block_size + 8);
+      if (__atomic_load_n(st, __ATOMIC_ACQUIRE) == 0) {
+        __atomic_store_n(st, 1u, __ATOMIC_RELEASE);
+        p->rearmed.fetch_add(1, std::memory_order_relaxed);
+        b = (b + 1) % nblocks;
+      } else {
+        std::this_thread::yield();
+      }
+    }
+  });
+  return p;
+}
+
+uint64_t gpk_synth_tp_producer_stop(void* h) {
+  TpProducer* p = static_cast<TpProducer*>(h);
+  p->stop = true;
+  p->th.join();
+  uint64_t n = p->rearmed.load();
+  delete p;
+  return n;
 }
 
 // Launch the streaming-read probe over data[0, nbytes & ~15) on `stream`.

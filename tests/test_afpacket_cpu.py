@@ -1,0 +1,337 @@
+"""AF_PACKET ring walker (gpk_afpacket.cpp, host code) against the oracle
+restatement of afpacket.TPacket.ZeroCopyReadPacketData
+(oracle/afpacket_oracle.py), on real kernel-filled rings captured on lo
+(tests/golden/afpacket/), on generated rings of all three TPACKET versions
+with every quirk the walk has, and on a live loopback capture.
+"""
+import ctypes
+import json
+import os
+import socket
+import struct
+
+import numpy as np
+import pytest
+
+import ringgen
+from gopacket_amd import _lib, afpacket
+from oracle import afpacket_oracle as AO
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "afpacket")
+
+
+def native_reader(ring, version, opts):
+    o = afpacket.parseOptions(*_opt_list(opts))
+    arr = np.frombuffer(ring, np.uint8)
+    h = ctypes.c_void_p()
+    _lib.check(_lib.lib().gpk_tpacket_attach(ctypes.byref(h), arr.ctypes.data, arr.nbytes, version, ctypes.byref(o)))
+    return h, arr
+
+
+def _opt_list(opts):
+    out = [afpacket.OptFrameSize(opts["frame_size"]), afpacket.OptBlockSize(opts["block_size"]),
+           afpacket.OptNumBlocks(opts["num_blocks"])]
+    if opts.get("add_vlan_header"):
+        out.append(afpacket.OptAddVLANHeader(1))
+    return out
+
+
+def native_index(h, ring_len, m, side):
+    off = np.zeros(max(m, 1), np.uint64)
+    cap = np.zeros(max(m, 1), np.uint32)
+    ci = np.zeros(max(m, 1), _lib.TPINFO_DTYPE)
+    n, used = ctypes.c_uint64(), ctypes.c_uint64()
+    st = _lib.lib().gpk_tpacket_index(h, 0, off.ctypes.data, cap.ctypes.data, ci.ctypes.data, m, ctypes.byref(n),
+                                      side.ctypes.data, len(side), ctypes.byref(used))
+    k = n.value
+    pk = []
+    for i in range(k):
+        o, c = int(off[i]), int(cap[i])
+        pk.append(bytes(side[o - ring_len:o - ring_len + c]) if o >= ring_len else None)
+    recs = [(int(off[i]), int(cap[i]), int(ci[i]["ts_sec"]), int(ci[i]["ts_nsec"]), int(ci[i]["length"]),
+             int(ci[i]["iface"]), int(ci[i]["vlan"])) for i in range(k)]
+    return recs, pk, st
+
+
+def native_error(h):
+    buf = ctypes.create_string_buffer(256)
+    pan = ctypes.c_int()
+    _lib.lib().gpk_tpacket_error(h, buf, 256, ctypes.byref(pan))
+    return buf.value.decode(), bool(pan.value)
+
+
+def rearm(ring, version, opts, h):
+    if version == AO.V3:
+        struct.pack_into("<I", ring, h * opts["block_size"] + 8, 1)
+    else:
+        struct.pack_into("<I", ring, h * opts["frame_size"], 1)
+
+
+def compare(ring0, version, opts, rng, rounds=6):
+    """Walk the same ring with the native reader and the oracle, in random call
+    sizes, re-arming random headers (an emulated kernel) at every wait."""
+    ring_n, ring_o = bytearray(ring0), bytearray(ring0)
+    h, arr = native_reader(ring_n, version, opts)
+    try:
+        orc = AO.TPacketOracle(ring_o, version, dict(opts))
+        side = np.zeros(1 << 16, np.uint8)
+        nh = opts["num_blocks"] if version == AO.V3 else opts["num_blocks"] * opts["block_size"] // opts["frame_size"]
+        total = 0
+        for _ in range(rounds):
+            m = int(rng.integers(1, 40))
+            got, side_pk, st = native_index(h, len(ring_n), m, side)
+            exp, kind, err = orc.read_until_stop(m)
+            # side offsets: the native side buffer restarts each call, the oracle's grows
+            assert len(got) == len(exp)
+            for g, e, spk in zip(got, exp, side_pk):
+                if e[0] >= len(ring_o):
+                    assert g[0] >= len(ring_n) and spk == orc.data(e[0], e[1]), (g, e)
+                    assert g[1:] == e[1:]
+                else:
+                    assert g == e
+            total += len(got)
+            assert st == {"full": _lib.TP_FULL, AO.WAIT: _lib.TP_WAIT, AO.ERROR: _lib.TP_ERROR}[kind], (st, kind)
+            if kind == AO.ERROR:
+                text, panic = native_error(h)
+                assert text == err
+                break
+            if kind == AO.WAIT:
+                for _k in range(int(rng.integers(1, 4))):
+                    hh = int(rng.integers(0, nh))
+                    rearm(ring_n, version, opts, hh)
+                    rearm(ring_o, version, opts, hh)
+        assert bytes(ring_n) == bytes(ring_o)  # the same headers released
+        p, q = ctypes.c_int64(), ctypes.c_int64()
+        _lib.lib().gpk_tpacket_stats(h, ctypes.byref(p), ctypes.byref(q))
+        assert p.value == orc.packets
+        return total
+    finally:
+        _lib.lib().gpk_tpacket_close(h)
+
+
+# ---- options (afpacket_test.go TestParseOptions) -----------------------------
+
+def test_parse_options_table():
+    # afpacket_test.go:17-41
+    for opts, err in (([afpacket.OptBlockSize(2)], True), ([afpacket.OptFrameSize(333)], True),
+                      ([afpacket.OptTPacketVersion(-3)], True), ([afpacket.OptTPacketVersion(5)], True),
+                      ([afpacket.OptFrameSize(1 << 10)], False)):
+        if err:
+            with pytest.raises(afpacket.AfpacketError):
+                afpacket.parseOptions(*opts)
+        else:
+            o = afpacket.parseOptions(*opts)
+            assert o.frame_size == 1 << 10 and o.block_size == afpacket.DefaultBlockSize
+            assert o.frames_per_block == afpacket.DefaultBlockSize // (1 << 10)
+            assert o.num_blocks == 128 and o.block_timeout_ns == 64_000_000 and o.poll_timeout_ns == -1_000_000
+            assert o.version == -1 and o.socktype == 3 and o.protocol == 3
+    # the texts of options.check (options.go:197-211)
+    with pytest.raises(afpacket.AfpacketError, match=r"^block size 2 must be divisible by page size 4096$"):
+        afpacket.parseOptions(afpacket.OptBlockSize(2))
+    with pytest.raises(afpacket.AfpacketError, match=r"^block size 524288 must be divisible by frame size 333$"):
+        afpacket.parseOptions(afpacket.OptFrameSize(333))
+    with pytest.raises(afpacket.AfpacketError, match=r"^num blocks 0 must be >= 1$"):
+        afpacket.parseOptions(afpacket.OptNumBlocks(0))
+    with pytest.raises(afpacket.AfpacketError, match=r"^tpacket version InvalidVersion is invalid$"):
+        afpacket.parseOptions(afpacket.OptTPacketVersion(5))
+    with pytest.raises(afpacket.AfpacketError, match=r"^block timeout 500µs must be > 1ms$"):
+        afpacket.parseOptions(afpacket.OptBlockTimeout(500_000))
+    with pytest.raises(afpacket.AfpacketError, match="unknown type in options"):
+        afpacket.parseOptions(3.5)
+
+
+# ---- real kernel rings --------------------------------------------------------
+
+def _gold():
+    meta = json.load(open(os.path.join(GOLD, "lo_rings.json")))
+    for r in meta["rings"]:
+        yield meta, r, bytearray(open(os.path.join(GOLD, r["file"]), "rb").read())
+
+
+def test_kernel_rings_match_oracle_and_sent_datagrams():
+    for meta, r, ring in _gold():
+        opts = dict(frame_size=r["frame_size"], block_size=r["block_size"], num_blocks=r["num_blocks"])
+        orc = AO.TPacketOracle(bytearray(ring), r["version"], dict(opts))
+        exp, kind, _ = orc.read_until_stop()
+        assert kind == AO.WAIT and len(exp) >= 12
+        # what was sent: every UDP datagram to the port, twice (out + in on lo), in order
+        udp = []
+        for e in exp:
+            d = orc.data(e[0], e[1])
+            assert e[1] == e[4] and e[5] == 1  # caplen == length, ifindex of lo
+            if d[12:14] == b"\x08\x00" and d[23] == 17 and struct.unpack(">H", d[36:38])[0] == r["udp_port"]:
+                udp.append(d[42:])
+        sent = [bytes.fromhex(x) for x in meta["payloads_hex"]]
+        assert udp == [p for p in sent for _ in (0, 1)][:len(udp)] and len(udp) >= 6
+        # the native walker agrees, bit for bit, and releases the same headers
+        compare(ring, r["version"], opts, np.random.default_rng(1), rounds=3)
+
+
+# ---- generated rings ------------------------------------------------------------
+
+@pytest.mark.parametrize("vlan", [False, True])
+def test_random_v3_rings(vlan):
+    rng = np.random.default_rng(7 + vlan)
+    n = 0
+    for _ in range(300):
+        ring = ringgen.random_v3(rng)
+        n += compare(ring, AO.V3, dict(frame_size=2048, block_size=4096, num_blocks=6, add_vlan_header=vlan), rng)
+    assert n > 2000
+
+
+@pytest.mark.parametrize("version", [AO.V1, AO.V2])
+@pytest.mark.parametrize("vlan", [False, True])
+def test_random_frame_rings(version, vlan):
+    rng = np.random.default_rng(11 + version * 2 + vlan)
+    n = 0
+    for _ in range(300):
+        ring = ringgen.random_frames(rng, version)
+        n += compare(ring, version, dict(frame_size=512, block_size=4096, num_blocks=2, add_vlan_header=vlan), rng)
+    assert n > 2000
+
+
+def test_empty_block_retry_and_vlan_edge_cases():
+    pk = lambda n, s=0: bytes((s + i) & 0xFF for i in range(n))  # noqa: E731
+    opts = dict(frame_size=4096, block_size=4096, num_blocks=4)
+    cases = [
+        # first packet of a block with tp_len 0: the block is skipped on a fresh header
+        [dict(status=1, pkts=[dict(data=pk(60), length=0), dict(data=pk(70))]), dict(status=1, pkts=[dict(data=pk(61))])],
+        # an empty block (num_pkts 0) between full ones
+        [dict(status=1, pkts=[dict(data=pk(60))]), dict(status=1, pkts=[], num_pkts=0),
+         dict(status=1, pkts=[dict(data=pk(62)), dict(data=pk(63), next="zero"), dict(data=pk(64))])],
+        # VLAN-tagged packets, one shorter than 12 bytes (insertVlanHeader panics)
+        [dict(status=1, pkts=[dict(data=pk(60), tci=0x123, pstatus=0x11), dict(data=pk(8), tci=7)])],
+        # a chain that leaves the ring (the reference would fault)
+        [dict(status=1, pkts=[dict(data=pk(60), next=1 << 20), dict(data=pk(60))])],
+        # nanoseconds beyond one second (time.Unix normalises)
+        [dict(status=1, pkts=[dict(data=pk(60), sec=5, nsec=4_000_000_000)])],
+    ]
+    rng = np.random.default_rng(3)
+    for blocks in cases:
+        for vlan in (False, True):
+            ring = ringgen.v3_ring(blocks, 4096, 4)
+            compare(ring, AO.V3, dict(opts, add_vlan_header=vlan), rng, rounds=4)
+    # the panic text
+    ring = ringgen.v3_ring(cases[2], 4096, 4)
+    orc = AO.TPacketOracle(bytearray(ring), AO.V3, dict(opts, add_vlan_header=True))
+    out, kind, err = orc.read_until_stop()
+    assert len(out) == 1 and kind == AO.ERROR and err == "runtime error: slice bounds out of range [:12] with capacity 8"
+
+
+def test_deferred_release_holds_headers_until_released():
+    rng = np.random.default_rng(5)
+    blocks = [dict(status=1, pkts=[dict(data=ringgen.random_packet(rng, 20, 200)) for _ in range(5)])
+              for _ in range(4)]
+    ring = ringgen.v3_ring(blocks, 4096, 4)
+    opts = dict(frame_size=4096, block_size=4096, num_blocks=4)
+    h, arr = native_reader(ring, AO.V3, opts)
+    L = _lib.lib()
+    try:
+        L.gpk_tpacket_defer(h, 1)
+        side = np.zeros(4096, np.uint8)
+        got, _, st = native_index(h, len(ring), 100, side)
+        assert len(got) == 20 and st == _lib.TP_WAIT
+        status = lambda b: struct.unpack_from("<I", ring, b * 4096 + 8)[0]  # noqa: E731
+        assert [status(b) for b in range(4)] == [1, 1, 1, 1]  # all four finished, none handed back
+        first, count = ctypes.c_uint64(), ctypes.c_uint64()
+        L.gpk_tpacket_take_new_headers(h, ctypes.byref(first), ctypes.byref(count))
+        assert (first.value, count.value) == (0, 4)
+        seq = ctypes.c_uint64()
+        L.gpk_tpacket_release_seq(h, ctypes.byref(seq))
+        assert seq.value == 4  # the walk moved past block 3 and stopped at deferred block 0
+        L.gpk_tpacket_release(h, 2)
+        assert [status(b) for b in range(4)] == [0, 0, 1, 1]
+        L.gpk_tpacket_release(h, 3)
+        assert [status(b) for b in range(4)] == [0, 0, 0, 1]
+        # the same blocks handed over again: the walk goes on into block 0
+        struct.pack_into("<I", ring, 8, 1)
+        got2, _, st = native_index(h, len(ring), 100, side)
+        assert len(got2) == 5 and got2[0][0] == got[0][0]
+    finally:
+        L.gpk_tpacket_close(h)
+
+
+def test_python_mirror_reads_like_the_reference():
+    rng = np.random.default_rng(9)
+    blocks = [dict(status=1, pkts=[dict(data=ringgen.random_packet(rng, 20, 200), tci=0x42, pstatus=0x11)
+                                  for _ in range(3)])]
+    ring = ringgen.v3_ring(blocks, 4096, 2)
+    tp = afpacket.AttachRing(ring, afpacket.TPacketVersion3, afpacket.OptFrameSize(4096),
+                             afpacket.OptBlockSize(4096), afpacket.OptNumBlocks(2), afpacket.OptAddVLANHeader(True))
+    orc = AO.TPacketOracle(bytearray(ring), AO.V3, dict(frame_size=4096, block_size=4096, num_blocks=2,
+                                                       add_vlan_header=True))
+    for _ in range(3):
+        d, ci = tp.ZeroCopyReadPacketData()
+        k, e = orc.read()
+        assert d == orc.data(e[0], e[1]) and d[12:16] == b"\x81\x00\x00\x42"
+        assert ci.Timestamp == (e[2], e[3]) and ci.CaptureLength == e[1] and ci.Length == e[4]
+        assert ci.InterfaceIndex == e[5] and ci.AncillaryData == [afpacket.AncillaryVLAN(0x42)]
+    with pytest.raises(afpacket.WouldBlock):
+        tp.ZeroCopyReadPacketData()
+    assert tp.Stats() == afpacket.Stats(3, 0)
+    tp.Close()
+
+
+def test_synth_v3_ring_walks_like_the_oracle():
+    """The benchmark's ring generator (libgpk_synth) writes what the oracle reads."""
+    S = _lib.synth_lib()
+    from gopacket_amd import synth
+    ring = np.zeros(8 * 65536, np.uint8)
+    counts = np.zeros(8, np.uint64)
+    n = S.gpk_synth_tpacket_v3(ring.ctypes.data, 65536, 8, synth.C4_IMIX, 100, 4, 5, counts.ctypes.data)
+    assert n == counts.sum() and n > 8 * 100
+    orc = AO.TPacketOracle(bytearray(ring.tobytes()), AO.V3, dict(frame_size=4096, block_size=65536, num_blocks=8))
+    out, kind, _ = orc.read_until_stop()
+    assert kind == AO.WAIT and len(out) == n
+    for k in (0, 1, int(n) // 2, int(n) - 1):
+        e = out[k]
+        assert orc.data(e[0], e[1]) == synth.packet(synth.C4_IMIX, 100 + k)
+        assert e[6] == ((((100 + k) * 37) & 0xFFF) if (100 + k) % 5 == 0 else -1)
+    compare(bytearray(ring.tobytes()), AO.V3, dict(frame_size=4096, block_size=65536, num_blocks=8),
+            np.random.default_rng(2), rounds=4)
+
+
+# ---- live capture ------------------------------------------------------------------
+
+def _can_capture():
+    try:
+        s = socket.socket(socket.AF_PACKET, socket.SOCK_RAW, socket.htons(3))
+        s.close()
+        return hasattr(socket, "if_nametoindex") and socket.if_nametoindex("lo") > 0
+    except (OSError, AttributeError):
+        return False
+
+
+@pytest.mark.skipif(not _can_capture(), reason="AF_PACKET sockets need CAP_NET_RAW")
+@pytest.mark.parametrize("version", [afpacket.TPacketVersion3, afpacket.TPacketVersion2, afpacket.TPacketVersion1])
+def test_live_loopback_capture(version):
+    tp = afpacket.NewTPacket(afpacket.OptInterface("lo"), afpacket.OptTPacketVersion(version),
+                             afpacket.OptFrameSize(2048), afpacket.OptBlockSize(1 << 16), afpacket.OptNumBlocks(8),
+                             afpacket.OptBlockTimeout(5_000_000), afpacket.OptPollTimeout(2_000_000_000))
+    assert tp.version == version and tp.fd >= 0
+    port = 41000 + version
+    rx = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
+    rx.bind(("127.0.0.1", port))
+    u = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
+    sent = [bytes([i]) * (10 + 37 * i) for i in range(10)]
+    for p in sent:
+        u.sendto(p, ("127.0.0.1", port))
+    seen = []
+    try:
+        while len(seen) < len(sent):
+            d, ci = tp.ReadPacketData()
+            if len(d) >= 42 and d[12:14] == b"\x08\x00" and d[23] == 17 and struct.unpack(">H", d[36:38])[0] == port:
+                seen.append(d[42:])
+                assert ci.CaptureLength == len(d) and ci.Length == len(d) and ci.InterfaceIndex == 1
+    except afpacket.AfpacketError as e:
+        pytest.fail("capture ended: %s after %d" % (e, len(seen)))
+    finally:
+        u.close()
+        rx.close()
+    # on lo each datagram shows up once outgoing and once incoming
+    assert [p for p in seen] == [p for p in sent for _ in (0, 1)][:len(seen)]
+    st = tp.Stats()
+    assert st.Packets >= len(seen)
+    tp.SetBPF([(0x06, 0, 0, 0)])  # "ret #0": drop everything
+    tp.SetBPF([])
+    tp.Close()

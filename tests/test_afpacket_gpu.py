@@ -1,0 +1,97 @@
+"""gpk_tpacket_pump (AF_PACKET ring -> HBM mirror -> decode -> results)
+against the oracles: the afpacket ring-walk oracle for the packet stream and
+CaptureInfo, the decode oracle for every result. Small batches and few
+in-flight slots force blocks to be continued across batches, mirror regions
+to be reused and deferred headers to be released mid-run.
+"""
+import numpy as np
+import pytest
+
+import pktutil
+import ringgen
+from configs import CONFIGS, assert_same, device_parser, oracle_parser
+from gopacket_amd import _lib, afpacket, synth
+from oracle import afpacket_oracle as AO
+
+pytestmark = pytest.mark.gpu
+
+
+def expect(ring, version, opts):
+    orc = AO.TPacketOracle(bytearray(ring), version, dict(opts))
+    out, kind, err = orc.read_until_stop()
+    return [orc.data(e[0], e[1]) for e in out], out
+
+
+def check(gpu_ctx, tp, pk, exp, cfg="statsassembly", **kw):
+    got, st = tp.Pump(gpu_ctx, device_parser(CONFIGS[cfg]), **kw)
+    assert st["packets"] == len(pk), st
+    data, off, cap = pktutil.pack(pk)
+    ref = oracle_parser(CONFIGS[cfg]).decode(data, off, cap, nthreads=8, layouts=False)
+    assert_same(got, ref, "pump")
+    assert np.array_equal(got["caplens"], cap)
+    ci = got["ci"]
+    assert [(int(a), int(b), int(c), int(d), int(e)) for a, b, c, d, e in
+            zip(ci["ts_sec"], ci["ts_nsec"], ci["length"], ci["iface"], ci["vlan"])] == \
+        [(e[2], e[3], e[4], e[5], e[6]) for e in exp]
+    return st
+
+
+@pytest.mark.parametrize("vlan", [False, True])
+@pytest.mark.parametrize("batch,inflight", [(97, 2), (1000, 3), (1 << 20, 4)])
+def test_pump_synth_v3_ring(gpu_ctx, vlan, batch, inflight):
+    S = _lib.synth_lib()
+    bs, nb = 65536, 16
+    ring = np.zeros(bs * nb, np.uint8)
+    n = S.gpk_synth_tpacket_v3(ring.ctypes.data, bs, nb, synth.C4_IMIX, 1234, 7, 3, None)
+    opts = dict(frame_size=4096, block_size=bs, num_blocks=nb, add_vlan_header=vlan)
+    pk, exp = expect(ring.tobytes(), AO.V3, opts)
+    assert len(pk) == n
+    args = [afpacket.OptFrameSize(4096), afpacket.OptBlockSize(bs), afpacket.OptNumBlocks(nb)]
+    if vlan:
+        args.append(afpacket.OptAddVLANHeader(True))
+    tp = afpacket.AttachRing(ring, afpacket.TPacketVersion3, *args)
+    st = check(gpu_ctx, tp, pk, exp, batch_pkts=batch, inflight=inflight)
+    assert st["ring_bytes_copied"] == bs * nb
+    # every block handed back to the kernel at the end
+    assert all(int(ring[b * bs + 8]) == 0 for b in range(nb))
+    tp.Close()
+
+
+def test_pump_laps_the_ring_with_a_producer(gpu_ctx):
+    """An emulated kernel re-arms each released block: the pump goes round the
+    ring several times; packet k is ring packet k mod n."""
+    S = _lib.synth_lib()
+    bs, nb = 65536, 8
+    ring = np.zeros(bs * nb, np.uint8)
+    n = int(S.gpk_synth_tpacket_v3(ring.ctypes.data, bs, nb, synth.C3_TCP1500, 0, 7, 0, None))
+    opts = dict(frame_size=4096, block_size=bs, num_blocks=nb)
+    pk, exp = expect(ring.tobytes(), AO.V3, opts)
+    tp = afpacket.AttachRing(ring, afpacket.TPacketVersion3, afpacket.OptFrameSize(4096), afpacket.OptBlockSize(bs),
+                             afpacket.OptNumBlocks(nb), afpacket.OptPollTimeout(5_000_000_000))
+    prod = S.gpk_synth_tp_producer_start(ring.ctypes.data, bs, nb)
+    try:
+        laps = 5
+        st = check(gpu_ctx, tp, pk * laps, exp * laps, cfg="eth_ip4_tcp_payload", batch_pkts=50, inflight=3,
+                   max_packets=n * laps, wait=True)
+    finally:
+        rearmed = S.gpk_synth_tp_producer_stop(prod)
+    assert rearmed >= nb * (laps - 1)
+    assert st["ring_bytes_copied"] >= bs * nb * laps
+    tp.Close()
+
+
+@pytest.mark.parametrize("version", [AO.V1, AO.V2])
+def test_pump_frame_rings(gpu_ctx, version):
+    fz = pktutil.fuzz_packets(21 + version, 64)
+    # well-formed C4 packets and fuzzed ones; frame 50 not handed over (the walk stops there)
+    pkts = [synth.packet(synth.C4_IMIX, i * 7) if i % 3 else fz[i] for i in range(64)]
+    frames = [dict(status=0 if i == 50 else 1, data=p[:1900], tci=(i * 11) & 0xFFF if i % 4 == 0 else 0)
+              for i, p in enumerate(pkts)]
+    ring = ringgen.frame_ring(version, frames, 2048, 64)
+    opts = dict(frame_size=2048, block_size=8192, num_blocks=16, add_vlan_header=True)
+    pk, exp = expect(ring, version, opts)
+    assert len(pk) == 50
+    tp = afpacket.AttachRing(np.frombuffer(ring, np.uint8).copy(), version, afpacket.OptFrameSize(2048),
+                             afpacket.OptBlockSize(8192), afpacket.OptNumBlocks(16), afpacket.OptAddVLANHeader(True))
+    check(gpu_ctx, tp, pk, exp, batch_pkts=7, inflight=2)
+    tp.Close()

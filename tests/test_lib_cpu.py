@@ -17,7 +17,7 @@ def header_functions():
     names = set()
     for h in sorted(os.listdir(os.path.join(ROOT, "include"))):
         src = open(os.path.join(ROOT, "include", h)).read()
-        names |= set(re.findall(r"^(?:int|int64_t|const char\*)\s+(gpk_\w+)\(", src, re.M))
+        names |= set(re.findall(r"^(?:int|int64_t|void|const char\*)\s+(gpk_\w+)\(", src, re.M))
     return sorted(names)
 
 
