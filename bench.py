@@ -276,7 +276,7 @@ def c5_replay(ctx, gib=10.0, reps=2, threads=16):
                 source="page-cached file in %s" % os.path.dirname(path))
 
 
-def afpacket_pump(ctx, packets=16 * 2**20, block_mib=4, blocks=64, reps=2):
+def afpacket_pump(ctx, packets=16 * 2**20, block_mib=4, blocks=64, reps=2, batch=1 << 18):
     """Row (f)2: a TPACKET_V3 ring (blocks x block_mib MiB, laid out as the
     kernel fills it, C4 IMIX packets) drained by gpk_tpacket_pump: ring walk ->
     HtoD of each retired block into the HBM mirror -> decode -> DtoH, blocks
@@ -293,8 +293,6 @@ def afpacket_pump(ctx, packets=16 * 2**20, block_mib=4, blocks=64, reps=2):
     ring = np.zeros(bs * blocks, np.uint8)
     counts = np.zeros(blocks, np.uint64)
     n_ring = int(S.gpk_synth_tpacket_v3(ring.ctypes.data, bs, blocks, 4, 0, 2, 0, counts.ctypes.data))
-    tp = afpacket.AttachRing(ring, afpacket.TPacketVersion3, afpacket.OptFrameSize(4096), afpacket.OptBlockSize(bs),
-                             afpacket.OptNumBlocks(blocks), afpacket.OptPollTimeout(10_000_000_000))
     rng = np.random.default_rng(6)
     sample = sorted(set(int(x) for x in rng.integers(0, packets, 2048)) | {0, packets - 1})
     picked = {}
@@ -306,16 +304,20 @@ def afpacket_pump(ctx, packets=16 * 2**20, block_mib=4, blocks=64, reps=2):
             picked[i] = (rec[j].copy(), fl[[j, k + j, 2 * k + j]].copy())
 
     runs = []
-    for _ in range(reps):
+    for _ in range(reps):  # each run: a fresh reader on a ring whose blocks are all handed over
         picked.clear()
+        ring[8::bs] = 1
+        tp = afpacket.AttachRing(ring, afpacket.TPacketVersion3, afpacket.OptFrameSize(4096),
+                                 afpacket.OptBlockSize(bs), afpacket.OptNumBlocks(blocks),
+                                 afpacket.OptPollTimeout(10_000_000_000))
         prod = S.gpk_synth_tp_producer_start(ring.ctypes.data, bs, blocks)
         try:
-            _, st = tp.Pump(ctx, parser, batch_pkts=1 << 20, max_packets=packets, wait=True, inflight=4,
+            _, st = tp.Pump(ctx, parser, batch_pkts=batch, max_packets=packets, wait=True, inflight=4,
                             collect=False, on_batch=on_batch)
         finally:
             S.gpk_synth_tp_producer_stop(prod)
+            tp.Close()
         runs.append(st)
-    tp.Close()
     st = min(runs, key=lambda x: x["wall_s"])
     # packet k of the pump is ring packet k mod n_ring, i.e. synth packet k mod n_ring
     idx = sorted(picked)
@@ -337,7 +339,7 @@ def afpacket_pump(ctx, packets=16 * 2**20, block_mib=4, blocks=64, reps=2):
                 runs_wall_s=[round(r["wall_s"], 4) for r in runs],
                 breakdown_s=dict(index=round(st["index_s"], 4), gpu_copy_decode=round(st["gpu_s"], 4),
                                  kernel=round(st["kernel_s"], 4)),
-                batches=st["batches"], waits=st["waits"],
+                batches=st["batches"], batch_pkts=batch, waits=st["waits"],
                 parity="%s (%d sampled packets vs oracle)" % ("bit-exact" if ok else "MISMATCH", len(idx)))
 
 

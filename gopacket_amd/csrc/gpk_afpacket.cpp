@@ -119,6 +119,16 @@ struct gpk_tpacket {
   bool panic = false, dead = false;
   // SocketStats accumulators
   uint32_t ss_packets = 0, ss_drops = 0, ss_freeze = 0;
+  // V3 blocks walked ahead in parallel (prewalk), valid for one index call
+  struct Pre {
+    uint64_t epoch = 0;
+    std::vector<uint64_t> off, pos;
+    std::vector<uint32_t> cap;
+    std::vector<gpk_tp_info> ci;
+  };
+  std::vector<Pre> pre;
+  uint64_t epoch = 0;
+  int threads = 16;
 };
 
 namespace {
@@ -399,7 +409,114 @@ int init_geometry(gpk_tpacket* t) {
   if (t->hdr_bytes * t->nhdr > t->bytes) return GPK_EINVAL;
   t->pending.assign(t->nhdr, 0);
   t->fresh.assign(t->nhdr, 1);
+  if (t->version == GPK_TPACKET_V3) t->pre.resize(t->nhdr);
   return GPK_OK;
+}
+
+// Walk V3 blocks the way consecutive ZeroCopyReadPacketData calls would,
+// from each one's first packet to its last, without touching the reader's
+// state. A walk is valid only for a block the reference would read packet by
+// packet with no special case (handed over, not deferred, a non-empty first
+// packet, every header and byte inside the ring, no VLAN header to insert).
+// The chain inside a block is a dependent load per packet; G blocks are
+// walked in lockstep so that G loads are in flight at once.
+struct Chain {
+  gpk_tpacket::Pre* P;
+  uint64_t pos;
+  uint32_t k, n;
+  bool live;
+};
+
+bool chain_start(gpk_tpacket* t, uint64_t h, Chain& c) {
+  c.P = &t->pre[h];
+  c.live = false;
+  if (t->pending[h] || !(header_status(t, h) & kStatusUser)) return false;
+  const uint64_t base = header_pos(t, h);
+  c.n = ld<uint32_t>(t->ring + base + 12);
+  if (c.n == 0) return false;
+  c.P->off.resize(c.n);
+  c.P->pos.resize(c.n);
+  c.P->cap.resize(c.n);
+  c.P->ci.resize(c.n);
+  c.pos = base + ld<uint32_t>(t->ring + base + 16);
+  c.k = 0;
+  c.live = true;
+  return true;
+}
+
+// one packet of a chain: false when the chain ended (done or refused)
+inline bool chain_step(const gpk_tpacket* t, Chain& c, bool& ok) {
+  const uint64_t pos = c.pos;
+  if (pos > t->bytes || t->bytes - pos < kV3Hdr + 8 + 4) return ok = false;  // header + sockaddr_ll ifindex
+  const uint8_t* p = t->ring + pos;
+  const uint32_t snap = ld<uint32_t>(p + 12), len = ld<uint32_t>(p + 16), st = ld<uint32_t>(p + 20);
+  const uint16_t mac = ld<uint16_t>(p + 24);
+  const uint32_t tci = ld<uint32_t>(p + 32);
+  if ((c.k == 0 && len == 0) || (tci != 0 && t->o.add_vlan_header)) return ok = false;
+  const uint64_t d = pos + mac;
+  if (d > t->bytes || t->bytes - d < snap) return ok = false;
+  gpk_tpacket::Pre& P = *c.P;
+  P.pos[c.k] = pos;
+  P.off[c.k] = d;
+  P.cap[c.k] = snap;
+  gpk_tp_info& ci = P.ci[c.k];
+  go_unix(ld<uint32_t>(p + 4), ld<uint32_t>(p + 8), &ci.ts_sec, &ci.ts_nsec);
+  ci.length = len;
+  ci.iface = ld<int32_t>(p + tp_align(kV3Hdr) + 4);
+  ci.vlan = (st & kStatusVlanValid) ? (int32_t)(tci & 0xfff) : -1;
+  const uint32_t nx = ld<uint32_t>(p);
+  c.pos = pos + (nx ? nx : tp_align((uint64_t)snap + mac));
+  ok = true;
+  return ++c.k < c.n;
+}
+
+void prewalk_group(gpk_tpacket* t, const uint64_t* hs, int G, uint64_t epoch) {
+  Chain c[8];
+  int live = 0;
+  for (int g = 0; g < G; g++) {
+    c[g].P = &t->pre[hs[g]];
+    c[g].P->epoch = 0;
+    if (chain_start(t, hs[g], c[g])) live++;
+  }
+  while (live) {
+    for (int g = 0; g < G; g++) {
+      if (!c[g].live) continue;
+      bool ok = true;
+      if (!chain_step(t, c[g], ok)) {
+        c[g].live = false;
+        live--;
+        if (ok) c[g].P->epoch = epoch;
+      }
+    }
+  }
+}
+
+// Pre-walk, on up to t->threads threads, the handed-over blocks the walk will
+// reach next, until they hold about `want` packets.
+void prewalk(gpk_tpacket* t, uint64_t want) {
+  t->epoch++;  // every earlier pre-walk is stale from here on
+  const GoState& s = t->s;
+  uint64_t h = (s.have_current && !s.polling) ? (s.cur_hdr + 1) % t->nhdr
+                                               : (uint64_t)(s.offset >= (int64_t)t->nhdr ? 0 : s.offset);
+  std::vector<uint64_t> list;
+  uint64_t sum = 0;
+  for (uint64_t i = 0; i + 1 < t->nhdr && sum < want; i++, h = (h + 1) % t->nhdr) {
+    if (t->pending[h] || !(header_status(t, h) & kStatusUser)) break;
+    list.push_back(h);
+    sum += ld<uint32_t>(t->ring + header_pos(t, h) + 12);
+  }
+  if (list.size() < 2) return;
+  static constexpr int G = 4;  // chains in flight per thread
+  const size_t groups = (list.size() + G - 1) / G;
+  const int T = (int)std::min<size_t>(std::max(1, t->threads), groups);
+  const uint64_t epoch = t->epoch;
+  std::vector<std::thread> th;
+  for (int w = 0; w < T; w++)
+    th.emplace_back([t, w, T, groups, epoch, &list] {
+      for (size_t j = (size_t)w; j < groups; j += (size_t)T)
+        prewalk_group(t, list.data() + j * G, (int)std::min<size_t>(G, list.size() - j * G), epoch);
+    });
+  for (auto& x : th) x.join();
 }
 
 void set_err(char* err, size_t cap, const std::string& s) {
@@ -598,6 +715,13 @@ int gpk_tpacket_index(gpk_tpacket* t, int wait, uint64_t* offsets, uint32_t* cap
   Call c{t, &rel, &fr, wait != 0, side, side ? side_cap : 0, 0};
   uint64_t k = 0;
   int ret = GPK_TP_FULL;
+  // large calls over V3 blocks: the blocks ahead are walked in parallel, and
+  // the exact walk below takes a block's packets from there after reading its
+  // first packet itself (a DRAM-latency-bound pointer chase per packet otherwise)
+  const bool bulk = t->version == GPK_TPACKET_V3 && max >= 4096 && t->threads > 1;
+  if (bulk) prewalk(t, max);
+  std::vector<uint8_t> visited;  // a block's pre-walk serves its first visit only
+  if (bulk) visited.assign(t->nhdr, 0);
   while (k < max) {
     const GoState snap = t->s;
     rel.clear();
@@ -626,6 +750,22 @@ int gpk_tpacket_index(gpk_tpacket* t, int wait, uint64_t* offsets, uint32_t* cap
     caplens[k] = c.caplen;
     if (ci) ci[k] = c.ci;
     k++;
+    if (bulk && t->s.used == 0 && !visited[t->s.cur_hdr]) {
+      const uint64_t h = t->s.cur_hdr;
+      visited[h] = 1;
+      gpk_tpacket::Pre& P = t->pre[h];
+      if (P.epoch == t->epoch && P.off[0] == c.off && P.pos[0] == t->s.pkt) {
+        // packets 1.. of the block: what the next() calls would return
+        const uint64_t m = std::min<uint64_t>(P.off.size() - 1, max - k);
+        memcpy(offsets + k, P.off.data() + 1, m * 8);
+        memcpy(caplens + k, P.cap.data() + 1, m * 4);
+        if (ci) memcpy(ci + k, P.ci.data() + 1, m * sizeof(gpk_tp_info));
+        k += m;
+        t->s.used = (uint32_t)m;
+        t->s.pkt = P.pos[m];
+        t->s.packets += (int64_t)m;
+      }
+    }
   }
   *n = k;
   if (side_used) *side_used = c.side_used;

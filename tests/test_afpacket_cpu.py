@@ -335,3 +335,56 @@ def test_live_loopback_capture(version):
     tp.SetBPF([(0x06, 0, 0, 0)])  # "ret #0": drop everything
     tp.SetBPF([])
     tp.Close()
+
+
+@pytest.mark.parametrize("vlan", [False, True])
+def test_parallel_prewalk_equals_sequential_walk(vlan):
+    """Calls of >= 4096 packets take V3 blocks from the parallel pre-walk; the
+    result must be the oracle's, with blocks the pre-walk must refuse mixed in
+    (empty first packets, VLAN tags to insert, blocks not handed over, chains
+    leaving the block) and headers re-armed between calls."""
+    S = _lib.synth_lib()
+    from gopacket_amd import synth
+    bs, nb = 65536, 24
+    for seed in range(3):
+        rng = np.random.default_rng(40 + seed)
+        ring = np.zeros(bs * nb, np.uint8)
+        S.gpk_synth_tpacket_v3(ring.ctypes.data, bs, nb, synth.C4_IMIX, seed * 1000, 3, 7, None)
+        raw = bytearray(ring.tobytes())
+        for b in rng.choice(nb, 6, replace=False):
+            base = int(b) * bs
+            k = int(rng.integers(0, 4))
+            if k == 0:
+                struct.pack_into("<I", raw, base + 8, 0)  # not handed over
+            elif k == 1:
+                struct.pack_into("<I", raw, base + 48 + 16, 0)  # first packet tp_len 0
+            elif k == 2:
+                struct.pack_into("<I", raw, base + 12, struct.unpack_from("<I", raw, base + 12)[0] + 1)  # chain runs on
+            else:
+                struct.pack_into("<I", raw, base + 48 + 32, 0x77)  # a VLAN TCI on the first packet
+        opts = dict(frame_size=4096, block_size=bs, num_blocks=nb, add_vlan_header=vlan)
+        ring_n, ring_o = bytearray(raw), bytearray(raw)
+        h, arr = native_reader(ring_n, AO.V3, opts)
+        orc = AO.TPacketOracle(ring_o, AO.V3, dict(opts))
+        side = np.zeros(1 << 20, np.uint8)
+        try:
+            for _ in range(5):
+                m = int(rng.integers(4096, 12000))
+                got, side_pk, st = native_index(h, len(ring_n), m, side)
+                exp, kind, err = orc.read_until_stop(m)
+                assert len(got) == len(exp)
+                for g, e, spk in zip(got, exp, side_pk):
+                    if e[0] >= len(ring_o):
+                        assert spk == orc.data(e[0], e[1]) and g[1:] == e[1:]
+                    else:
+                        assert g == e
+                if kind == AO.ERROR:
+                    assert native_error(h)[0] == err
+                    break
+                for _k in range(int(rng.integers(1, 6))):
+                    hh = int(rng.integers(0, nb))
+                    rearm(ring_n, AO.V3, opts, hh)
+                    rearm(ring_o, AO.V3, opts, hh)
+            assert bytes(ring_n) == bytes(ring_o)
+        finally:
+            _lib.lib().gpk_tpacket_close(h)
