@@ -61,7 +61,7 @@ EXPORTS = (
     "gpk_capreader_index_all", "gpk_capindex_free",
     # include/gpk_afpacket.h
     "gpk_tp_default_opts", "gpk_tp_check_opts", "gpk_tpacket_new", "gpk_tpacket_attach", "gpk_tpacket_close",
-    "gpk_tpacket_ring", "gpk_tpacket_index", "gpk_tpacket_defer", "gpk_tpacket_release_seq", "gpk_tpacket_release",
+    "gpk_tpacket_ring", "gpk_tpacket_index", "gpk_tpacket_defer", "gpk_tpacket_set_threads", "gpk_tpacket_release_seq", "gpk_tpacket_release",
     "gpk_tpacket_take_new_headers", "gpk_tpacket_geometry", "gpk_tpacket_error", "gpk_tpacket_stats",
     "gpk_tpacket_socket_stats", "gpk_tpacket_set_bpf", "gpk_tpacket_set_fanout", "gpk_tpacket_pump",
 )
@@ -223,6 +223,7 @@ def lib():
         "gpk_tpacket_ring": ([vp, P(vp), P(u64), P(c_int), P(c_int)], c_int),
         "gpk_tpacket_index": ([vp, c_int, vp, vp, vp, u64, P(u64), vp, u64, P(u64)], c_int),
         "gpk_tpacket_defer": ([vp, c_int], c_int),
+        "gpk_tpacket_set_threads": ([vp, c_int], c_int),
         "gpk_tpacket_release_seq": ([vp, P(u64)], c_int),
         "gpk_tpacket_release": ([vp, u64], c_int),
         "gpk_tpacket_take_new_headers": ([vp, P(u64), P(u64)], c_int),

@@ -33,6 +33,9 @@
 
 #include <algorithm>
 #include <chrono>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
 #include <cstdio>
 #include <cstring>
 #include <deque>
@@ -82,6 +85,62 @@ double now_s() {
 // Header sizes (header.go:125-127) and the sockaddr_ll that follows each.
 constexpr uint64_t kV1Hdr = 0x20, kV2Hdr = 0x20, kV3Hdr = 0x30;
 
+// A fixed set of worker threads that run one function per call: the
+// pre-walk runs on every large index call, so spawning threads there would
+// cost as much as the walk of a few blocks.
+class Pool {
+ public:
+  ~Pool() {
+    {
+      std::lock_guard<std::mutex> l(m_);
+      stop_ = true;
+      gen_++;
+    }
+    cv_.notify_all();
+    for (auto& x : th_) x.join();
+  }
+  // fn(w, T) on workers w = 0..T-1; returns when all are done
+  void run(int T, const std::function<void(int, int)>& fn) {
+    while ((int)th_.size() < T) {
+      const int w = (int)th_.size();
+      th_.emplace_back([this, w] { loop(w); });
+    }
+    std::unique_lock<std::mutex> l(m_);
+    fn_ = &fn;
+    T_ = T;
+    left_ = T;
+    gen_++;
+    cv_.notify_all();
+    done_.wait(l, [this] { return left_ == 0; });
+    fn_ = nullptr;
+  }
+
+ private:
+  void loop(int w) {
+    uint64_t seen = 0;
+    for (;;) {
+      std::unique_lock<std::mutex> l(m_);
+      cv_.wait(l, [&] { return gen_ != seen; });
+      seen = gen_;
+      if (stop_) return;
+      if (w >= T_) continue;
+      const std::function<void(int, int)>* f = fn_;
+      const int T = T_;
+      l.unlock();
+      (*f)(w, T);
+      l.lock();
+      if (--left_ == 0) done_.notify_one();
+    }
+  }
+  std::vector<std::thread> th_;
+  std::mutex m_;
+  std::condition_variable cv_, done_;
+  const std::function<void(int, int)>* fn_ = nullptr;
+  int T_ = 0, left_ = 0;
+  uint64_t gen_ = 0;
+  bool stop_ = false;
+};
+
 // Go-side reader state that one ZeroCopyReadPacketData call mutates.
 struct GoState {
   int64_t offset = 0;             // TPacket.offset
@@ -122,6 +181,10 @@ struct gpk_tpacket {
   // V3 blocks walked ahead in parallel (prewalk), valid for one index call
   struct Pre {
     uint64_t epoch = 0;
+    bool direct = false;  // written to the caller's arrays at pred
+    uint64_t pred = 0;
+    uint32_t n = 0;
+    uint64_t first_off = 0, first_pos = 0, last_pos = 0;
     std::vector<uint64_t> off, pos;
     std::vector<uint32_t> cap;
     std::vector<gpk_tp_info> ci;
@@ -129,6 +192,7 @@ struct gpk_tpacket {
   std::vector<Pre> pre;
   uint64_t epoch = 0;
   int threads = 16;
+  Pool pool;
 };
 
 namespace {
@@ -425,19 +489,29 @@ struct Chain {
   uint64_t pos;
   uint32_t k, n;
   bool live;
+  uint64_t* off;  // where the block's packets go: the caller's arrays at the
+  uint32_t* cap;  // predicted position (direct), or the block's own arrays
+  gpk_tp_info* ci;
+  uint64_t* posv;  // header positions (own arrays only)
 };
 
 bool chain_start(gpk_tpacket* t, uint64_t h, Chain& c) {
-  c.P = &t->pre[h];
   c.live = false;
   if (t->pending[h] || !(header_status(t, h) & kStatusUser)) return false;
   const uint64_t base = header_pos(t, h);
   c.n = ld<uint32_t>(t->ring + base + 12);
   if (c.n == 0) return false;
-  c.P->off.resize(c.n);
-  c.P->pos.resize(c.n);
-  c.P->cap.resize(c.n);
-  c.P->ci.resize(c.n);
+  gpk_tpacket::Pre& P = *c.P;
+  if (!P.direct) {
+    P.off.resize(c.n);
+    P.pos.resize(c.n);
+    P.cap.resize(c.n);
+    P.ci.resize(c.n);
+    c.off = P.off.data();
+    c.cap = P.cap.data();
+    c.ci = P.ci.data();
+    c.posv = P.pos.data();
+  }
   c.pos = base + ld<uint32_t>(t->ring + base + 16);
   c.k = 0;
   c.live = true;
@@ -455,28 +529,32 @@ inline bool chain_step(const gpk_tpacket* t, Chain& c, bool& ok) {
   if ((c.k == 0 && len == 0) || (tci != 0 && t->o.add_vlan_header)) return ok = false;
   const uint64_t d = pos + mac;
   if (d > t->bytes || t->bytes - d < snap) return ok = false;
-  gpk_tpacket::Pre& P = *c.P;
-  P.pos[c.k] = pos;
-  P.off[c.k] = d;
-  P.cap[c.k] = snap;
-  gpk_tp_info& ci = P.ci[c.k];
-  go_unix(ld<uint32_t>(p + 4), ld<uint32_t>(p + 8), &ci.ts_sec, &ci.ts_nsec);
-  ci.length = len;
-  ci.iface = ld<int32_t>(p + tp_align(kV3Hdr) + 4);
-  ci.vlan = (st & kStatusVlanValid) ? (int32_t)(tci & 0xfff) : -1;
+  c.off[c.k] = d;
+  c.cap[c.k] = snap;
+  if (c.ci) {
+    gpk_tp_info& ci = c.ci[c.k];
+    go_unix(ld<uint32_t>(p + 4), ld<uint32_t>(p + 8), &ci.ts_sec, &ci.ts_nsec);
+    ci.length = len;
+    ci.iface = ld<int32_t>(p + tp_align(kV3Hdr) + 4);
+    ci.vlan = (st & kStatusVlanValid) ? (int32_t)(tci & 0xfff) : -1;
+  }
+  if (c.posv) c.posv[c.k] = pos;
+  if (c.k == 0) {
+    c.P->first_off = d;
+    c.P->first_pos = pos;
+  }
+  c.P->last_pos = pos;
   const uint32_t nx = ld<uint32_t>(p);
   c.pos = pos + (nx ? nx : tp_align((uint64_t)snap + mac));
   ok = true;
   return ++c.k < c.n;
 }
 
-void prewalk_group(gpk_tpacket* t, const uint64_t* hs, int G, uint64_t epoch) {
-  Chain c[8];
+void prewalk_group(gpk_tpacket* t, Chain* c, int G, uint64_t epoch) {
   int live = 0;
   for (int g = 0; g < G; g++) {
-    c[g].P = &t->pre[hs[g]];
     c[g].P->epoch = 0;
-    if (chain_start(t, hs[g], c[g])) live++;
+    if (chain_start(t, c[g].P - t->pre.data(), c[g])) live++;
   }
   while (live) {
     for (int g = 0; g < G; g++) {
@@ -485,38 +563,57 @@ void prewalk_group(gpk_tpacket* t, const uint64_t* hs, int G, uint64_t epoch) {
       if (!chain_step(t, c[g], ok)) {
         c[g].live = false;
         live--;
-        if (ok) c[g].P->epoch = epoch;
+        if (ok) {
+          c[g].P->epoch = epoch;
+          c[g].P->n = c[g].n;
+        }
       }
     }
   }
 }
 
 // Pre-walk, on up to t->threads threads, the handed-over blocks the walk will
-// reach next, until they hold about `want` packets.
-void prewalk(gpk_tpacket* t, uint64_t want) {
+// reach next, until they hold `max` packets. A block is written straight to
+// the caller's arrays at the position it will have if every block before it
+// contributes all of its packets (the exact walk checks that); the block that
+// crosses `max` goes to its own arrays, to be taken in part.
+void prewalk(gpk_tpacket* t, uint64_t max, uint64_t* offsets, uint32_t* caplens, gpk_tp_info* ci) {
   t->epoch++;  // every earlier pre-walk is stale from here on
   const GoState& s = t->s;
+  uint64_t pos = 0;  // the current block's remaining packets come first
+  if (s.have_current && !s.polling && s.header_next_needed) {
+    const uint32_t n = ld<uint32_t>(t->ring + header_pos(t, s.cur_hdr) + 12);
+    pos = n > s.used + 1 ? n - s.used - 1 : 0;
+  }
   uint64_t h = (s.have_current && !s.polling) ? (s.cur_hdr + 1) % t->nhdr
                                                : (uint64_t)(s.offset >= (int64_t)t->nhdr ? 0 : s.offset);
-  std::vector<uint64_t> list;
-  uint64_t sum = 0;
-  for (uint64_t i = 0; i + 1 < t->nhdr && sum < want; i++, h = (h + 1) % t->nhdr) {
+  std::vector<Chain> list;
+  for (uint64_t i = 0; i + 1 < t->nhdr && pos < max; i++, h = (h + 1) % t->nhdr) {
     if (t->pending[h] || !(header_status(t, h) & kStatusUser)) break;
-    list.push_back(h);
-    sum += ld<uint32_t>(t->ring + header_pos(t, h) + 12);
+    const uint32_t n = ld<uint32_t>(t->ring + header_pos(t, h) + 12);
+    gpk_tpacket::Pre& P = t->pre[h];
+    Chain c{};
+    c.P = &P;
+    P.direct = pos + n <= max;
+    P.pred = pos;
+    if (P.direct) {
+      c.off = offsets + pos;
+      c.cap = caplens + pos;
+      c.ci = ci ? ci + pos : nullptr;
+      c.posv = nullptr;
+    }
+    list.push_back(c);
+    pos += n;
   }
   if (list.size() < 2) return;
   static constexpr int G = 4;  // chains in flight per thread
   const size_t groups = (list.size() + G - 1) / G;
   const int T = (int)std::min<size_t>(std::max(1, t->threads), groups);
   const uint64_t epoch = t->epoch;
-  std::vector<std::thread> th;
-  for (int w = 0; w < T; w++)
-    th.emplace_back([t, w, T, groups, epoch, &list] {
-      for (size_t j = (size_t)w; j < groups; j += (size_t)T)
-        prewalk_group(t, list.data() + j * G, (int)std::min<size_t>(G, list.size() - j * G), epoch);
-    });
-  for (auto& x : th) x.join();
+  t->pool.run(T, [t, groups, epoch, &list](int w, int T) {
+    for (size_t j = (size_t)w; j < groups; j += (size_t)T)
+      prewalk_group(t, list.data() + j * G, (int)std::min<size_t>(G, list.size() - j * G), epoch);
+  });
 }
 
 void set_err(char* err, size_t cap, const std::string& s) {
@@ -719,7 +816,7 @@ int gpk_tpacket_index(gpk_tpacket* t, int wait, uint64_t* offsets, uint32_t* cap
   // the exact walk below takes a block's packets from there after reading its
   // first packet itself (a DRAM-latency-bound pointer chase per packet otherwise)
   const bool bulk = t->version == GPK_TPACKET_V3 && max >= 4096 && t->threads > 1;
-  if (bulk) prewalk(t, max);
+  if (bulk) prewalk(t, max, offsets, caplens, ci);
   std::vector<uint8_t> visited;  // a block's pre-walk serves its first visit only
   if (bulk) visited.assign(t->nhdr, 0);
   while (k < max) {
@@ -754,15 +851,23 @@ int gpk_tpacket_index(gpk_tpacket* t, int wait, uint64_t* offsets, uint32_t* cap
       const uint64_t h = t->s.cur_hdr;
       visited[h] = 1;
       gpk_tpacket::Pre& P = t->pre[h];
-      if (P.epoch == t->epoch && P.off[0] == c.off && P.pos[0] == t->s.pkt) {
+      if (P.epoch == t->epoch && P.first_off == c.off && P.first_pos == t->s.pkt) {
         // packets 1.. of the block: what the next() calls would return
-        const uint64_t m = std::min<uint64_t>(P.off.size() - 1, max - k);
-        memcpy(offsets + k, P.off.data() + 1, m * 8);
-        memcpy(caplens + k, P.cap.data() + 1, m * 4);
-        if (ci) memcpy(ci + k, P.ci.data() + 1, m * sizeof(gpk_tp_info));
+        uint64_t m = 0;
+        if (P.direct) {
+          if (P.pred == k - 1) {  // already in place
+            m = P.n - 1;
+            t->s.pkt = P.last_pos;
+          }
+        } else {
+          m = std::min<uint64_t>(P.n - 1, max - k);
+          memcpy(offsets + k, P.off.data() + 1, m * 8);
+          memcpy(caplens + k, P.cap.data() + 1, m * 4);
+          if (ci) memcpy(ci + k, P.ci.data() + 1, m * sizeof(gpk_tp_info));
+          t->s.pkt = P.pos[m];
+        }
         k += m;
         t->s.used = (uint32_t)m;
-        t->s.pkt = P.pos[m];
         t->s.packets += (int64_t)m;
       }
     }
@@ -770,6 +875,12 @@ int gpk_tpacket_index(gpk_tpacket* t, int wait, uint64_t* offsets, uint32_t* cap
   *n = k;
   if (side_used) *side_used = c.side_used;
   return ret;
+}
+
+int gpk_tpacket_set_threads(gpk_tpacket* t, int threads) {
+  if (!t || threads < 1 || threads > 256) return GPK_EINVAL;
+  t->threads = threads;
+  return GPK_OK;
 }
 
 int gpk_tpacket_defer(gpk_tpacket* t, int on) {

@@ -110,6 +110,9 @@ typedef struct gpk_tp_info {
 int gpk_tpacket_index(gpk_tpacket* t, int wait, uint64_t* offsets, uint32_t* caplens, gpk_tp_info* ci, uint64_t max,
                       uint64_t* n, uint8_t* side, uint64_t side_cap, uint64_t* side_used);
 int gpk_tpacket_defer(gpk_tpacket* t, int on);
+/* Host threads for the parallel pre-walk of V3 blocks in large index calls
+ * (default 16; 1 = the plain sequential walk). Results do not depend on it. */
+int gpk_tpacket_set_threads(gpk_tpacket* t, int threads);
 /* Header releases are numbered in walk order; *seq = the count so far. */
 int gpk_tpacket_release_seq(const gpk_tpacket* t, uint64_t* seq);
 /* Hand back every deferred header with release number < seq. */
