@@ -606,11 +606,12 @@ void prewalk(gpk_tpacket* t, uint64_t max, uint64_t* offsets, uint32_t* caplens,
     pos += n;
   }
   if (list.size() < 2) return;
-  static constexpr int G = 4;  // chains in flight per thread
+  // chains in flight per thread: up to 4, fewer when there are few blocks per thread
+  const int G = (int)std::max<size_t>(1, std::min<size_t>(4, list.size() / std::max(1, t->threads)));
   const size_t groups = (list.size() + G - 1) / G;
   const int T = (int)std::min<size_t>(std::max(1, t->threads), groups);
   const uint64_t epoch = t->epoch;
-  t->pool.run(T, [t, groups, epoch, &list](int w, int T) {
+  t->pool.run(T, [t, G, groups, epoch, &list](int w, int T) {
     for (size_t j = (size_t)w; j < groups; j += (size_t)T)
       prewalk_group(t, list.data() + j * G, (int)std::min<size_t>(G, list.size() - j * G), epoch);
   });
@@ -816,7 +817,25 @@ int gpk_tpacket_index(gpk_tpacket* t, int wait, uint64_t* offsets, uint32_t* cap
   // the exact walk below takes a block's packets from there after reading its
   // first packet itself (a DRAM-latency-bound pointer chase per packet otherwise)
   const bool bulk = t->version == GPK_TPACKET_V3 && max >= 4096 && t->threads > 1;
+  // the block the last call stopped in, if that call pre-walked it: its
+  // remaining packets come from there too
+  const GoState& s0 = t->s;
+  gpk_tpacket::Pre* carry = nullptr;
+  if (bulk && s0.have_current && !s0.polling && s0.header_next_needed) {
+    gpk_tpacket::Pre& P = t->pre[s0.cur_hdr];
+    if (P.epoch == t->epoch && !P.direct && s0.used < P.pos.size() && P.pos[s0.used] == s0.pkt) carry = &P;
+  }
   if (bulk) prewalk(t, max, offsets, caplens, ci);
+  if (carry) {
+    const uint64_t m = std::min<uint64_t>(carry->n - 1 - t->s.used, max);
+    memcpy(offsets, carry->off.data() + t->s.used + 1, m * 8);
+    memcpy(caplens, carry->cap.data() + t->s.used + 1, m * 4);
+    if (ci) memcpy(ci, carry->ci.data() + t->s.used + 1, m * sizeof(gpk_tp_info));
+    t->s.used += (uint32_t)m;
+    t->s.pkt = carry->pos[t->s.used];
+    t->s.packets += (int64_t)m;
+    k = m;
+  }
   std::vector<uint8_t> visited;  // a block's pre-walk serves its first visit only
   if (bulk) visited.assign(t->nhdr, 0);
   while (k < max) {

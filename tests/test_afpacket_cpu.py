@@ -345,7 +345,7 @@ def test_parallel_prewalk_equals_sequential_walk(vlan):
     leaving the block) and headers re-armed between calls."""
     S = _lib.synth_lib()
     from gopacket_amd import synth
-    bs, nb = 65536, 24
+    bs, nb = 65536, 64
     for seed in range(3):
         rng = np.random.default_rng(40 + seed)
         ring = np.zeros(bs * nb, np.uint8)
