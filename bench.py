@@ -343,6 +343,69 @@ def afpacket_pump(ctx, packets=16 * 2**20, block_mib=4, blocks=64, reps=2, batch
                 parity="%s (%d sampled packets vs oracle)" % ("bit-exact" if ok else "MISMATCH", len(idx)))
 
 
+def flow_grouping(ctx, n=64 * 2**20, reps=5):
+    """Row (f)3: C6 traffic (C4's frames, endpoints from a heavy-tailed pool of
+    2^20 flows in both directions, 5 % IPv4 fragments) generated in HBM,
+    decoded with layouts, then grouped on the device by each consumer's key
+    (gpk_group_batch). Timed with HIP events on the stream. Sampled groups are
+    checked against the oracle's key of their packets."""
+    import torch
+    from gopacket_amd import _lib, engine, flows, synth
+    from oracle import flows_oracle as FO
+    from oracle import oracle as O
+    dec = ["ETHERNET", "DOT1Q", "IPV4", "IPV6", "IPV6_EXT", "TCP", "UDP", "PAYLOAD"]
+    parser = engine.ParserConfig(17, [engine.DECODER_KINDS[d] for d in CONFIGS["c4"]["decoders"]], outputs=7)
+    stream = torch.cuda.current_stream()
+    d, o, c = synth.device_batch(6, 0, n)
+    rec = torch.zeros(n * 16, dtype=torch.uint8, device="cuda")
+    err = torch.zeros(2 * n, dtype=torch.int32, device="cuda")
+    fl = torch.zeros(3 * n, dtype=torch.int64, device="cuda")
+    lay = torch.zeros(n * 64, dtype=torch.uint8, device="cuda")
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ctx.decode_device(parser, d, o, c, rec, err, fl, lay, stream=stream)
+    e0.record(stream)
+    for _ in range(reps):
+        ctx.decode_device(parser, d, o, c, rec, err, fl, lay, stream=stream)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    dec_ms = e0.elapsed_time(e1) / reps
+    g = flows.Grouper(n)
+    out = {}
+    for name, kind, buckets in (("connection", FO.CONNECTION, 8), ("defrag", FO.DEFRAG, 8),
+                                ("net_bucket8", FO.NET_BUCKET, 8)):
+        res = g.group(d, o, c, rec, lay, fl, kind=kind, buckets=buckets)  # warm
+        e0.record(stream)
+        for _ in range(reps):
+            res = g.group(d, o, c, rec, lay, fl, kind=kind, buckets=buckets)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / reps
+        G, K = res["counts"].cpu().tolist()
+        ok = True
+        if kind != FO.NET_BUCKET:  # sampled groups: one oracle key per group, distinct across groups
+            perm = res["perm"][:K].cpu().numpy()
+            start = res["start"][:G + 1].cpu().numpy()
+            rng = np.random.default_rng(4)
+            keys = []
+            for gg in rng.choice(G, min(G, 64), replace=False):
+                idx = perm[start[gg]:start[gg + 1]][:32]
+                pk = [synth.packet(6, int(i)) for i in idx]
+                cap = np.array([len(x) for x in pk], np.uint32)
+                off = np.concatenate([[0], np.cumsum(cap[:-1], dtype=np.uint64)]).astype(np.uint64)
+                r = O.OracleParser(17, dec).decode(np.frombuffer(b"".join(pk) + bytes(16), np.uint8), off, cap)
+                ks = {FO.packet_key(kind, p, r["records"][k], r["layouts"][k], 0, 8) for k, p in enumerate(pk)}
+                ok = ok and len(ks) == 1 and not isinstance(next(iter(ks)), int)
+                keys.append(next(iter(ks)))
+            ok = ok and len(set(keys)) == len(keys)
+        out[name] = dict(ms=round(ms, 4), Mpkts_s=round(n / ms / 1e3, 1), groups=G, keyed_packets=K,
+                         parity="%s (sampled groups vs oracle keys)" % ("ok" if ok else "MISMATCH")
+                         if kind != FO.NET_BUCKET else "see tests/test_flows_gpu.py")
+    g.close()
+    return dict(workload="(f)3: C6 64M packets (IMIX, 2^20 heavy-tailed flows, both directions, 5%% IPv4 "
+                         "fragments), decode with layouts, then group by consumer key in HBM",
+                packets=n, decode_with_layouts_ms=round(dec_ms, 4), grouping=out)
+
+
 def load_traffic(name, n):
     """HBM bytes per launch of the decode kernel from the committed PMC
     profile (profiles/hbm_traffic.json, tools/make_profiles.py): measured
@@ -371,6 +434,8 @@ def main():
                     help="also run config C5: replay a GIB-GiB pcapng end to end (gpk_replay_file)")
     ap.add_argument("--afpacket", type=int, default=0, metavar="MPKTS",
                     help="also drain MPKTS Mi packets from an emulated TPACKET_V3 ring (gpk_tpacket_pump)")
+    ap.add_argument("--flows", action="store_true",
+                    help="also time row (f)3: flow-keyed grouping of 64M C6 packets (gpk_group_batch)")
     ap.add_argument("--tables", default="auto", choices=["auto", "global"],
                     help="next-layer tables: compact LDS copy (auto) or device-memory tables (global)")
     args = ap.parse_args()
@@ -424,6 +489,8 @@ def main():
             out["pcie_inclusive"] = pcie_inclusive(head, ctx)
         if args.c5 > 0 and world == 1:
             out["c5"] = c5_replay(ctx, gib=args.c5)
+        if args.flows and world == 1:
+            out["flows"] = flow_grouping(ctx)
         if args.afpacket > 0 and world == 1:
             out["afpacket"] = afpacket_pump(ctx, packets=args.afpacket * 2**20)
         if world == 1 and not args.no_cpu_baseline:

@@ -64,7 +64,19 @@ EXPORTS = (
     "gpk_tpacket_ring", "gpk_tpacket_index", "gpk_tpacket_defer", "gpk_tpacket_set_threads", "gpk_tpacket_release_seq", "gpk_tpacket_release",
     "gpk_tpacket_take_new_headers", "gpk_tpacket_geometry", "gpk_tpacket_error", "gpk_tpacket_stats",
     "gpk_tpacket_socket_stats", "gpk_tpacket_set_bpf", "gpk_tpacket_set_fanout", "gpk_tpacket_pump",
+    # include/gpk_flows.h
+    "gpk_grouper_create", "gpk_grouper_destroy", "gpk_group_batch",
 )
+
+# include/gpk_flows.h constants
+GROUP_CONNECTION, GROUP_DEFRAG, GROUP_NET_BUCKET = 1, 2, 3
+GROUP_NONE, GROUP_USELESS, GROUP_FRAG_TOO_SMALL, GROUP_FRAG_OFFSET, GROUP_FRAG_OVERRUN, GROUP_UNKNOWN = \
+    -1, -2, -3, -4, -5, -6
+
+
+class Groups(ctypes.Structure):
+    _fields_ = [("group_of", ctypes.c_void_p), ("perm", ctypes.c_void_p), ("start", ctypes.c_void_p),
+                ("first", ctypes.c_void_p), ("counts", ctypes.c_void_p)]
 
 # include/gpk_afpacket.h constants
 TPACKET_V1, TPACKET_V2, TPACKET_V3, TPACKET_HIGHEST = 0, 1, 2, -1
@@ -234,6 +246,9 @@ def lib():
         "gpk_tpacket_set_bpf": ([vp, vp, u32], c_int),
         "gpk_tpacket_set_fanout": ([vp, c_int, ctypes.c_uint16], c_int),
         "gpk_tpacket_pump": ([vp, vp, vp, P(PumpOpts), PUMP_CB, vp, P(PumpStats)], c_int),
+        "gpk_grouper_create": ([P(vp), c_int, u64], c_int),
+        "gpk_grouper_destroy": ([vp], c_int),
+        "gpk_group_batch": ([vp, P(Batch), P(Results), c_int, u32, P(Groups), vp], c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)

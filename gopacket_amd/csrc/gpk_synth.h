@@ -17,6 +17,9 @@
 #define GPK_SYNTH_C2_UDP64 2    /* 64 B Eth/IPv4/UDP, 10% zero UDP checksum      */
 #define GPK_SYNTH_C3_TCP1500 3  /* 1500 B Eth/IPv4/TCP, 50% NOP,NOP,TS options    */
 #define GPK_SYNTH_C4_IMIX 4     /* 64/594/1518 7:4:1, Dot1Q/QinQ, IPv4/IPv6(+HBH) */
+#define GPK_SYNTH_C6_FLOWS 6    /* C4's frames with endpoints from 2^20 skewed flows in both
+                                   directions, SYN/FIN/RST and empty-payload TCP, 5% IPv4
+                                   fragments (row (f)3: flow-keyed grouping)               */
 
 namespace gpk_synth {
 
@@ -74,6 +77,7 @@ struct Desc {
   uint32_t hlen;        // header bytes before the payload
   uint32_t l3;          // offset of the network header
   uint32_t l4;          // offset of the transport header
+  uint32_t end;         // end of the IP datagram (< len: Ethernet padding follows)
 };
 
 GPK_HD void put16(uint8_t* b, uint32_t v) {
@@ -105,6 +109,7 @@ GPK_HD void describe(int cfg, uint64_t i, Desc& d) {
   d.doff = 5;
   d.l4_zero = 0;
   d.corrupt = 0;
+  d.end = d.len;
   uint64_t r1 = r.next(), r2 = r.next(), r3 = r.next();
   if (cfg == GPK_SYNTH_C2_UDP64) {
     d.l4_zero = (r1 % 10) == 0;
@@ -211,6 +216,46 @@ GPK_HD void describe(int cfg, uint64_t i, Desc& d) {
     }
     d.hlen = l4 + 4 * d.doff;
   }
+  if (cfg == GPK_SYNTH_C6_FLOWS) {  // endpoints from a flow pool, TCP flags, fragments
+    const uint64_t fr = r.next();
+    const uint64_t u = fr & 0xfffff;
+    const uint64_t flow = (u * u * u) >> 40;  // heavy-tailed: a few elephant flows, many mice
+    const uint64_t fh = mix64(flow * 0x9E3779B97F4A7C15ull + 0x51ED270B1F2A3C5Dull);
+    const bool swap = (fr >> 20) & 1;
+    uint32_t pa = 1024 + (uint32_t)((fh >> 32) % 64512), pb = 1024 + (uint32_t)((fh >> 48) % 64512);
+    while (d.udp ? udp_port_taken(pa) : tcp_port_taken(pa)) pa++;
+    while (d.udp ? udp_port_taken(pb) : tcp_port_taken(pb)) pb++;
+    put16(h + l4, swap ? pb : pa);
+    put16(h + l4 + 2, swap ? pa : pb);
+    if (!d.v6) {
+      const uint32_t a = 0x0a000000u | (uint32_t)(fh & 0xffffff), b = 0x0a000000u | (uint32_t)((fh >> 24) & 0xffffff);
+      put32(h + d.l3 + 12, swap ? b : a);
+      put32(h + d.l3 + 16, swap ? a : b);
+      if (((fr >> 28) % 20) == 0) {  // a fragment: DF cleared, MF and/or an offset
+        const uint32_t k = (uint32_t)(fr >> 33);
+        const uint32_t off = (k & 1) ? 0u : 1u + ((k >> 1) % 180u);
+        const uint32_t mf = (off == 0 || ((k >> 9) & 1)) ? 0x2000u : 0u;
+        put16(h + d.l3 + 6, mf | off);
+        put16(h + d.l3 + 4, (uint32_t)((fh >> 8) + ((k >> 10) & 3)) & 0xffff);
+      }
+    } else {
+      const uint64_t g = mix64(fh);
+      uint8_t* s6 = h + d.l3 + (swap ? 24 : 8);
+      uint8_t* d6 = h + d.l3 + (swap ? 8 : 24);
+      put32(s6, 0x20010db8u); put32(s6 + 4, (uint32_t)fh); put32(s6 + 8, (uint32_t)(fh >> 32)); put32(s6 + 12, (uint32_t)g);
+      put32(d6, 0x20010db8u); put32(d6 + 4, (uint32_t)(g >> 32)); put32(d6 + 8, (uint32_t)flow); put32(d6 + 12, 0x1u);
+    }
+    if (!d.udp) {
+      const uint32_t k = (uint32_t)((fr >> 40) % 100);
+      h[l4 + 13] = k < 2 ? 0x02 : (k < 3 ? 0x11 : (k < 4 ? 0x04 : 0x18));  // SYN, FIN|ACK, RST, ACK|PSH
+      if (k >= 4 && k < 14) {  // header-only segment, the rest of the frame is padding
+        h[l4 + 13] = 0x10;  // ACK
+        d.end = l4 + 4 * d.doff;
+        if (!d.v6) put16(h + d.l3 + 2, d.end - d.l3);
+        else put16(h + d.l3 + 4, d.end - d.l3 - 40);
+      }
+    }
+  }
 }
 
 GPK_HD uint32_t byte_at(const Desc& d, uint64_t i, uint32_t p) {
@@ -233,7 +278,7 @@ GPK_HD void finish(Desc& d, uint64_t i) {
     if (d.corrupt == 1) c ^= 0x0100;
     put16(h + d.l3 + 10, c);
   }
-  uint32_t l4len = d.len - d.l4;
+  uint32_t l4len = d.end - d.l4;
   uint32_t s = proto + l4len;
   if (!d.v6) {
     for (uint32_t k = 12; k < 20; k += 2) s += (uint32_t)h[d.l3 + k] << 8 | h[d.l3 + k + 1];
@@ -242,8 +287,8 @@ GPK_HD void finish(Desc& d, uint64_t i) {
   }
   uint32_t p = d.l4;
   for (; p < d.hlen; p++) s += (uint32_t)h[p] << (((p - d.l4) & 1) ? 0 : 8);
-  for (; p < d.len && (p & 7); p++) s += payload_byte(i, p) << (((p - d.l4) & 1) ? 0 : 8);
-  for (; p + 8 <= d.len; p += 8) {
+  for (; p < d.end && (p & 7); p++) s += payload_byte(i, p) << (((p - d.l4) & 1) ? 0 : 8);
+  for (; p + 8 <= d.end; p += 8) {
     uint64_t w = payload_group(i, p >> 3);
     uint32_t e = 0, o = 0;  // bytes at even / odd packet positions
     for (int k = 0; k < 8; k += 2) {
@@ -252,7 +297,7 @@ GPK_HD void finish(Desc& d, uint64_t i) {
     }
     s += ((p - d.l4) & 1) ? (o << 8) + e : (e << 8) + o;
   }
-  for (; p < d.len; p++) s += payload_byte(i, p) << (((p - d.l4) & 1) ? 0 : 8);
+  for (; p < d.end; p++) s += payload_byte(i, p) << (((p - d.l4) & 1) ? 0 : 8);
   uint32_t c = fold16(s);
   if (d.udp && c == 0) c = 0xffff;  // RFC768 (udp.go:95-100)
   if (d.l4_zero) c = 0;

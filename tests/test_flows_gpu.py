@@ -1,0 +1,117 @@
+"""gpk_group_batch (flow-keyed grouping in HBM) against the grouping oracle
+(oracle/flows_oracle.py) run on the decode oracle's results: the same groups
+in the same order, the same packets in each, the same reason codes, on
+ip4defrag's test frames, tcpassembly's filter cases, fuzzed and golden
+packets and C6 traffic; at 8 M packets, properties the grouping must have."""
+import numpy as np
+import pytest
+
+import flowcases
+import pktutil
+from configs import CONFIGS, device_parser, oracle_parser
+from gopacket_amd import flows, synth
+from oracle import flows_oracle as FO
+
+pytestmark = pytest.mark.gpu
+
+KINDS = [(FO.CONNECTION, 8), (FO.DEFRAG, 8), (FO.NET_BUCKET, 8), (FO.NET_BUCKET, 1024)]
+
+
+def device_decode(gpu_ctx, data, off, cap, cfg):
+    import torch
+    n = off.numel()
+    rec = torch.zeros(n * 16, dtype=torch.uint8, device="cuda")
+    err = torch.zeros(2 * n, dtype=torch.int32, device="cuda")
+    fl = torch.zeros(3 * n, dtype=torch.int64, device="cuda")
+    lay = torch.zeros(n * 64, dtype=torch.uint8, device="cuda")
+    gpu_ctx.decode_device(device_parser(cfg), data, off, cap, rec, err, fl, lay, stream=torch.cuda.current_stream())
+    return rec, fl, lay
+
+
+def check(gpu_ctx, packets, cfg=flowcases.DEFRAG_PARSER, kinds=KINDS):
+    import torch
+    data, off, cap = pktutil.pack(packets)
+    d = torch.from_numpy(data).cuda()
+    o = torch.from_numpy(off.astype(np.int64)).cuda()
+    c = torch.from_numpy(cap.astype(np.int32)).cuda()
+    rec, fl, lay = device_decode(gpu_ctx, d, o, c, cfg)
+    ref = oracle_parser(cfg).decode(data, off, cap, layouts=True)
+    g = flows.Grouper(max(len(packets), 1))
+    for kind, buckets in kinds:
+        out = g.group(d, o, c, rec, lay, fl, kind=kind, buckets=buckets)
+        torch.cuda.synchronize()
+        groups, group_of = flows.Grouper.to_lists(out)
+        og, oc = FO.group(kind, packets, ref["records"], ref["layouts"], ref["flows"], buckets)
+        assert group_of == oc, (kind, [(i, a, b) for i, (a, b) in enumerate(zip(group_of, oc)) if a != b][:5])
+        assert groups == list(og.values()), kind
+        first = out["first"][:len(groups)].cpu().tolist()
+        assert first == [v[0] for v in og.values()]
+    g.close()
+
+
+def test_defrag_frames_and_security_checks(gpu_ctx):
+    frames, _ = flowcases.defrag_frames()
+    pk = list(frames.values()) + [f for _, f in flowcases.defrag_struct_cases()] + list(frames.values())
+    check(gpu_ctx, pk)
+
+
+def test_connection_cases(gpu_ctx):
+    check(gpu_ctx, flowcases.connection_cases() * 3)
+
+
+def test_fuzzed_and_golden(gpu_ctx):
+    pk = pktutil.fuzz_packets(91, 30000)
+    for name in ("test_ethernet.pcap", "test_dns.pcap"):
+        pk += pktutil.read_pcap(pktutil.GOLDEN + "/" + name)[1]
+    check(gpu_ctx, pk)
+    check(gpu_ctx, pk, cfg=CONFIGS["fragment_no_payload"])
+
+
+def test_c6_traffic(gpu_ctx):
+    data, off, cap = synth.host_batch(6, 1000, 200000)
+    check(gpu_ctx, [bytes(data[o:o + c]) for o, c in zip(off, cap)])
+
+
+def test_empty_and_single(gpu_ctx):
+    check(gpu_ctx, [flowcases.connection_cases()[0]])
+    check(gpu_ctx, [b"\x00" * 10])
+
+
+def test_large_batch_properties(gpu_ctx):
+    """8 M C6 packets generated in HBM: every group is one key (sampled against
+    the oracle's key of its packets), groups are in first-appearance order,
+    packets ascend inside a group, every keyed packet is in exactly one group."""
+    import torch
+    n = 8 << 20
+    d, o, c = synth.device_batch(6, 0, n)
+    cfg = flowcases.DEFRAG_PARSER
+    rec, fl, lay = device_decode(gpu_ctx, d, o, c, cfg)
+    g = flows.Grouper(n)
+    out = g.group(d, o, c, rec, lay, fl, kind=FO.CONNECTION)
+    torch.cuda.synchronize()
+    G, K = out["counts"].cpu().tolist()
+    perm = out["perm"][:K].cpu().numpy()
+    start = out["start"][:G + 1].cpu().numpy()
+    first = out["first"][:G].cpu().numpy()
+    gof = out["group_of"].cpu().numpy()
+    assert 0 < G < K <= n and start[0] == 0 and start[G] == K
+    assert np.all(np.diff(first) > 0)                       # first appearance order
+    assert np.array_equal(np.sort(perm), np.nonzero(gof >= 0)[0])  # a partition of the keyed packets
+    gid = np.repeat(np.arange(G), np.diff(start))
+    assert np.array_equal(gof[perm], gid)
+    inner = np.diff(perm.astype(np.int64))
+    assert np.all((inner > 0) | (np.diff(gid) > 0))         # ascending inside each group
+    assert np.array_equal(perm[start[:-1]], first)
+    # sampled groups: every packet's key (oracle, from the oracle decode) is the group's key
+    rng = np.random.default_rng(3)
+    seen = []
+    for gg in list(rng.choice(G, 40, replace=False)) + [int(np.argmax(np.diff(start)))]:
+        idx = perm[start[gg]:start[gg + 1]][:50]
+        pk = [synth.packet(6, int(i)) for i in idx]
+        data, off, cap = pktutil.pack(pk)
+        ref = oracle_parser(cfg).decode(data, off, cap, layouts=True)
+        keys = {FO.packet_key(FO.CONNECTION, p, ref["records"][k], ref["layouts"][k], 0, 8) for k, p in enumerate(pk)}
+        assert len(keys) == 1 and not isinstance(next(iter(keys)), int)
+        seen.append(next(iter(keys)))
+    assert len(set(seen)) == len(seen)  # distinct groups, distinct keys
+    g.close()
