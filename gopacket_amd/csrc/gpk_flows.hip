@@ -142,8 +142,20 @@ __global__ void __launch_bounds__(256) key_kernel(KeyArgs a) {
   a.code[i] = c;
   if (c) return;
   if (a.kind == GPK_GROUP_NET_BUCKET) {
-    atomicMin(&a.bucket_min[w[0]], (uint32_t)i);
-    a.hash[i] = w[0];
+    // a few buckets shared by every packet: the lowest lane of the wave per
+    // bucket, and only while the bucket's minimum can still drop
+    const uint32_t b = w[0];
+    uint64_t todo = __ballot(1);
+    while (todo) {
+      const uint32_t lead = (uint32_t)__builtin_ctzll(todo);
+      const uint32_t lb = (uint32_t)__shfl((int)b, (int)lead);
+      const uint64_t same = __ballot(b == lb);
+      todo &= ~same;
+      if (b == lb && (uint32_t)__lane_id() == lead &&
+          __hip_atomic_load(&a.bucket_min[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) > (uint32_t)i)
+        atomicMin(&a.bucket_min[b], (uint32_t)i);
+    }
+    a.hash[i] = b;
     return;
   }
   uint64_t h = 0x9E3779B97F4A7C15ull;
@@ -182,7 +194,9 @@ __global__ void __launch_bounds__(256) insert_kernel(const uint32_t* keys, const
     if ((cur >> kIdxBits) == tag && same_key(keys, i, cur & kIdxMask)) break;
     pos = (pos + 1) & tmask;
   }
-  atomicMin(&slot_min[pos], (uint32_t)i);
+  // elephant flows hit one slot many times: skip the atomic once it cannot lower the minimum
+  if (__hip_atomic_load(&slot_min[pos], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) > (uint32_t)i)
+    atomicMin(&slot_min[pos], (uint32_t)i);
   slot_of[i] = (uint32_t)pos;
 }
 
