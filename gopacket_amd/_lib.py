@@ -21,6 +21,7 @@ SYNTH_PATH = os.path.join(_HERE, "libgpk_synth.so")
 
 # include/gpk.h constants
 GPK_OK = 0
+GPK_EINVAL, GPK_ENOMEM, GPK_EHIP, GPK_ENODEV, GPK_EUNSUPP = -1, -2, -3, -4, -5
 OUT_IP4_CSUM, OUT_L4_CSUM, OUT_FLOWS, OUT_ALL = 1, 2, 4, 7
 TABLES_AUTO, TABLES_GLOBAL = 0, 1
 DEC_NONE, DEC_ETHERNET, DEC_DOT1Q, DEC_IPV4, DEC_IPV6, DEC_IPV6_EXT, DEC_TCP, DEC_UDP, DEC_PAYLOAD, \
@@ -66,7 +67,12 @@ EXPORTS = (
     "gpk_tpacket_socket_stats", "gpk_tpacket_set_bpf", "gpk_tpacket_set_fanout", "gpk_tpacket_pump",
     # include/gpk_flows.h
     "gpk_grouper_create", "gpk_grouper_destroy", "gpk_group_batch",
+    # include/gpk_bpf.h
+    "gpk_bpf_create", "gpk_bpf_destroy", "gpk_bpf_run", "gpk_bpf_select",
 )
+
+BPF_INSN_DTYPE = np.dtype([("code", "<u2"), ("jt", "u1"), ("jf", "u1"), ("k", "<u4")])
+BPF_MAX_INSNS = 4096
 
 # include/gpk_flows.h constants
 GROUP_CONNECTION, GROUP_DEFRAG, GROUP_NET_BUCKET = 1, 2, 3
@@ -249,6 +255,10 @@ def lib():
         "gpk_grouper_create": ([P(vp), c_int, u64], c_int),
         "gpk_grouper_destroy": ([vp], c_int),
         "gpk_group_batch": ([vp, P(Batch), P(Results), c_int, u32, P(Groups), vp], c_int),
+        "gpk_bpf_create": ([P(vp), vp, u32, ctypes.c_char_p, ctypes.c_size_t], c_int),
+        "gpk_bpf_destroy": ([vp], c_int),
+        "gpk_bpf_run": ([vp, P(Batch), vp, vp, vp], c_int),
+        "gpk_bpf_select": ([vp, P(Batch), vp, vp, vp, vp, vp, vp], c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)

@@ -121,3 +121,39 @@ def fnv_hash(s):
 def flow_fast_hash(typ, src, dst):
     src, dst = bytes(src), bytes(dst)
     return lib().oracle_flow_fast_hash(typ, src, len(src), dst, len(dst))
+
+
+BPF_INSN_DTYPE = np.dtype([("code", "<u2"), ("jt", "u1"), ("jf", "u1"), ("k", "<u4")])
+
+
+def bpf_program(insns):
+    arr = np.zeros(len(insns), BPF_INSN_DTYPE)
+    for i, x in enumerate(insns):
+        arr[i] = (int(x[0]) & 0xFFFF, int(x[1]) & 0xFF, int(x[2]) & 0xFF, int(x[3]) & 0xFFFFFFFF)
+    return arr
+
+
+def bpf_filter(insns, pkt, wirelen=None):
+    """libpcap bpf_filter restated (oracle/bpf_oracle.c): the filter's return value."""
+    L = lib()
+    prog = bpf_program(insns)
+    pkt = bytes(pkt)
+    L.oracle_bpf_filter.restype = ctypes.c_uint32
+    L.oracle_bpf_filter.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_char_p, ctypes.c_uint32,
+                                    ctypes.c_uint32]
+    return L.oracle_bpf_filter(prog.ctypes.data, len(prog), pkt, len(pkt) if wirelen is None else wirelen, len(pkt))
+
+
+def bpf_batch(insns, data, offsets, caplens, wirelens=None):
+    L = lib()
+    prog = bpf_program(insns)
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+    caplens = np.ascontiguousarray(caplens, dtype=np.uint32)
+    w = None if wirelens is None else np.ascontiguousarray(wirelens, dtype=np.uint32)
+    ret = np.zeros(len(offsets), np.uint32)
+    L.oracle_bpf_batch.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p,
+                                   ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]
+    L.oracle_bpf_batch(prog.ctypes.data, len(prog), data.ctypes.data, offsets.ctypes.data, caplens.ctypes.data,
+                       w.ctypes.data if w is not None else None, len(offsets), ret.ctypes.data)
+    return ret
