@@ -406,6 +406,54 @@ def flow_grouping(ctx, n=64 * 2**20, reps=5):
                 packets=n, decode_with_layouts_ms=round(dec_ms, 4), grouping=out)
 
 
+def bpf_filter_bench(ctx, n=64 * 2**20, reps=10):
+    """Row (f)4: classic BPF (the reference's own TestBPFInstruction programs)
+    over 64M C4 IMIX packets in HBM: gpk_bpf_run (return value per packet) and
+    gpk_bpf_select (compacted matching index). Timed with HIP events; a
+    sample of 2048 packets checked against the oracle (libpcap bpf_filter)."""
+    import torch
+    from gopacket_amd import bpf, synth
+    from oracle import oracle as O
+    d, o, c = synth.device_batch(4, 0, n)
+    stream = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    g = json.load(open(os.path.join(ROOT, "tests", "golden", "bpf_programs.json")))
+    progs = {x["filter"]: x["insns"] for x in g["instruction_cases"] if not x["error"]}
+    rng = np.random.default_rng(8)
+    sample = np.unique(rng.integers(0, n, 2048))
+    out = {}
+    ret = torch.empty(n, dtype=torch.int32, device="cuda")
+    for name, prog in progs.items():
+        f = bpf.NewBPFInstructionFilter(prog)
+        f.Run(d, o, c, ret=ret)
+        e0.record(stream)
+        for _ in range(reps):
+            f.Run(d, o, c, ret=ret)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        run_ms = e0.elapsed_time(e1) / reps
+        f.Select(d, o, c)
+        e0.record(stream)
+        for _ in range(reps):
+            oo, oc, oi, cnt = f.Select(d, o, c)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        sel_ms = e0.elapsed_time(e1) / reps
+        got = ret.cpu().numpy()[sample].astype(np.uint32)
+        pk = [synth.packet(4, int(i)) for i in sample]
+        cap = np.array([len(x) for x in pk], np.uint32)
+        off = np.concatenate([[0], np.cumsum(cap[:-1], dtype=np.uint64)]).astype(np.uint64)
+        ref = O.bpf_batch(prog, np.frombuffer(b"".join(pk) + bytes(16), np.uint8), off, cap)
+        out[name] = dict(insns=len(prog), run_ms=round(run_ms, 4), run_Gpkts_s=round(n / run_ms / 1e6, 2),
+                         select_ms=round(sel_ms, 4), matches=int(cnt.item()),
+                         index_GBps=round(n * 16 / (run_ms * 1e-3) / 1e9, 1),
+                         parity="%s (%d sampled packets vs oracle)" % ("bit-exact" if np.array_equal(got, ref)
+                                                                       else "MISMATCH", len(sample)))
+        f.close()
+    return dict(workload="(f)4: classic BPF (pcap_test.go TestBPFInstruction programs) over 64M C4 IMIX "
+                         "packets in HBM", packets=n, programs=out)
+
+
 def load_traffic(name, n):
     """HBM bytes per launch of the decode kernel from the committed PMC
     profile (profiles/hbm_traffic.json, tools/make_profiles.py): measured
@@ -436,6 +484,7 @@ def main():
                     help="also drain MPKTS Mi packets from an emulated TPACKET_V3 ring (gpk_tpacket_pump)")
     ap.add_argument("--flows", action="store_true",
                     help="also time row (f)3: flow-keyed grouping of 64M C6 packets (gpk_group_batch)")
+    ap.add_argument("--bpf", action="store_true", help="also time row (f)4: classic BPF over 64M C4 packets")
     ap.add_argument("--tables", default="auto", choices=["auto", "global"],
                     help="next-layer tables: compact LDS copy (auto) or device-memory tables (global)")
     args = ap.parse_args()
@@ -489,6 +538,8 @@ def main():
             out["pcie_inclusive"] = pcie_inclusive(head, ctx)
         if args.c5 > 0 and world == 1:
             out["c5"] = c5_replay(ctx, gib=args.c5)
+        if args.bpf and world == 1:
+            out["bpf"] = bpf_filter_bench(ctx)
         if args.flows and world == 1:
             out["flows"] = flow_grouping(ctx)
         if args.afpacket > 0 and world == 1:
