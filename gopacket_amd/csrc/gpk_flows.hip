@@ -242,7 +242,57 @@ __global__ void __launch_bounds__(256) finish_kernel(const uint32_t* fs, const u
   }
 }
 
+// pack: caplens of the packets in `order`, then one wave per packet copying
+// its bytes (64 consecutive bytes per wave instruction on both sides)
+__global__ void __launch_bounds__(256) pack_caplens_kernel(const uint32_t* caplens, const uint32_t* order, uint64_t m,
+                                                           uint32_t* out_caplens) {
+  const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j < m) out_caplens[j] = caplens[order[j]];
+}
+
+__global__ void __launch_bounds__(256) pack_bytes_kernel(const uint8_t* data, const uint64_t* offsets,
+                                                         const uint32_t* order, const uint32_t* out_caplens,
+                                                         const uint64_t* out_offsets, uint64_t m, uint8_t* out) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t waves = (uint64_t)gridDim.x * (blockDim.x / 64);
+  for (uint64_t j = (uint64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); j < m; j += waves) {
+    const uint8_t* src = data + offsets[order[j]];
+    uint8_t* dst = out + out_offsets[j];
+    const uint32_t n = out_caplens[j];
+    for (uint32_t b = lane; b < n; b += 64) dst[b] = src[b];
+  }
+}
+
+struct Widen64 {
+  __host__ __device__ uint64_t operator()(uint32_t v) const { return v; }
+};
+
 }  // namespace
+
+extern "C" int gpk_pack_batch(const gpk_batch* in, const uint32_t* order, uint64_t m, uint8_t* out_data,
+                              uint64_t* out_offsets, uint32_t* out_caplens, void* stream) {
+  if (!in || (m && (!order || !out_data || !out_offsets || !out_caplens || !in->data || !in->offsets ||
+                    !in->caplens)))
+    return GPK_EINVAL;
+  if (m == 0) return GPK_OK;
+  if (m >= (1ull << 31)) return GPK_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  const dim3 blk(256), grd((unsigned)((m + 255) / 256));
+  hipLaunchKernelGGL(pack_caplens_kernel, grd, blk, 0, s, in->caplens, order, m, out_caplens);
+  hipcub::TransformInputIterator<uint64_t, Widen64, const uint32_t*> it(out_caplens, Widen64());
+  size_t tb = 0;
+  if (hipcub::DeviceScan::ExclusiveSum(nullptr, tb, it, out_offsets, (int)m, s) != hipSuccess) return GPK_EHIP;
+  void* tmp = nullptr;
+  if (hipMallocAsync(&tmp, tb, s) != hipSuccess) return GPK_ENOMEM;
+  const bool ok = hipcub::DeviceScan::ExclusiveSum(tmp, tb, it, out_offsets, (int)m, s) == hipSuccess;
+  (void)hipFreeAsync(tmp, s);
+  if (!ok) return GPK_EHIP;
+  const uint64_t want = (m + 3) / 4;  // 4 waves per block, one packet per wave per pass
+  const unsigned blocks = (unsigned)(want < 65536 ? want : 65536);
+  hipLaunchKernelGGL(pack_bytes_kernel, dim3(blocks), blk, 0, s, in->data, in->offsets, order, out_caplens,
+                     out_offsets, m, out_data);
+  return hipGetLastError() == hipSuccess ? GPK_OK : GPK_EHIP;
+}
 
 struct gpk_grouper {
   int device = 0;

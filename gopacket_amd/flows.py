@@ -71,3 +71,21 @@ class Grouper:
             self.close()
         except Exception:
             pass
+
+
+def pack_batch(data, offsets, caplens, order, total_bytes=None, stream=None):
+    """gpk_pack_batch: the packets `order` (device int32 tensor) of a device
+    batch, made dense in that order. Returns (data, offsets, caplens) tensors."""
+    import torch
+    m = order.numel()
+    dev = order.device
+    if total_bytes is None:
+        total_bytes = int(caplens.index_select(0, order.long()).sum(dtype=torch.int64).item()) if m else 0
+    out_d = torch.empty(total_bytes + 16, dtype=torch.uint8, device=dev)
+    out_o = torch.empty(max(m, 1), dtype=torch.int64, device=dev)
+    out_c = torch.empty(max(m, 1), dtype=torch.int32, device=dev)
+    b = _lib.Batch(data.data_ptr(), offsets.data_ptr(), caplens.data_ptr(), offsets.numel(), data.numel())
+    sp = None if stream is None else (stream if isinstance(stream, int) else stream.cuda_stream)
+    _lib.check(_lib.lib().gpk_pack_batch(ctypes.byref(b), order.data_ptr() if m else None, m, out_d.data_ptr(),
+                                         out_o.data_ptr(), out_c.data_ptr(), sp))
+    return out_d, out_o[:m], out_c[:m]

@@ -5,6 +5,12 @@ parser.go:304, layers_decoder.go:20), so a batch splits into contiguous
 per-GPU ranges with no collective on the data path; results are disjoint
 index ranges that concatenate. One process per GPU (torch.distributed),
 each decoding its range on its own HIP stream.
+
+The one step with a real exchange is flow affinity across GPUs: the
+reference's sharding idiom (doc.go:219-225, channels[FastHash() & 7]) at node
+scale, where every rank must end up with all packets of its flows (both
+directions). exchange_packets does that with three all-to-alls (counts,
+capture lengths, packet bytes); over RCCL they run on xGMI.
 """
 import numpy as np
 
@@ -37,3 +43,49 @@ def max_over_ranks(x, world, device=None):
     t = torch.tensor([float(x)], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def exchange_packets(data, offsets, caplens, dest, world, group=None, pack=None):
+    """All-to-all of whole packets: packet i goes to rank dest[i] (dest[i] < 0:
+    dropped). Every rank calls it with its own batch (torch tensors on its
+    device for RCCL, CPU tensors for gloo). Returns (data, offsets, caplens,
+    src_rank, src_index) of the packets this rank receives, ordered by source
+    rank, then by the source's batch order.
+
+    pack(data, offsets, caplens, order) -> (dense bytes, offsets, caplens):
+    gopacket_amd.flows.pack_batch (the HIP kernel) by default; a test on
+    CPU tensors passes its own."""
+    import torch
+    import torch.distributed as dist
+    if pack is None:
+        from .flows import pack_batch as pack
+    dev = offsets.device
+    dest = dest.to(torch.int64)
+    keep = dest >= 0
+    key = torch.where(keep, dest, torch.full_like(dest, world))
+    _, order = torch.sort(key, stable=True)
+    n_keep = int(keep.sum().item())
+    order = order[:n_keep].to(torch.int32)
+    send_pkts = torch.bincount(dest[keep], minlength=world).to(torch.int64)
+    pdata, _, pcap = pack(data, offsets, caplens, order)
+    pcap64 = pcap.to(torch.int64)
+    bounds = torch.cumsum(send_pkts, 0)
+    csum = torch.cat([torch.zeros(1, dtype=torch.int64, device=dev), torch.cumsum(pcap64, 0)])
+    send_bytes = csum[bounds] - csum[bounds - send_pkts]
+    recv_pkts = torch.empty_like(send_pkts)
+    recv_bytes = torch.empty_like(send_bytes)
+    dist.all_to_all_single(recv_pkts, send_pkts, group=group)
+    dist.all_to_all_single(recv_bytes, send_bytes, group=group)
+    sp, rp = send_pkts.tolist(), recv_pkts.tolist()
+    sb, rb = send_bytes.tolist(), recv_bytes.tolist()
+    r_cap = torch.empty(sum(rp), dtype=torch.int32, device=dev)
+    r_idx = torch.empty(sum(rp), dtype=torch.int32, device=dev)
+    r_data = torch.empty(sum(rb) + 16, dtype=torch.uint8, device=dev)
+    dist.all_to_all_single(r_cap, pcap.contiguous(), output_split_sizes=rp, input_split_sizes=sp, group=group)
+    dist.all_to_all_single(r_idx, order.contiguous(), output_split_sizes=rp, input_split_sizes=sp, group=group)
+    dist.all_to_all_single(r_data[:sum(rb)], pdata[:sum(sb)].contiguous(), output_split_sizes=rb,
+                           input_split_sizes=sb, group=group)
+    r_off = torch.cat([torch.zeros(1, dtype=torch.int64, device=dev),
+                       torch.cumsum(r_cap.to(torch.int64), 0)[:-1]]) if len(r_cap) else r_cap.to(torch.int64)
+    src = torch.repeat_interleave(torch.arange(world, device=dev), torch.tensor(rp, device=dev))
+    return r_data, r_off, r_cap, src, r_idx

@@ -80,6 +80,15 @@ typedef struct gpk_groups {
 int gpk_group_batch(gpk_grouper* g, const gpk_batch* batch, const gpk_results* res, int kind, uint32_t buckets,
                     const gpk_groups* out, void* stream);
 
+/* Pack packets order[0..m) of a batch into a dense batch, in that order:
+ * out_data receives their bytes back to back (it must hold their total
+ * length), out_offsets[j] / out_caplens[j] index packet order[j]. The send
+ * side of a per-flow exchange between GPUs (gopacket_amd/shard.py
+ * exchange_packets: the doc.go:219-225 sharding idiom across ranks), or a
+ * filtered batch made dense. Device arrays; asynchronous on stream. */
+int gpk_pack_batch(const gpk_batch* in, const uint32_t* order, uint64_t m, uint8_t* out_data, uint64_t* out_offsets,
+                   uint32_t* out_caplens, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
