@@ -9,7 +9,8 @@
 //                     packet has no key; store the key words and a 64-bit hash
 //   2. insert_kernel  open-addressing table in HBM: the hash picks the slot,
 //                     the full key words decide equality (a hash collision
-//                     probes on), atomicMin keeps each key's first packet
+//                     probes on), a 64-bit atomicMin of the slot word keeps
+//                     each key's first packet in its index field
 //   3. first_kernel   every keyed packet gets its key's first packet index
 //   4. radix sort     (first index, packet index) pairs, stable, on the bits
 //                     the batch size needs: groups in order of first
@@ -176,8 +177,8 @@ __device__ __forceinline__ bool same_key(const uint32_t* keys, uint64_t a, uint6
 }
 
 __global__ void __launch_bounds__(256) insert_kernel(const uint32_t* keys, const uint64_t* hash, const int32_t* code,
-                                                     uint64_t n, unsigned long long* table, uint32_t* slot_min,
-                                                     uint64_t tmask, uint32_t* slot_of) {
+                                                     uint64_t n, unsigned long long* table, uint64_t tmask,
+                                                     uint32_t* slot_of) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n || code[i]) return;
   const uint64_t h = hash[i];
@@ -194,20 +195,23 @@ __global__ void __launch_bounds__(256) insert_kernel(const uint32_t* keys, const
     if ((cur >> kIdxBits) == tag && same_key(keys, i, cur & kIdxMask)) break;
     pos = (pos + 1) & tmask;
   }
-  // elephant flows hit one slot many times: skip the atomic once it cannot lower the minimum
-  if (__hip_atomic_load(&slot_min[pos], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) > (uint32_t)i)
-    atomicMin(&slot_min[pos], (uint32_t)i);
+  // The slot word's index field becomes the key's first packet: the tag is the
+  // same for every packet of the key, so a 64-bit atomicMin of the word lowers
+  // only the index. Elephant flows hit one slot many times: skip the atomic
+  // once it cannot lower it.
+  if ((__hip_atomic_load(&table[pos], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & kIdxMask) > i)
+    atomicMin(&table[pos], word);
   slot_of[i] = (uint32_t)pos;
 }
 
 __global__ void __launch_bounds__(256) first_kernel(const int32_t* code, const uint32_t* slot_of,
-                                                    const uint32_t* slot_min, const uint64_t* hash,
+                                                    const unsigned long long* table, const uint64_t* hash,
                                                     const uint32_t* bucket_min, int kind, uint64_t n, uint32_t* f,
                                                     uint32_t* iota) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   uint32_t v = (uint32_t)n;  // not keyed: sorts after every group
-  if (!code[i]) v = kind == GPK_GROUP_NET_BUCKET ? bucket_min[hash[i]] : slot_min[slot_of[i]];
+  if (!code[i]) v = kind == GPK_GROUP_NET_BUCKET ? bucket_min[hash[i]] : (uint32_t)(table[slot_of[i]] & kIdxMask);
   f[i] = v;
   iota[i] = (uint32_t)i;
 }
@@ -302,7 +306,6 @@ struct gpk_grouper {
   int32_t* code = nullptr;
   uint32_t* slot_of = nullptr;
   unsigned long long* table = nullptr;
-  uint32_t* slot_min = nullptr;
   uint32_t* bucket_min = nullptr;
   uint32_t* f = nullptr;
   uint32_t* fs = nullptr;
@@ -323,7 +326,7 @@ int end_bit(uint64_t n) {  // bits to hold 0..n
 
 void free_all(gpk_grouper* g) {
   for (void* p : {(void*)g->keys, (void*)g->hash, (void*)g->code, (void*)g->slot_of, (void*)g->table,
-                  (void*)g->slot_min, (void*)g->bucket_min, (void*)g->f, (void*)g->fs, (void*)g->iota,
+                  (void*)g->bucket_min, (void*)g->f, (void*)g->fs, (void*)g->iota,
                   (void*)g->heads, (void*)g->gid, g->tmp})
     if (p) (void)hipFree(p);
 }
@@ -352,7 +355,6 @@ extern "C" int gpk_grouper_create(gpk_grouper** out, int device, uint64_t max_pa
        hipMalloc((void**)&g->hash, n * 8) == hipSuccess && hipMalloc((void**)&g->code, n * 4) == hipSuccess &&
        hipMalloc((void**)&g->slot_of, n * 4) == hipSuccess &&
        hipMalloc((void**)&g->table, g->tsize * 8) == hipSuccess &&
-       hipMalloc((void**)&g->slot_min, g->tsize * 4) == hipSuccess &&
        hipMalloc((void**)&g->bucket_min, (1u << 16) * 4) == hipSuccess &&
        hipMalloc((void**)&g->f, n * 4) == hipSuccess && hipMalloc((void**)&g->fs, n * 4) == hipSuccess &&
        hipMalloc((void**)&g->iota, n * 4) == hipSuccess && hipMalloc((void**)&g->heads, n * 4) == hipSuccess &&
@@ -392,17 +394,16 @@ extern "C" int gpk_group_batch(gpk_grouper* g, const gpk_batch* b, const gpk_res
   const dim3 blk(256), grd((unsigned)((n + 255) / 256));
   if (kind == GPK_GROUP_NET_BUCKET) {
     if (hipMemsetAsync(g->bucket_min, 0xFF, (size_t)buckets * 4, s) != hipSuccess) return GPK_EHIP;
-  } else if (hipMemsetAsync(g->table, 0xFF, g->tsize * 8, s) != hipSuccess ||
-             hipMemsetAsync(g->slot_min, 0xFF, g->tsize * 4, s) != hipSuccess) {
+  } else if (hipMemsetAsync(g->table, 0xFF, g->tsize * 8, s) != hipSuccess) {
     return GPK_EHIP;
   }
   KeyArgs a{b->data, b->offsets, b->caplens, r->records, r->layouts, r->flows, n, kind, buckets,
             g->keys, g->hash, g->code, g->bucket_min};
   hipLaunchKernelGGL(key_kernel, grd, blk, 0, s, a);
   if (kind != GPK_GROUP_NET_BUCKET)
-    hipLaunchKernelGGL(insert_kernel, grd, blk, 0, s, g->keys, g->hash, g->code, n, g->table, g->slot_min,
-                       g->tsize - 1, g->slot_of);
-  hipLaunchKernelGGL(first_kernel, grd, blk, 0, s, g->code, g->slot_of, g->slot_min, g->hash, g->bucket_min, kind, n,
+    hipLaunchKernelGGL(insert_kernel, grd, blk, 0, s, g->keys, g->hash, g->code, n, g->table, g->tsize - 1,
+                       g->slot_of);
+  hipLaunchKernelGGL(first_kernel, grd, blk, 0, s, g->code, g->slot_of, g->table, g->hash, g->bucket_min, kind, n,
                      g->f, g->iota);
   size_t tb = g->tmp_bytes;
   if (hipcub::DeviceRadixSort::SortPairs(g->tmp, tb, g->f, g->fs, g->iota, o->perm, (int)n, 0, end_bit(n), s) !=
