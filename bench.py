@@ -401,9 +401,30 @@ def flow_grouping(ctx, n=64 * 2**20, reps=5):
                          parity="%s (sampled groups vs oracle keys)" % ("ok" if ok else "MISMATCH")
                          if kind != FO.NET_BUCKET else "see tests/test_flows_gpu.py")
     g.close()
+    del d, o, c, rec, err, fl, lay
+    torch.cuda.empty_cache()
+    # CPU baseline: the reference keys each packet with one map lookup (single
+    # goroutine per StreamPool / defragmenter); its C restatement with a hash
+    # map, one thread, over a 1 Mi-packet host sample of the same traffic
+    # (decode results precomputed, untimed)
+    m = 1 << 20
+    hd, ho, hc = synth.host_batch(6, 0, m)
+    hr = O.OracleParser(17, dec).decode(hd, ho, hc, nthreads=16, layouts=True)
+    cpu = {}
+    for name, kind in (("connection", FO.CONNECTION), ("defrag", FO.DEFRAG), ("net_bucket8", FO.NET_BUCKET)):
+        reps, t0 = 0, time.perf_counter()
+        while True:
+            O.group_batch(kind, hd, ho, hr["records"], hr["layouts"], hr["flows"], 8)
+            reps += 1
+            el = time.perf_counter() - t0
+            if el >= 2.0:
+                break
+        cpu[name] = round(reps * m / el / 1e6, 2)
     return dict(workload="(f)3: C6 64M packets (IMIX, 2^20 heavy-tailed flows, both directions, 5%% IPv4 "
                          "fragments), decode with layouts, then group by consumer key in HBM",
-                packets=n, decode_with_layouts_ms=round(dec_ms, 4), grouping=out)
+                packets=n, decode_with_layouts_ms=round(dec_ms, 4), grouping=out,
+                cpu_baseline=dict(Mpkts_s=cpu, cores=1, kind="port",
+                                  sample="1 Mi C6 packets, oracle/flows_oracle.c (one hash-map lookup per packet)"))
 
 
 def bpf_filter_bench(ctx, n=64 * 2**20, reps=10):
@@ -450,6 +471,20 @@ def bpf_filter_bench(ctx, n=64 * 2**20, reps=10):
                          parity="%s (%d sampled packets vs oracle)" % ("bit-exact" if np.array_equal(got, ref)
                                                                        else "MISMATCH", len(sample)))
         f.close()
+    # CPU baseline: libpcap's bpf_filter restated (oracle/bpf_oracle.c), one
+    # thread as pcap_offline_filter runs per handle, over a 1 Mi-packet sample
+    m = 1 << 20
+    hd, ho, hc = synth.host_batch(4, 0, m)
+    for name, prog in progs.items():
+        reps, t0 = 0, time.perf_counter()
+        while True:
+            O.bpf_batch(prog, hd, ho, hc)
+            reps += 1
+            el = time.perf_counter() - t0
+            if el >= 1.5:
+                break
+        out[name]["cpu_baseline"] = dict(Mpkts_s=round(reps * m / el / 1e6, 2), cores=1, kind="port",
+                                         sample="1 Mi C4 packets, oracle/bpf_oracle.c")
     return dict(workload="(f)4: classic BPF (pcap_test.go TestBPFInstruction programs) over 64M C4 IMIX "
                          "packets in HBM", packets=n, programs=out)
 

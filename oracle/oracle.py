@@ -157,3 +157,19 @@ def bpf_batch(insns, data, offsets, caplens, wirelens=None):
     L.oracle_bpf_batch(prog.ctypes.data, len(prog), data.ctypes.data, offsets.ctypes.data, caplens.ctypes.data,
                        w.ctypes.data if w is not None else None, len(offsets), ret.ctypes.data)
     return ret
+
+
+def group_batch(kind, data, offsets, records, layouts, flows=None, buckets=8):
+    """oracle/flows_oracle.c: (number of groups, group_of per packet)."""
+    L = lib()
+    n = len(offsets)
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+    out = np.zeros(n, np.int32)
+    L.oracle_group_batch.restype = ctypes.c_int64
+    L.oracle_group_batch.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                     ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_void_p]
+    g = L.oracle_group_batch(int(kind), data.ctypes.data, offsets.ctypes.data, records.ctypes.data,
+                             layouts.ctypes.data if layouts is not None else None,
+                             flows.ctypes.data if flows is not None else None, n, buckets, out.ctypes.data)
+    return g, out

@@ -92,3 +92,19 @@ def test_c6_traffic_has_repeating_flows_in_both_directions():
     fgroups, fcodes = FO.group(FO.DEFRAG, pk, res["records"], res["layouts"])
     assert len(fgroups) > 100 and max(len(v) for v in fgroups.values()) >= 2
     assert fcodes.count(FO.NONE) > 0.8 * len(pk)
+
+
+def test_c_restatement_equals_python_oracle():
+    """oracle/flows_oracle.c (the CPU baseline) keys exactly like the Python oracle."""
+    from gopacket_amd import synth
+    from oracle import oracle as O
+    data, off, cap = synth.host_batch(6, 500, 30000)
+    pk = [bytes(data[o:o + c]) for o, c in zip(off, cap)] + pktutil.fuzz_packets(8, 5000)
+    frames, _ = flowcases.defrag_frames()
+    pk += list(frames.values()) + [f for _, f in flowcases.defrag_struct_cases()] + flowcases.connection_cases()
+    d, o, c = pktutil.pack(pk)
+    res = oracle_parser(flowcases.DEFRAG_PARSER).decode(d, o, c, layouts=True)
+    for kind, buckets in ((FO.CONNECTION, 8), (FO.DEFRAG, 8), (FO.NET_BUCKET, 8), (FO.NET_BUCKET, 256)):
+        groups, codes = FO.group(kind, pk, res["records"], res["layouts"], res["flows"], buckets)
+        g, out = O.group_batch(kind, d, o, res["records"], res["layouts"], res["flows"], buckets)
+        assert g == len(groups) and out.tolist() == codes, kind
