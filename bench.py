@@ -400,6 +400,22 @@ def flow_grouping(ctx, n=64 * 2**20, reps=5):
         out[name] = dict(ms=round(ms, 4), Mpkts_s=round(n / ms / 1e3, 1), groups=G, keyed_packets=K,
                          parity="%s (sampled groups vs oracle keys)" % ("ok" if ok else "MISMATCH")
                          if kind != FO.NET_BUCKET else "see tests/test_flows_gpu.py")
+    # fused: the decode kernel derives the key (no layouts, no second header pass)
+    fused = {}
+    for name, kind in (("connection", FO.CONNECTION), ("defrag", FO.DEFRAG)):
+        res = g.decode_group(ctx, parser, d, o, c, rec, err, fl, kind=kind)
+        e0.record(stream)
+        for _ in range(reps):
+            res = g.decode_group(ctx, parser, d, o, c, rec, err, fl, kind=kind)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / reps
+        G, K = res["counts"].cpu().tolist()
+        same = (G, K) == (out[name]["groups"], out[name]["keyed_packets"])
+        fused[name] = dict(decode_and_group_ms=round(ms, 4), Mpkts_s=round(n / ms / 1e3, 1),
+                           separate_ms=round(dec_ms + out[name]["ms"], 4),
+                           same_groups_as_separate="yes" if same else "NO")
+    out["fused_decode_group"] = fused
     g.close()
     del d, o, c, rec, err, fl, lay
     torch.cuda.empty_cache()
@@ -554,7 +570,7 @@ def main():
                        "parser": "+".join(CONFIGS[head]["decoders"])},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": load_traffic(head, r["n"]),
-                         "kernel": "gpk::decode_kernel<true,false,true>", "traffic_unit": "bytes per launch", "kernel_ms": round(r["kernel_ms"], 4),
+                         "kernel": "gpk::decode_kernel<true,false,true,false>", "traffic_unit": "bytes per launch", "kernel_ms": round(r["kernel_ms"], 4),
                          "algo_bytes_per_launch": r["algo_bytes"],
                          "probe_read_GBps": r["probe_gbs"] and round(r["probe_gbs"], 1)},
             "parity": r["parity"],

@@ -66,7 +66,7 @@ EXPORTS = (
     "gpk_tpacket_take_new_headers", "gpk_tpacket_geometry", "gpk_tpacket_error", "gpk_tpacket_stats",
     "gpk_tpacket_socket_stats", "gpk_tpacket_set_bpf", "gpk_tpacket_set_fanout", "gpk_tpacket_pump",
     # include/gpk_flows.h
-    "gpk_grouper_create", "gpk_grouper_destroy", "gpk_group_batch", "gpk_pack_batch",
+    "gpk_grouper_create", "gpk_grouper_destroy", "gpk_group_batch", "gpk_pack_batch", "gpk_decode_group_batch",
     # include/gpk_bpf.h
     "gpk_bpf_create", "gpk_bpf_destroy", "gpk_bpf_run", "gpk_bpf_select",
 )
@@ -256,6 +256,7 @@ def lib():
         "gpk_grouper_destroy": ([vp], c_int),
         "gpk_group_batch": ([vp, P(Batch), P(Results), c_int, u32, P(Groups), vp], c_int),
         "gpk_pack_batch": ([P(Batch), vp, u64, vp, vp, vp, vp], c_int),
+        "gpk_decode_group_batch": ([vp, vp, P(Batch), P(Results), vp, c_int, P(Groups), vp], c_int),
         "gpk_bpf_create": ([P(vp), vp, u32, ctypes.c_char_p, ctypes.c_size_t], c_int),
         "gpk_bpf_destroy": ([vp], c_int),
         "gpk_bpf_run": ([vp, P(Batch), vp, vp, vp], c_int),

@@ -62,6 +62,12 @@ struct KParams {
   const uint32_t* ctab;     // compact blob in device memory, or null: global tables
   CompactGeom cg;
   uint32_t fast;            // GPK_FAST_* : which transitions the straight-line path may take
+  // fused grouping keys (gpk_decode_group_batch): 0 = off, else GPK_GROUP_CONNECTION /
+  // GPK_GROUP_DEFRAG; per packet 10 key words, a 64-bit hash and a reason code
+  int32_t key_kind;
+  uint32_t* keys;
+  uint64_t* khash;
+  int32_t* kcode;
 };
 
 // Straight-line common-case parse (fast_parser below). Each bit says the

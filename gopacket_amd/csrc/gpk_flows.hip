@@ -27,6 +27,10 @@
 
 #include "../../include/gpk_flows.h"
 
+// gpk_host.cpp: gpk_decode_batch with the fused key derivation
+int gpk_decode_batch_keys(gpk_ctx* c, const gpk_parser* p, const gpk_batch* b, const gpk_results* o, int key_kind,
+                          uint32_t* keys, uint64_t* khash, int32_t* kcode, void* stream);
+
 namespace {
 
 constexpr int kKeyWords = 10;
@@ -333,6 +337,8 @@ void free_all(gpk_grouper* g) {
 
 }  // namespace
 
+static int group_rest(gpk_grouper* g, uint64_t n, int kind, const gpk_groups& o, hipStream_t s);
+
 extern "C" int gpk_grouper_create(gpk_grouper** out, int device, uint64_t max_packets) {
   if (!out || max_packets == 0 || max_packets >= (1ull << kIdxBits)) return GPK_EINVAL;
   int ndev = 0;
@@ -400,19 +406,42 @@ extern "C" int gpk_group_batch(gpk_grouper* g, const gpk_batch* b, const gpk_res
   KeyArgs a{b->data, b->offsets, b->caplens, r->records, r->layouts, r->flows, n, kind, buckets,
             g->keys, g->hash, g->code, g->bucket_min};
   hipLaunchKernelGGL(key_kernel, grd, blk, 0, s, a);
+  return group_rest(g, n, kind, *o, s);
+}
+
+extern "C" int gpk_decode_group_batch(gpk_ctx* ctx, const gpk_parser* p, const gpk_batch* b, const gpk_results* r,
+                                      gpk_grouper* g, int kind, const gpk_groups* o, void* stream) {
+  if (!ctx || !p || !b || !r || !g || !o || !o->group_of || !o->perm || !o->start || !o->first || !o->counts)
+    return GPK_EINVAL;
+  if (kind != GPK_GROUP_CONNECTION && kind != GPK_GROUP_DEFRAG) return GPK_EINVAL;
+  const uint64_t n = b->n;
+  if (n > g->cap) return GPK_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  int rc = gpk_decode_batch_keys(ctx, p, b, r, kind, g->keys, g->hash, g->code, stream);
+  if (rc) return rc;
+  if (hipSetDevice(g->device) != hipSuccess) return GPK_EHIP;
+  if (hipMemsetAsync(o->counts, 0, 8, s) != hipSuccess || hipMemsetAsync(o->start, 0, 4, s) != hipSuccess)
+    return GPK_EHIP;
+  if (n == 0) return GPK_OK;
+  if (hipMemsetAsync(g->table, 0xFF, g->tsize * 8, s) != hipSuccess) return GPK_EHIP;
+  return group_rest(g, n, kind, *o, s);
+}
+
+static int group_rest(gpk_grouper* g, uint64_t n, int kind, const gpk_groups& o, hipStream_t s) {
+  const dim3 blk(256), grd((unsigned)((n + 255) / 256));
   if (kind != GPK_GROUP_NET_BUCKET)
     hipLaunchKernelGGL(insert_kernel, grd, blk, 0, s, g->keys, g->hash, g->code, n, g->table, g->tsize - 1,
                        g->slot_of);
   hipLaunchKernelGGL(first_kernel, grd, blk, 0, s, g->code, g->slot_of, g->table, g->hash, g->bucket_min, kind, n,
                      g->f, g->iota);
   size_t tb = g->tmp_bytes;
-  if (hipcub::DeviceRadixSort::SortPairs(g->tmp, tb, g->f, g->fs, g->iota, o->perm, (int)n, 0, end_bit(n), s) !=
+  if (hipcub::DeviceRadixSort::SortPairs(g->tmp, tb, g->f, g->fs, g->iota, o.perm, (int)n, 0, end_bit(n), s) !=
       hipSuccess)
     return GPK_EHIP;
   hipLaunchKernelGGL(heads_kernel, grd, blk, 0, s, g->fs, n, g->heads);
   tb = g->tmp_bytes;
   if (hipcub::DeviceScan::InclusiveSum(g->tmp, tb, g->heads, g->gid, (int)n, s) != hipSuccess) return GPK_EHIP;
-  hipLaunchKernelGGL(finish_kernel, grd, blk, 0, s, g->fs, o->perm, g->gid, g->code, n, o->group_of, o->start,
-                     o->first, o->counts);
+  hipLaunchKernelGGL(finish_kernel, grd, blk, 0, s, g->fs, o.perm, g->gid, g->code, n, o.group_of, o.start,
+                     o.first, o.counts);
   return hipGetLastError() == hipSuccess ? GPK_OK : GPK_EHIP;
 }

@@ -377,6 +377,10 @@ static int make_params(gpk_ctx* c, const gpk_parser* p, const gpk_batch* b, cons
   P.first = p->first;
   P.outputs = p->outputs;
   P.ignore_unsupported = p->ignore_unsupported;
+  P.key_kind = 0;
+  P.keys = nullptr;
+  P.khash = nullptr;
+  P.kcode = nullptr;
   return GPK_OK;
 }
 
@@ -385,6 +389,29 @@ int gpk_decode_batch(gpk_ctx* c, const gpk_parser* p, const gpk_batch* b, const 
   gpk::KParams P;
   int rc = make_params(c, p, b, o, P);
   if (rc) return rc;
+  hipStream_t s = (hipStream_t)stream;
+  std::lock_guard<std::mutex> g(c->mu);
+  HIPCHK(hipSetDevice(c->device));
+  rc = upload(c, p, s, P);
+  if (rc) return rc;
+  HIPCHK(gpk_launch_decode(&P, (p->outputs & GPK_OUT_L4_CSUM) != 0, o->layouts != nullptr, s));
+  return GPK_OK;
+}
+
+// gpk_decode_batch plus the fused grouping key per packet (gpk_flows.hip
+// gpk_decode_group_batch): library-internal, not part of the C ABI.
+__attribute__((visibility("hidden"))) int gpk_decode_batch_keys(gpk_ctx* c, const gpk_parser* p, const gpk_batch* b,
+                                                                const gpk_results* o, int key_kind, uint32_t* keys,
+                                                                uint64_t* khash, int32_t* kcode, void* stream) {
+  if (!o || o->layouts || (key_kind != 1 && key_kind != 2) || (b && b->n && (!keys || !khash || !kcode)))
+    return GPK_EINVAL;
+  gpk::KParams P;
+  int rc = make_params(c, p, b, o, P);
+  if (rc) return rc;
+  P.key_kind = key_kind;
+  P.keys = keys;
+  P.khash = khash;
+  P.kcode = kcode;
   hipStream_t s = (hipStream_t)stream;
   std::lock_guard<std::mutex> g(c->mu);
   HIPCHK(hipSetDevice(c->device));

@@ -298,7 +298,68 @@ __device__ __forceinline__ uint64_t shfl_down64(uint64_t v, int d) {
   return ((uint64_t)(uint32_t)__shfl_down((int)(uint32_t)(v >> 32), d) << 32) | (uint32_t)__shfl_down((int)(uint32_t)v, d);
 }
 
-template <bool kL4, bool kLayout, class TT>
+// The grouping key of gpk_flows.hip's key_kernel, derived here from the parse
+// and the header bytes still in this lane's LDS window (include/gpk_flows.h:
+// tcpassembly's key{netFlow, TransportFlow()}, ip4defrag's ipv4{NetworkFlow(),
+// Id}), so the grouping needs no second pass over layouts and headers. Same
+// words, same hash, same reason codes as key_kernel.
+__device__ __forceinline__ uint32_t rd4raw(const Rd& r, uint32_t p) {
+  return rd8(r, p) | rd8(r, p + 1) << 8 | rd8(r, p + 2) << 16 | rd8(r, p + 3) << 24;
+}
+__device__ __forceinline__ int derive_key(const KParams& P, const Rd& r, const Parse& q, uint32_t err, uint32_t* w) {
+#pragma unroll
+  for (int k = 0; k < 10; k++) w[k] = 0;
+  if (P.key_kind == 1) {  // GPK_GROUP_CONNECTION
+    if (!clean(q, GPK_DEC_TCP)) return -1;
+    uint32_t net = 0;
+    bool seen = false;
+    const uint32_t m = q.nlayers < GPK_MAX_INLINE_LAYERS ? q.nlayers : GPK_MAX_INLINE_LAYERS;
+    for (uint32_t k = 0; k < m && !seen; k++) {
+      const uint32_t c = (uint32_t)(q.layers >> (4 * k)) & 15u;
+      if (c == GPK_CODE_IPV4 || c == GPK_CODE_IPV6) net = c;
+      seen = c == GPK_CODE_TCP;
+    }
+    if (!seen) return -6;
+    if (!net) return -1;
+    const uint32_t t0 = q.start(GPK_DEC_TCP);
+    const uint32_t flags = rd8(r, t0 + 13), doff = rd8(r, t0 + 12) >> 4;
+    if (!(flags & 7u) && (q.end(GPK_DEC_TCP) - t0) - doff * 4 == 0) return -2;
+    if (net == GPK_CODE_IPV4) {
+      const uint32_t ip = clean(q, GPK_DEC_IPV4) ? q.start(GPK_DEC_IPV4) : GPK_LAYOUT_ABSENT;
+      w[0] = 1u | 1u << 8 | 4u << 16;
+      w[1] = rd4raw(r, ip + 12);
+      w[5] = rd4raw(r, ip + 16);
+    } else {
+      const uint32_t ip = clean(q, GPK_DEC_IPV6) ? q.start(GPK_DEC_IPV6) : GPK_LAYOUT_ABSENT;
+      w[0] = 1u | 2u << 8 | 4u << 16;
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        w[1 + k] = rd4raw(r, ip + 8 + 4 * k);
+        w[5 + k] = rd4raw(r, ip + 24 + 4 * k);
+      }
+    }
+    w[9] = rd4raw(r, t0);
+    return 0;
+  }
+  // GPK_GROUP_DEFRAG
+  if (!clean(q, GPK_DEC_IPV4) || (err >= GPK_ERR_IP4_HDR_SHORT && err <= GPK_ERR_IP4_OPT_BADLEN)) return -1;
+  const uint32_t s = q.start(GPK_DEC_IPV4);
+  const uint32_t ff = rd16(r, s + 6), flags = ff >> 13, fo = ff & 0x1FFF;
+  if (flags & 2u) return -1;
+  if (!(flags & 1u) && fo == 0) return -1;
+  uint32_t len = rd16(r, s + 2);
+  if (len == 0) len = (q.end(GPK_DEC_IPV4) - s) & 0xFFFF;
+  if ((flags & 1u) && ((len - (rd8(r, s) & 15u) * 4) & 0xFFFF) < 8) return -3;
+  if (fo > 8183) return -4;
+  if (((fo * 8 + len) & 0xFFFF) > 65535u) return -5;
+  w[0] = 2u | 1u << 8;
+  w[1] = rd4raw(r, s + 12);
+  w[5] = rd4raw(r, s + 16);
+  w[9] = rd16(r, s + 4);
+  return 0;
+}
+
+template <bool kL4, bool kLayout, class TT, bool kKeys = false>
 __device__ __forceinline__ void decode_packet(const KParams& P, const TT& T, uint64_t i, bool active, uint64_t off,
                                               uint32_t cl, uint32_t slot_dw, uint32_t lane) {
   const uint32_t m = (uint32_t)(off & 15);
@@ -574,6 +635,23 @@ __device__ __forceinline__ void decode_packet(const KParams& P, const TT& T, uin
       P.err_args[2 * i] = s.a0;
       P.err_args[2 * i + 1] = s.a1;
     }
+    if (kKeys) {  // fused grouping key (gpk_decode_group_batch)
+      uint32_t w[10];
+      const int c = derive_key(P, r, q, s.err & GPK_ST_ERR_MASK, w);
+      P.kcode[i] = c;
+      if (!c) {
+        uint64_t h = 0x9E3779B97F4A7C15ull;
+#pragma unroll
+        for (int k = 0; k < 10; k++) {
+          P.keys[i * 10 + k] = w[k];
+          h = (h ^ w[k]) * 0xBF58476D1CE4E5B9ull;
+          h ^= h >> 29;
+        }
+        h = (h ^ (h >> 30)) * 0xBF58476D1CE4E5B9ull;
+        h = (h ^ (h >> 27)) * 0x94D049BB133111EBull;
+        P.khash[i] = h ^ (h >> 31);
+      }
+    }
     if (kLayout) {
       const int slot_kind[8] = {GPK_DEC_ETHERNET, GPK_DEC_DOT1Q, GPK_DEC_IPV4, GPK_DEC_IPV6,
                                        GPK_DEC_IPV6_EXT, GPK_DEC_TCP,  GPK_DEC_UDP,  GPK_DEC_PAYLOAD};
@@ -601,7 +679,7 @@ __device__ __forceinline__ void decode_packet(const KParams& P, const TT& T, uin
 // (registers) and the offsets/caplens of tile t+2*grid too, so the global
 // load latency of the read-once header bytes is hidden behind decode work.
 // The LDS slot is lane-private: no barrier between tiles.
-template <bool kL4, bool kLayout, class TT>
+template <bool kL4, bool kLayout, class TT, bool kKeys = false>
 __device__ __forceinline__ void decode_tiles(const KParams& P, const TT& T) {
   const uint32_t tid = threadIdx.x;
   const uint32_t lane = tid & 63;
@@ -624,7 +702,7 @@ __device__ __forceinline__ void decode_tiles(const KParams& P, const TT& T) {
     const uint32_t nc1 = win_chunks(nxt, i1 < P.n);
     load_window(P, nxt, nc1, w);                         // tile t+grid, in flight
     const Idx nn = load_index(P, i1 + stride * kBlock);  // tile t+2*grid
-    decode_packet<kL4, kLayout>(P, T, i, i < P.n, cur.off, cur.cl, slot_dw, lane);
+    decode_packet<kL4, kLayout, TT, kKeys>(P, T, i, i < P.n, cur.off, cur.cl, slot_dw, lane);
     t += stride;
     if (t >= ntiles) break;
     i = i1;
@@ -639,7 +717,7 @@ __device__ __forceinline__ void decode_tiles(const KParams& P, const TT& T) {
     Win w;
     load_window(P, cur, nc, w);
     store_window(slot_dw, nc, w);
-    decode_packet<kL4, kLayout>(P, T, i, i < P.n, cur.off, cur.cl, slot_dw, lane);
+    decode_packet<kL4, kLayout, TT, kKeys>(P, T, i, i < P.n, cur.off, cur.cl, slot_dw, lane);
   }
 #else
   Idx nxt = load_index(P, i);
@@ -650,7 +728,7 @@ __device__ __forceinline__ void decode_tiles(const KParams& P, const TT& T) {
     load_window(P, cur, nc, w);
     nxt = load_index(P, i + stride * kBlock);  // next tile's offsets/caplens
     store_window(slot_dw, nc, w);
-    decode_packet<kL4, kLayout>(P, T, i, i < P.n, cur.off, cur.cl, slot_dw, lane);
+    decode_packet<kL4, kLayout, TT, kKeys>(P, T, i, i < P.n, cur.off, cur.cl, slot_dw, lane);
     t += stride;
     if (t >= ntiles) break;
     i += stride * kBlock;
@@ -663,7 +741,7 @@ __device__ __forceinline__ void decode_tiles(const KParams& P, const TT& T) {
 // read; otherwise they are read from the global DevTables. Either way the
 // only vector-memory traffic of the decode is the packet bytes themselves,
 // so waiting on a lookup never waits on the next tile's prefetch.
-template <bool kL4, bool kLayout, bool kCompact>
+template <bool kL4, bool kLayout, bool kCompact, bool kKeys = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GPK_WAVES_PER_EU, 8))) void decode_kernel(
     KParams P) {
   if ((uint64_t)blockIdx.x * kBlock * GPK_PPL >= P.n) return;  // uniform over the block
@@ -715,24 +793,24 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GPK_WAVE
   }
 #endif
   if (kCompact)
-    decode_packet<kL4, kLayout>(P, LTab{P.cg, base}, i0, i0 < P.n, c0.off, c0.cl, slot_dw, tid & 63);
+    decode_packet<kL4, kLayout, LTab, kKeys>(P, LTab{P.cg, base}, i0, i0 < P.n, c0.off, c0.cl, slot_dw, tid & 63);
   else
-    decode_packet<kL4, kLayout>(P, GTab{P.tab}, i0, i0 < P.n, c0.off, c0.cl, slot_dw, tid & 63);
+    decode_packet<kL4, kLayout, GTab, kKeys>(P, GTab{P.tab}, i0, i0 < P.n, c0.off, c0.cl, slot_dw, tid & 63);
   if (GPK_PPL == 2) {
     store_window(slot_dw, n1, w1);  // lane-private slot, reused
     if (kCompact)
-      decode_packet<kL4, kLayout>(P, LTab{P.cg, base}, i1, i1 < P.n, c1.off, c1.cl, slot_dw, tid & 63);
+      decode_packet<kL4, kLayout, LTab, kKeys>(P, LTab{P.cg, base}, i1, i1 < P.n, c1.off, c1.cl, slot_dw, tid & 63);
     else
-      decode_packet<kL4, kLayout>(P, GTab{P.tab}, i1, i1 < P.n, c1.off, c1.cl, slot_dw, tid & 63);
+      decode_packet<kL4, kLayout, GTab, kKeys>(P, GTab{P.tab}, i1, i1 < P.n, c1.off, c1.cl, slot_dw, tid & 63);
   }
 #else
   if (kCompact) {
     const uint32_t base = kBlock * kSlotDw;
     for (uint32_t w = threadIdx.x; w < P.cg.words; w += kBlock) gpk_smem[base + w] = P.ctab[w];
     __syncthreads();
-    decode_tiles<kL4, kLayout>(P, LTab{P.cg, base});
+    decode_tiles<kL4, kLayout, LTab, kKeys>(P, LTab{P.cg, base});
   } else {
-    decode_tiles<kL4, kLayout>(P, GTab{P.tab});
+    decode_tiles<kL4, kLayout, GTab, kKeys>(P, GTab{P.tab});
   }
 #endif
 }
@@ -752,7 +830,7 @@ __global__ void list_kernel(KParams P, uint64_t index, int64_t* out, uint32_t ca
 
 namespace {
 
-template <bool kL4, bool kLayout, bool kCompact>
+template <bool kL4, bool kLayout, bool kCompact, bool kKeys = false>
 hipError_t launch(const gpk::KParams* P, hipStream_t stream) {
   using namespace gpk;
   constexpr int lds = kCompact ? kLdsBytes + kCtDwords * 4 : kLdsBytes;
@@ -764,7 +842,7 @@ hipError_t launch(const gpk::KParams* P, hipStream_t stream) {
   if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
   if (!cached_bpc[dev]) {
     int bpc = 0, cus = 0;
-    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, decode_kernel<kL4, kLayout, kCompact>, kBlock, lds);
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, decode_kernel<kL4, kLayout, kCompact, kKeys>, kBlock, lds);
     if (e != hipSuccess) return e;
     e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     if (e != hipSuccess) return e;
@@ -779,12 +857,17 @@ hipError_t launch(const gpk::KParams* P, hipStream_t stream) {
   if (ntiles < grid * 8) grid = (ntiles + 7) / 8;
   if (!GPK_PERSISTENT && !GPK_PREFETCH) grid = (ntiles + GPK_PPL - 1) / GPK_PPL;
   if (grid < 1) grid = 1;
-  hipLaunchKernelGGL((decode_kernel<kL4, kLayout, kCompact>), dim3((unsigned)grid), dim3(kBlock), lds, stream, *P);
+  hipLaunchKernelGGL((decode_kernel<kL4, kLayout, kCompact, kKeys>), dim3((unsigned)grid), dim3(kBlock), lds, stream,
+                     *P);
   return hipGetLastError();
 }
 
 template <bool kCompact>
 hipError_t launch_outputs(const gpk::KParams* P, int with_l4, int with_layout, hipStream_t stream) {
+  if (P->key_kind) {  // fused grouping keys: no layouts (gpk_decode_group_batch)
+    if (with_layout) return hipErrorInvalidValue;
+    return with_l4 ? launch<true, false, kCompact, true>(P, stream) : launch<false, false, kCompact, true>(P, stream);
+  }
   if (with_l4 && with_layout) return launch<true, true, kCompact>(P, stream);
   if (with_l4) return launch<true, false, kCompact>(P, stream);
   if (with_layout) return launch<false, true, kCompact>(P, stream);

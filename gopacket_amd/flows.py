@@ -52,6 +52,30 @@ class Grouper:
                                               ctypes.byref(g), sp))
         return out
 
+    def decode_group(self, ctx, parser, data, offsets, caplens, records, err_args=None, flows=None, kind=CONNECTION,
+                     out=None, stream=None):
+        """gpk_decode_group_batch: decode (records/err_args/flows as
+        Context.decode_device, no layouts) and group by `kind` (CONNECTION or
+        DEFRAG) with the key derived inside the decode kernel."""
+        import torch
+        n = offsets.numel()
+        dev = offsets.device
+        if out is None:
+            out = dict(group_of=torch.empty(n, dtype=torch.int32, device=dev),
+                       perm=torch.empty(n, dtype=torch.int32, device=dev),
+                       start=torch.empty(n + 1, dtype=torch.int32, device=dev),
+                       first=torch.empty(max(n, 1), dtype=torch.int32, device=dev),
+                       counts=torch.zeros(2, dtype=torch.int32, device=dev))
+        b = _lib.Batch(data.data_ptr(), offsets.data_ptr(), caplens.data_ptr(), n, data.numel())
+        r = _lib.Results(records.data_ptr(), err_args.data_ptr() if err_args is not None else None,
+                         flows.data_ptr() if flows is not None else None, None)
+        g = _lib.Groups(out["group_of"].data_ptr(), out["perm"].data_ptr(), out["start"].data_ptr(),
+                        out["first"].data_ptr(), out["counts"].data_ptr())
+        sp = None if stream is None else (stream if isinstance(stream, int) else stream.cuda_stream)
+        _lib.check(_lib.lib().gpk_decode_group_batch(ctx.h, parser.h, ctypes.byref(b), ctypes.byref(r), self.h,
+                                                     int(kind), ctypes.byref(g), sp))
+        return out
+
     @staticmethod
     def to_lists(out):
         """Host view: (groups: list of packet-index lists in group order, group_of list)."""

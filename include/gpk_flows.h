@@ -80,6 +80,14 @@ typedef struct gpk_groups {
 int gpk_group_batch(gpk_grouper* g, const gpk_batch* batch, const gpk_results* res, int kind, uint32_t buckets,
                     const gpk_groups* out, void* stream);
 
+/* gpk_decode_batch and gpk_group_batch (CONNECTION or DEFRAG) in one: the
+ * decode kernel derives each packet's key from the header bytes it already
+ * holds in LDS, so the grouping reads no layouts and no header bytes again.
+ * res as for gpk_decode_batch, without layouts (GPK_EINVAL otherwise); same
+ * groups as gpk_decode_batch with layouts followed by gpk_group_batch. */
+int gpk_decode_group_batch(gpk_ctx* ctx, const gpk_parser* p, const gpk_batch* batch, const gpk_results* res,
+                           gpk_grouper* g, int kind, const gpk_groups* out, void* stream);
+
 /* Pack packets order[0..m) of a batch into a dense batch, in that order:
  * out_data receives their bytes back to back (it must hold their total
  * length), out_offsets[j] / out_caplens[j] index packet order[j]. The send

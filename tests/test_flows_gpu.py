@@ -46,6 +46,15 @@ def check(gpu_ctx, packets, cfg=flowcases.DEFRAG_PARSER, kinds=KINDS):
         assert groups == list(og.values()), kind
         first = out["first"][:len(groups)].cpu().tolist()
         assert first == [v[0] for v in og.values()]
+        if kind in (FO.CONNECTION, FO.DEFRAG):  # the fused path: keys derived in the decode kernel
+            n = len(packets)
+            rec2 = torch.zeros(n * 16, dtype=torch.uint8, device="cuda")
+            fl2 = torch.zeros(3 * n, dtype=torch.int64, device="cuda")
+            out2 = g.decode_group(gpu_ctx, device_parser(cfg), d, o, c, rec2, None, fl2, kind=kind)
+            torch.cuda.synchronize()
+            groups2, group_of2 = flows.Grouper.to_lists(out2)
+            assert group_of2 == oc and groups2 == groups, ("fused", kind)
+            assert torch.equal(rec2, rec) and torch.equal(fl2, fl)
     g.close()
 
 
