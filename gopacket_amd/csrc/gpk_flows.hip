@@ -27,8 +27,8 @@
 
 #include "../../include/gpk_flows.h"
 
-// gpk_host.cpp: gpk_decode_batch with the fused key derivation
-int gpk_decode_batch_keys(gpk_ctx* c, const gpk_parser* p, const gpk_batch* b, const gpk_results* o, int key_kind,
+// gpk_host.cpp: gpk_decode_batch with the fused key derivation (library-internal)
+extern "C" int gpk_decode_batch_keys(gpk_ctx* c, const gpk_parser* p, const gpk_batch* b, const gpk_results* o, int key_kind,
                           uint32_t* keys, uint64_t* khash, int32_t* kcode, void* stream);
 
 namespace {

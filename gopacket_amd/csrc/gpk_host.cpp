@@ -400,7 +400,7 @@ int gpk_decode_batch(gpk_ctx* c, const gpk_parser* p, const gpk_batch* b, const 
 
 // gpk_decode_batch plus the fused grouping key per packet (gpk_flows.hip
 // gpk_decode_group_batch): library-internal, not part of the C ABI.
-__attribute__((visibility("hidden"))) int gpk_decode_batch_keys(gpk_ctx* c, const gpk_parser* p, const gpk_batch* b,
+extern "C" __attribute__((visibility("hidden"))) int gpk_decode_batch_keys(gpk_ctx* c, const gpk_parser* p, const gpk_batch* b,
                                                                 const gpk_results* o, int key_kind, uint32_t* keys,
                                                                 uint64_t* khash, int32_t* kcode, void* stream) {
   if (!o || o->layouts || (key_kind != 1 && key_kind != 2) || (b && b->n && (!keys || !khash || !kcode)))
