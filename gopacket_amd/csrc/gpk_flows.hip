@@ -208,32 +208,45 @@ __global__ void __launch_bounds__(256) insert_kernel(const uint32_t* keys, const
   slot_of[i] = (uint32_t)pos;
 }
 
+// FastHash buckets: each occupied bucket's rank by first appearance, so the
+// sort key needs log2(buckets) bits instead of log2(batch) (one radix pass)
+__global__ void __launch_bounds__(1024) bucket_rank_kernel(const uint32_t* bucket_min, uint32_t B, uint32_t* rank) {
+  for (uint32_t b = threadIdx.x; b < B; b += blockDim.x) {
+    const uint32_t m = bucket_min[b];
+    uint32_t r = 0;
+    for (uint32_t c = 0; c < B; c++) r += bucket_min[c] < m;  // distinct minima: no ties
+    rank[b] = r;
+  }
+}
+
 __global__ void __launch_bounds__(256) first_kernel(const int32_t* code, const uint32_t* slot_of,
                                                     const unsigned long long* table, const uint64_t* hash,
-                                                    const uint32_t* bucket_min, int kind, uint64_t n, uint32_t* f,
-                                                    uint32_t* iota) {
+                                                    const uint32_t* bucket_key, int kind, uint64_t n, uint32_t sentinel,
+                                                    uint32_t* f, uint32_t* iota) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  uint32_t v = (uint32_t)n;  // not keyed: sorts after every group
-  if (!code[i]) v = kind == GPK_GROUP_NET_BUCKET ? bucket_min[hash[i]] : (uint32_t)(table[slot_of[i]] & kIdxMask);
+  uint32_t v = sentinel;  // not keyed: sorts after every group
+  if (!code[i]) v = kind == GPK_GROUP_NET_BUCKET ? bucket_key[hash[i]] : (uint32_t)(table[slot_of[i]] & kIdxMask);
   f[i] = v;
   iota[i] = (uint32_t)i;
 }
 
-__global__ void __launch_bounds__(256) heads_kernel(const uint32_t* fs, uint64_t n, uint32_t* heads) {
+__global__ void __launch_bounds__(256) heads_kernel(const uint32_t* fs, uint64_t n, uint32_t sentinel,
+                                                    uint32_t* heads) {
   const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= n) return;
   const uint32_t v = fs[j];
-  heads[j] = v < n && (j == 0 || fs[j - 1] != v) ? 1u : 0u;
+  heads[j] = v < sentinel && (j == 0 || fs[j - 1] != v) ? 1u : 0u;
 }
 
 __global__ void __launch_bounds__(256) finish_kernel(const uint32_t* fs, const uint32_t* perm, const uint32_t* gid,
-                                                     const int32_t* code, uint64_t n, int32_t* group_of,
-                                                     uint32_t* start, uint32_t* first, uint32_t* counts) {
+                                                     const int32_t* code, uint64_t n, uint32_t sentinel,
+                                                     int32_t* group_of, uint32_t* start, uint32_t* first,
+                                                     uint32_t* counts) {
   const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= n) return;
   const uint32_t v = fs[j], pkt = perm[j];
-  if (v >= n) {
+  if (v >= sentinel) {
     group_of[pkt] = code[pkt];
     return;
   }
@@ -243,7 +256,7 @@ __global__ void __launch_bounds__(256) finish_kernel(const uint32_t* fs, const u
     start[g] = (uint32_t)j;
     first[g] = pkt;
   }
-  if (j + 1 == n || fs[j + 1] >= n) {  // the last keyed packet
+  if (j + 1 == n || fs[j + 1] >= sentinel) {  // the last keyed packet
     counts[0] = g + 1;
     counts[1] = (uint32_t)(j + 1);
     start[g + 1] = (uint32_t)(j + 1);
@@ -311,6 +324,8 @@ struct gpk_grouper {
   uint32_t* slot_of = nullptr;
   unsigned long long* table = nullptr;
   uint32_t* bucket_min = nullptr;
+  uint32_t* brank = nullptr;
+  uint32_t buckets = 0;
   uint32_t* f = nullptr;
   uint32_t* fs = nullptr;
   uint32_t* iota = nullptr;
@@ -330,7 +345,7 @@ int end_bit(uint64_t n) {  // bits to hold 0..n
 
 void free_all(gpk_grouper* g) {
   for (void* p : {(void*)g->keys, (void*)g->hash, (void*)g->code, (void*)g->slot_of, (void*)g->table,
-                  (void*)g->bucket_min, (void*)g->f, (void*)g->fs, (void*)g->iota,
+                  (void*)g->bucket_min, (void*)g->brank, (void*)g->f, (void*)g->fs, (void*)g->iota,
                   (void*)g->heads, (void*)g->gid, g->tmp})
     if (p) (void)hipFree(p);
 }
@@ -362,6 +377,7 @@ extern "C" int gpk_grouper_create(gpk_grouper** out, int device, uint64_t max_pa
        hipMalloc((void**)&g->slot_of, n * 4) == hipSuccess &&
        hipMalloc((void**)&g->table, g->tsize * 8) == hipSuccess &&
        hipMalloc((void**)&g->bucket_min, (1u << 16) * 4) == hipSuccess &&
+       hipMalloc((void**)&g->brank, (1u << 16) * 4) == hipSuccess &&
        hipMalloc((void**)&g->f, n * 4) == hipSuccess && hipMalloc((void**)&g->fs, n * 4) == hipSuccess &&
        hipMalloc((void**)&g->iota, n * 4) == hipSuccess && hipMalloc((void**)&g->heads, n * 4) == hipSuccess &&
        hipMalloc((void**)&g->gid, n * 4) == hipSuccess && hipMalloc(&g->tmp, g->tmp_bytes) == hipSuccess;
@@ -406,6 +422,7 @@ extern "C" int gpk_group_batch(gpk_grouper* g, const gpk_batch* b, const gpk_res
   KeyArgs a{b->data, b->offsets, b->caplens, r->records, r->layouts, r->flows, n, kind, buckets,
             g->keys, g->hash, g->code, g->bucket_min};
   hipLaunchKernelGGL(key_kernel, grd, blk, 0, s, a);
+  g->buckets = buckets;
   return group_rest(g, n, kind, *o, s);
 }
 
@@ -432,16 +449,25 @@ static int group_rest(gpk_grouper* g, uint64_t n, int kind, const gpk_groups& o,
   if (kind != GPK_GROUP_NET_BUCKET)
     hipLaunchKernelGGL(insert_kernel, grd, blk, 0, s, g->keys, g->hash, g->code, n, g->table, g->tsize - 1,
                        g->slot_of);
-  hipLaunchKernelGGL(first_kernel, grd, blk, 0, s, g->code, g->slot_of, g->table, g->hash, g->bucket_min, kind, n,
+  // sort key: the key's first packet index (sentinel n), or for buckets the
+  // bucket's first-appearance rank (sentinel = buckets: a few bits)
+  uint32_t sentinel = (uint32_t)n;
+  const uint32_t* bkey = g->bucket_min;
+  if (kind == GPK_GROUP_NET_BUCKET && g->buckets <= 4096) {
+    hipLaunchKernelGGL(bucket_rank_kernel, dim3(1), dim3(1024), 0, s, g->bucket_min, g->buckets, g->brank);
+    sentinel = g->buckets;
+    bkey = g->brank;
+  }
+  hipLaunchKernelGGL(first_kernel, grd, blk, 0, s, g->code, g->slot_of, g->table, g->hash, bkey, kind, n, sentinel,
                      g->f, g->iota);
   size_t tb = g->tmp_bytes;
-  if (hipcub::DeviceRadixSort::SortPairs(g->tmp, tb, g->f, g->fs, g->iota, o.perm, (int)n, 0, end_bit(n), s) !=
+  if (hipcub::DeviceRadixSort::SortPairs(g->tmp, tb, g->f, g->fs, g->iota, o.perm, (int)n, 0, end_bit(sentinel), s) !=
       hipSuccess)
     return GPK_EHIP;
-  hipLaunchKernelGGL(heads_kernel, grd, blk, 0, s, g->fs, n, g->heads);
+  hipLaunchKernelGGL(heads_kernel, grd, blk, 0, s, g->fs, n, sentinel, g->heads);
   tb = g->tmp_bytes;
   if (hipcub::DeviceScan::InclusiveSum(g->tmp, tb, g->heads, g->gid, (int)n, s) != hipSuccess) return GPK_EHIP;
-  hipLaunchKernelGGL(finish_kernel, grd, blk, 0, s, g->fs, o.perm, g->gid, g->code, n, o.group_of, o.start,
+  hipLaunchKernelGGL(finish_kernel, grd, blk, 0, s, g->fs, o.perm, g->gid, g->code, n, sentinel, o.group_of, o.start,
                      o.first, o.counts);
   return hipGetLastError() == hipSuccess ? GPK_OK : GPK_EHIP;
 }
