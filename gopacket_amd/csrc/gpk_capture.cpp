@@ -1028,6 +1028,11 @@ extern "C" int gpk_capreader_index_all(gpk_capreader* r, const uint8_t* buf, uin
             const uint64_t p = find_sync(snap, r->flags, buf, s0, to, len, base);
             if (p != ~0ull) walk_seg(snap, r->flags, buf, p, s1, len, seg[k]);
           });
+        // meanwhile the exact walk takes the first segment itself (the reader
+        // state it mutates is not the workers' snapshot)
+        st = seq_walk(r, buf, pos, base + span / T, 0, v, &stop);
+        pos = stop;
+        if (st != GPK_CAP_MORE) done = true;
         for (auto& t : th) t.join();
         for (int k = 1; k < T && !done; k++) {
           Seg& s = seg[k];

@@ -325,7 +325,9 @@ extern "C" int gpk_replay_file(gpk_ctx* ctx, const gpk_parser* parser, const cha
     gpk_capindex xi;
     uint64_t used = 0;
     double t_ix = now_s();
-    int st = gpk_capreader_index_all(rd, S.host + start, len, eof ? 1 : 0, opt.read_threads, &xi, &used);
+    // the walk is a dependent load per record: more chains than cores hide DRAM latency
+    const int walk_threads = std::min(64, 4 * opt.read_threads);
+    int st = gpk_capreader_index_all(rd, S.host + start, len, eof ? 1 : 0, walk_threads, &xi, &used);
     stats->index_s += now_s() - t_ix;
     if (st < 0) {
       rc = st;
