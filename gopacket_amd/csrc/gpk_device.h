@@ -65,6 +65,7 @@ struct KParams {
   // fused grouping keys (gpk_decode_group_batch): 0 = off, else GPK_GROUP_CONNECTION /
   // GPK_GROUP_DEFRAG; per packet 10 key words, a 64-bit hash and a reason code
   int32_t key_kind;
+  uint32_t small_headers;   // no Dot1Q / IPv6 / IPv6-extension / TCP decoder: a 4-chunk window suffices
   uint32_t* keys;
   uint64_t* khash;
   int32_t* kcode;

@@ -350,6 +350,12 @@ static int upload(gpk_ctx* c, const gpk_parser* p, hipStream_t s, gpk::KParams& 
   P.cg = c->cg;
   P.first_kind = (p->first >= 0 && p->first < GPK_MAX_LAYER_TYPE) ? p->tab.dispatch[p->first] : GPK_DEC_NONE;
   P.fast = fast_flags(p);
+  // headers that fit the 4-chunk window: no decoder that adds tags, IPv6, extension headers or TCP options
+  P.small_headers = 1;
+  for (int t = 0; t < GPK_MAX_LAYER_TYPE; t++) {
+    const int k = p->tab.dispatch[t];
+    if (k == GPK_DEC_DOT1Q || k == GPK_DEC_IPV6 || k == GPK_DEC_IPV6_EXT || k == GPK_DEC_TCP) P.small_headers = 0;
+  }
   return GPK_OK;
 }
 
@@ -378,6 +384,7 @@ static int make_params(gpk_ctx* c, const gpk_parser* p, const gpk_batch* b, cons
   P.outputs = p->outputs;
   P.ignore_unsupported = p->ignore_unsupported;
   P.key_kind = 0;
+  P.small_headers = 0;
   P.keys = nullptr;
   P.khash = nullptr;
   P.kcode = nullptr;

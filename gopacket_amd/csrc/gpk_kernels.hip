@@ -164,9 +164,16 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
 
 // Header window of one packet in registers: chunks [0, nchunk) of the
 // 16-byte-aligned run holding packet bytes [0, win).
-struct Win {
-  uint4 v[kWinChunks];
+template <int W>
+struct WinT {
+  uint4 v[W];
 };
+using Win = WinT<kWinChunks>;
+// LDS dwords per lane for a window of W chunks (odd: see kSlotDw)
+template <int W>
+constexpr int slot_dw_of() {
+  return W * 4 + (GPK_LINE_OWN ? 3 : 1);
+}
 
 struct Idx {
   uint64_t off;
@@ -182,23 +189,26 @@ __device__ __forceinline__ Idx load_index(const KParams& P, uint64_t i) {
   return x;
 }
 
+template <int W = kWinChunks>
 __device__ __forceinline__ uint32_t win_chunks(const Idx& x, bool active) {
   const uint32_t m = (uint32_t)(x.off & 15);
-  uint32_t win = kWinChunks * 16 - m;
+  uint32_t win = W * 16 - m;
   if (x.cl < win) win = x.cl;
   return active ? (m + win + 15) >> 4 : 0;
 }
 
-__device__ __forceinline__ void load_window(const KParams& P, const Idx& x, uint32_t nchunk, Win& w) {
+template <int W>
+__device__ __forceinline__ void load_window(const KParams& P, const Idx& x, uint32_t nchunk, WinT<W>& w) {
   const uint8_t* src = P.data + (x.off & ~15ull);
 #pragma unroll
-  for (int k = 0; k < kWinChunks; k++)
+  for (int k = 0; k < W; k++)
     if ((uint32_t)k < nchunk) w.v[k] = ld16(src + 16 * k);
 }
 
-__device__ __forceinline__ void store_window(uint32_t slot_dw, uint32_t nchunk, const Win& w) {
+template <int W>
+__device__ __forceinline__ void store_window(uint32_t slot_dw, uint32_t nchunk, const WinT<W>& w) {
 #pragma unroll
-  for (int k = 0; k < kWinChunks; k++)
+  for (int k = 0; k < W; k++)
     if ((uint32_t)k < nchunk) {
       gpk_smem[slot_dw + 4 * k + 0] = w.v[k].x;
       gpk_smem[slot_dw + 4 * k + 1] = w.v[k].y;
@@ -359,11 +369,11 @@ __device__ __forceinline__ int derive_key(const KParams& P, const Rd& r, const P
   return 0;
 }
 
-template <bool kL4, bool kLayout, class TT, bool kKeys = false>
+template <bool kL4, bool kLayout, class TT, bool kKeys = false, int W = kWinChunks>
 __device__ __forceinline__ void decode_packet(const KParams& P, const TT& T, uint64_t i, bool active, uint64_t off,
                                               uint32_t cl, uint32_t slot_dw, uint32_t lane) {
   const uint32_t m = (uint32_t)(off & 15);
-  uint32_t win = kWinChunks * 16 - m;
+  uint32_t win = W * 16 - m;
   if (cl < win) win = cl;
   Rd r{P.data + off, slot_dw * 4 + m, win};
 
@@ -741,8 +751,12 @@ __device__ __forceinline__ void decode_tiles(const KParams& P, const TT& T) {
 // read; otherwise they are read from the global DevTables. Either way the
 // only vector-memory traffic of the decode is the packet bytes themselves,
 // so waiting on a lookup never waits on the next tile's prefetch.
-template <bool kL4, bool kLayout, bool kCompact, bool kKeys = false>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GPK_WAVES_PER_EU, 8))) void decode_kernel(
+// W: header-window chunks. The 5-chunk default holds Ethernet + two tags +
+// IPv6 + TCP; parsers with no Dot1Q/IPv6/TCP decoder and no L4 checksum (C2)
+// run a 4-chunk window whose smaller LDS slot and 64-VGPR budget give 8 waves
+// per SIMD (A/B: C2 -8.6 %, C4 and C3 no gain or worse with 4 chunks).
+template <bool kL4, bool kLayout, bool kCompact, bool kKeys = false, int W = kWinChunks>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W == 4 ? 8 : GPK_WAVES_PER_EU, 8))) void decode_kernel(
     KParams P) {
   if ((uint64_t)blockIdx.x * kBlock * GPK_PPL >= P.n) return;  // uniform over the block
 #if !GPK_PERSISTENT && !GPK_PREFETCH
@@ -751,17 +765,17 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GPK_WAVE
   // registers) and the table blob are in flight together, so the two
   // dependent memory round trips are paid once for GPK_PPL packets.
   const uint32_t tid = threadIdx.x;
-  const uint32_t slot_dw = tid * kSlotDw;
+  const uint32_t slot_dw = tid * slot_dw_of<W>();
   const uint64_t i0 = (uint64_t)blockIdx.x * (kBlock * GPK_PPL) + tid, i1 = i0 + kBlock;
   static_assert(GPK_PPL == 1 || GPK_PPL == 2, "GPK_PPL is 1 or 2");
   const Idx c0 = load_index(P, i0);
   const Idx c1 = GPK_PPL == 2 ? load_index(P, i1) : Idx{0, 0};
-  const uint32_t n0 = win_chunks(c0, i0 < P.n);
-  const uint32_t n1 = GPK_PPL == 2 ? win_chunks(c1, i1 < P.n) : 0;
-  Win w0, w1;
+  const uint32_t n0 = win_chunks<W>(c0, i0 < P.n);
+  const uint32_t n1 = GPK_PPL == 2 ? win_chunks<W>(c1, i1 < P.n) : 0;
+  WinT<W> w0, w1;
   load_window(P, c0, n0, w0);
   if (GPK_PPL == 2) load_window(P, c1, n1, w1);
-  const uint32_t base = kBlock * kSlotDw;
+  const uint32_t base = kBlock * slot_dw_of<W>();
   if (kCompact) {
     for (uint32_t k = tid; k < P.cg.words; k += kBlock) gpk_smem[base + k] = P.ctab[k];
     __syncthreads();
@@ -793,15 +807,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GPK_WAVE
   }
 #endif
   if (kCompact)
-    decode_packet<kL4, kLayout, LTab, kKeys>(P, LTab{P.cg, base}, i0, i0 < P.n, c0.off, c0.cl, slot_dw, tid & 63);
+    decode_packet<kL4, kLayout, LTab, kKeys, W>(P, LTab{P.cg, base}, i0, i0 < P.n, c0.off, c0.cl, slot_dw, tid & 63);
   else
-    decode_packet<kL4, kLayout, GTab, kKeys>(P, GTab{P.tab}, i0, i0 < P.n, c0.off, c0.cl, slot_dw, tid & 63);
+    decode_packet<kL4, kLayout, GTab, kKeys, W>(P, GTab{P.tab}, i0, i0 < P.n, c0.off, c0.cl, slot_dw, tid & 63);
   if (GPK_PPL == 2) {
     store_window(slot_dw, n1, w1);  // lane-private slot, reused
     if (kCompact)
-      decode_packet<kL4, kLayout, LTab, kKeys>(P, LTab{P.cg, base}, i1, i1 < P.n, c1.off, c1.cl, slot_dw, tid & 63);
+      decode_packet<kL4, kLayout, LTab, kKeys, W>(P, LTab{P.cg, base}, i1, i1 < P.n, c1.off, c1.cl, slot_dw, tid & 63);
     else
-      decode_packet<kL4, kLayout, GTab, kKeys>(P, GTab{P.tab}, i1, i1 < P.n, c1.off, c1.cl, slot_dw, tid & 63);
+      decode_packet<kL4, kLayout, GTab, kKeys, W>(P, GTab{P.tab}, i1, i1 < P.n, c1.off, c1.cl, slot_dw, tid & 63);
   }
 #else
   if (kCompact) {
@@ -830,19 +844,21 @@ __global__ void list_kernel(KParams P, uint64_t index, int64_t* out, uint32_t ca
 
 namespace {
 
-template <bool kL4, bool kLayout, bool kCompact, bool kKeys = false>
+template <bool kL4, bool kLayout, bool kCompact, bool kKeys = false, int W = gpk::kWinChunks>
 hipError_t launch(const gpk::KParams* P, hipStream_t stream) {
   using namespace gpk;
-  constexpr int lds = kCompact ? kLdsBytes + kCtDwords * 4 : kLdsBytes;
+  constexpr int slot_lds = kBlock * slot_dw_of<W>() * 4;
+  constexpr int lds = kCompact ? slot_lds + kCtDwords * 4 : slot_lds;
   // Resident blocks per CU for this specialisation (cached per device).
-  static int cached_bpc[64], cached_cus[64];
+  static int cached_bpc[64], cached_cus[64];  // per instantiation
   int dev = 0;
   hipError_t e = hipGetDevice(&dev);
   if (e != hipSuccess) return e;
   if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
   if (!cached_bpc[dev]) {
     int bpc = 0, cus = 0;
-    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, decode_kernel<kL4, kLayout, kCompact, kKeys>, kBlock, lds);
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, decode_kernel<kL4, kLayout, kCompact, kKeys, W>, kBlock,
+                                                     lds);
     if (e != hipSuccess) return e;
     e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     if (e != hipSuccess) return e;
@@ -857,8 +873,8 @@ hipError_t launch(const gpk::KParams* P, hipStream_t stream) {
   if (ntiles < grid * 8) grid = (ntiles + 7) / 8;
   if (!GPK_PERSISTENT && !GPK_PREFETCH) grid = (ntiles + GPK_PPL - 1) / GPK_PPL;
   if (grid < 1) grid = 1;
-  hipLaunchKernelGGL((decode_kernel<kL4, kLayout, kCompact, kKeys>), dim3((unsigned)grid), dim3(kBlock), lds, stream,
-                     *P);
+  hipLaunchKernelGGL((decode_kernel<kL4, kLayout, kCompact, kKeys, W>), dim3((unsigned)grid), dim3(kBlock), lds,
+                     stream, *P);
   return hipGetLastError();
 }
 
@@ -868,6 +884,7 @@ hipError_t launch_outputs(const gpk::KParams* P, int with_l4, int with_layout, h
     if (with_layout) return hipErrorInvalidValue;
     return with_l4 ? launch<true, false, kCompact, true>(P, stream) : launch<false, false, kCompact, true>(P, stream);
   }
+  if (!with_l4 && !with_layout && P->small_headers) return launch<false, false, kCompact, false, 4>(P, stream);
   if (with_l4 && with_layout) return launch<true, true, kCompact>(P, stream);
   if (with_l4) return launch<true, false, kCompact>(P, stream);
   if (with_layout) return launch<false, true, kCompact>(P, stream);
