@@ -95,3 +95,33 @@ def test_pump_frame_rings(gpu_ctx, version):
                              afpacket.OptBlockSize(8192), afpacket.OptNumBlocks(16), afpacket.OptAddVLANHeader(True))
     check(gpu_ctx, tp, pk, exp, batch_pkts=7, inflight=2)
     tp.Close()
+
+
+def test_pump_stops_at_a_corrupt_chain_and_at_max_packets(gpu_ctx):
+    """A block whose chain leaves the ring ends the walk with the fault error
+    after the packets before it were delivered; max_packets stops early."""
+    import struct
+    pk = [synth.packet(synth.C4_IMIX, i) for i in range(30)]
+    blocks = [dict(status=1, pkts=[dict(data=p) for p in pk[:10]]),
+              dict(status=1, pkts=[dict(data=p) for p in pk[10:20]]),
+              dict(status=1, pkts=[dict(data=pk[20], next=1 << 24), dict(data=pk[21])])]
+    ring = np.frombuffer(ringgen.v3_ring(blocks, 8192, 4), np.uint8).copy()
+    opts = dict(frame_size=4096, block_size=8192, num_blocks=4)
+    exp_pk, exp = expect(ring.tobytes(), AO.V3, opts)
+    assert len(exp_pk) == 21  # 10 + 10 + the first packet of block 2, then the fault
+    tp = afpacket.AttachRing(ring, afpacket.TPacketVersion3, afpacket.OptFrameSize(4096),
+                             afpacket.OptBlockSize(8192), afpacket.OptNumBlocks(4))
+    got, st = tp.Pump(gpu_ctx, device_parser(CONFIGS["statsassembly"]), batch_pkts=8, inflight=2)
+    assert st["packets"] == 21 and st["status"] == _lib.TP_ERROR and "unexpected fault address" in st["error"]
+    data, off, cap = pktutil.pack(exp_pk)
+    ref = oracle_parser(CONFIGS["statsassembly"]).decode(data, off, cap, layouts=False)
+    assert_same(got, ref, "pump before fault")
+    tp.Close()
+    ring2 = np.frombuffer(ringgen.v3_ring(blocks[:2], 8192, 4), np.uint8).copy()
+    tp = afpacket.AttachRing(ring2, afpacket.TPacketVersion3, afpacket.OptFrameSize(4096),
+                             afpacket.OptBlockSize(8192), afpacket.OptNumBlocks(4))
+    got, st = tp.Pump(gpu_ctx, device_parser(CONFIGS["statsassembly"]), batch_pkts=4, max_packets=13)
+    assert st["packets"] == 13 and np.array_equal(got["caplens"], [len(p) for p in pk[:13]])
+    # block 0 was finished and handed back; block 1 is still current, so still the reader's
+    assert struct.unpack_from("<I", ring2, 8)[0] == 0
+    tp.Close()
