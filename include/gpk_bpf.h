@@ -51,7 +51,9 @@ int gpk_bpf_destroy(gpk_bpf* f);
 int gpk_bpf_run(gpk_bpf* f, const gpk_batch* batch, const uint32_t* wirelens, uint32_t* ret, void* stream);
 
 /* The matching packets, in batch order: out_offsets/out_caplens/out_index
- * [n] (device), *out_count (device u32). Async on stream. */
+ * [n] (device), *out_count (device u32). Async on stream. The filter keeps
+ * scratch for this call: use one filter from one stream at a time (one
+ * filter per goroutine/thread, as a pcap handle is). */
 int gpk_bpf_select(gpk_bpf* f, const gpk_batch* batch, const uint32_t* wirelens, uint64_t* out_offsets,
                    uint32_t* out_caplens, uint32_t* out_index, uint32_t* out_count, void* stream);
 

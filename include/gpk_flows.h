@@ -58,7 +58,9 @@ extern "C" {
 
 typedef struct gpk_grouper gpk_grouper;
 
-/* Workspace for batches of up to max_packets (< 2^28) on one device. */
+/* Workspace for batches of up to max_packets (< 2^28) on one device. A
+ * grouper's workspace serves one call at a time: calls on one stream are
+ * ordered; concurrent streams need one grouper each. */
 int gpk_grouper_create(gpk_grouper** out, int device, uint64_t max_packets);
 int gpk_grouper_destroy(gpk_grouper* g);
 
