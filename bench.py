@@ -29,6 +29,11 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 INDEX_BYTES = 12       # u64 offset + u32 caplen per packet
 
 CONFIGS = {
+    # BASELINE configs[0]: the reference's CPU-runnable case, pcap/test_ethernet.pcap's 10
+    # packets replayed 10^6 times (benchmark.go -repeat), as decode_test.go:192's parser
+    "c1": dict(pcap="tests/golden/test_ethernet.pcap", packets=10_000_000,
+               decoders=("Ethernet", "IPv4", "TCP", "Payload"), outputs=3,
+               workload="C1: test_ethernet.pcap (10 packets) replayed 1e6 times, Eth/IPv4/TCP decode + IPv4/TCP checksums"),
     "c3": dict(synth=3, decoders=("Ethernet", "IPv4", "TCP", "Payload"), outputs=7,
                workload="C3: 64M x 1500B Eth/IPv4/TCP, IPv4+TCP checksum, link/net/transport FastHash"),
     "c2": dict(synth=2, decoders=("Ethernet", "IPv4", "UDP", "Payload"), outputs=1,
@@ -91,9 +96,14 @@ def run_config(name, n, steps, warmup, rank, world, ctx, check_sample=2048, prob
     cfg = CONFIGS[name]
     kinds = [engine.DECODER_KINDS[d] for d in cfg["decoders"]]
     parser = engine.ParserConfig(17, kinds, outputs=cfg["outputs"])
+    if "pcap" in cfg:
+        n = cfg["packets"]
     first, n = shard.weak_range(rank, n)
     stream = torch.cuda.current_stream()
-    data, off, cap = synth.device_batch(cfg["synth"], first, n, stream=stream)
+    if "pcap" in cfg:
+        data, off, cap = pcap_tiled(cfg["pcap"], n)
+    else:
+        data, off, cap = synth.device_batch(cfg["synth"], first, n, stream=stream)
     rec = torch.empty(n * 16, dtype=torch.uint8, device="cuda")
     err = torch.zeros(2 * n, dtype=torch.int32, device="cuda")
     fl = torch.empty(3 * n, dtype=torch.int64, device="cuda") if cfg["outputs"] & 4 else None
@@ -128,13 +138,48 @@ def run_config(name, n, steps, warmup, rank, world, ctx, check_sample=2048, prob
     return res
 
 
+def pcap_packets(path):
+    """The packets of a classic little-endian pcap file (bench input, not the reader under test)."""
+    import struct
+    raw = open(os.path.join(ROOT, path), "rb").read()
+    pos, out = 24, []
+    while pos + 16 <= len(raw):
+        caplen = struct.unpack_from("<I", raw, pos + 8)[0]
+        out.append(raw[pos + 16:pos + 16 + caplen])
+        pos += 16 + caplen
+    return out
+
+
+def pcap_tiled(path, n):
+    """Device batch of n packets: the file's packets repeated in order."""
+    import torch
+    pk = pcap_packets(path)
+    one = np.frombuffer(b"".join(pk), np.uint8)
+    caps = np.array([len(p) for p in pk], np.int64)
+    reps = (n + len(pk) - 1) // len(pk)
+    cap = np.tile(caps, reps)[:n]
+    off = np.concatenate([[0], np.cumsum(cap[:-1])])
+    data = np.zeros(int(cap.sum()) + 256, np.uint8)
+    data[:len(one) * (n // len(pk))] = np.tile(one, n // len(pk))
+    rest = n % len(pk)
+    if rest:
+        tail = np.frombuffer(b"".join(pk[:rest]), np.uint8)
+        data[len(one) * (n // len(pk)):len(one) * (n // len(pk)) + len(tail)] = tail
+    return (torch.from_numpy(data).cuda(), torch.from_numpy(off).cuda(),
+            torch.from_numpy(cap.astype(np.int32)).cuda())
+
+
 def sample_parity(name, cfg, rec, fl, err, first, n, k):
     """Check k sampled packets of the device result against the CPU oracle."""
     from gopacket_amd import _lib, synth
     from oracle import oracle as O
     rng = np.random.default_rng(first + 17)
     idx = np.unique(np.concatenate([rng.integers(0, n, k), [0, n - 1]]))
-    pk = [synth.packet(cfg["synth"], first + int(i)) for i in idx]
+    if "pcap" in cfg:
+        src = pcap_packets(cfg["pcap"])
+        pk = [src[int(i) % len(src)] for i in idx]
+    else:
+        pk = [synth.packet(cfg["synth"], first + int(i)) for i in idx]
     cap = np.array([len(x) for x in pk], np.uint32)
     off = np.concatenate([[0], np.cumsum(cap[:-1], dtype=np.uint64)]).astype(np.uint64)
     data = np.frombuffer(b"".join(pk) + bytes(16), np.uint8)
@@ -523,7 +568,7 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--packets", type=int, default=64 * 2**20, help="packets per GPU")
-    ap.add_argument("--configs", default="c3,c2,c4", help="first one is the headline")
+    ap.add_argument("--configs", default="c3,c2,c4,c1", help="first one is the headline")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
