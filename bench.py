@@ -209,17 +209,25 @@ def cpu_baseline(name, seconds=12.0, batch=262144):
             "IPv6ExtensionSkipper": "IPV6_EXT", "TCP": "TCP", "UDP": "UDP", "Payload": "PAYLOAD"}[d]
            for d in cfg["decoders"]]
     p = O.OracleParser(17, dec, outputs=cfg["outputs"])
-    reps, t0 = 0, time.perf_counter()
-    while True:
-        p.decode(data, off, cap, nthreads=cores, layouts=False)
-        reps += 1
-        el = time.perf_counter() - t0
-        if el >= seconds:
-            break
-    pkts = reps * batch
-    return dict(value=pkts / el / 1e6, unit="Mpkts/s", cores=cores, kind="port",
-                sample="%d x %d-packet %s batch (%.1f MB) replayed, %.1f s, oracle/gpk_oracle.c at %d threads"
-                       % (reps, batch, name.upper(), len(data) / 1e6, el, cores))
+
+    def timed(threads, secs, nb):
+        reps, t0 = 0, time.perf_counter()
+        while True:
+            p.decode(data[:int(off[nb - 1]) + int(cap[nb - 1]) + 16], off[:nb], cap[:nb], nthreads=threads,
+                     layouts=False)
+            reps += 1
+            el = time.perf_counter() - t0
+            if el >= secs:
+                return reps, el
+
+    reps, el = timed(cores, seconds, batch)
+    # single-thread beside the nproc-thread figure (a quarter of the time, 1/16 of the batch)
+    reps1, el1 = timed(1, seconds / 4, batch // 16)
+    return dict(value=reps * batch / el / 1e6, unit="Mpkts/s", cores=cores, kind="port",
+                single_thread=round(reps1 * (batch // 16) / el1 / 1e6, 3),
+                sample="%d x %d-packet %s batch (%.1f MB) replayed, %.1f s, oracle/gpk_oracle.c at %d threads; "
+                       "single_thread: %d x %d packets, %.1f s, 1 thread"
+                       % (reps, batch, name.upper(), len(data) / 1e6, el, cores, reps1, batch // 16, el1))
 
 
 def pcie_inclusive(name, ctx, n=4 * 2**20, reps=5):

@@ -372,6 +372,7 @@ static int make_params(gpk_ctx* c, const gpk_parser* p, const gpk_batch* b, cons
   P.offsets = b->offsets;
   P.caplens = b->caplens;
   P.n = b->n;
+  P.big_packets = b->n && b->data_bytes / b->n >= 1024;
   P.records = o ? o->records : nullptr;
   P.err_args = o ? o->err_args : nullptr;
   P.flows = o && (p->outputs & GPK_OUT_FLOWS) ? o->flows : nullptr;

@@ -33,6 +33,12 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 #ifndef GPK_WAVES_PER_EU
 #define GPK_WAVES_PER_EU 6  // <= 80 VGPRs: 6 waves/SIMD, matching the 6 blocks per CU the LDS allows
 #endif
+#ifndef GPK_LDS_FIT
+#define GPK_LDS_FIT 1  // dynamic LDS sized to the parser's table blob (7 blocks/CU at 5 chunks)
+#endif
+#ifndef GPK_W4_WAVES
+#define GPK_W4_WAVES 8  // 4-chunk window kernel: 64 VGPRs
+#endif
 #ifndef GPK_PB_G
 #define GPK_PB_G 4  // phase B: pending packets per wave pass
 #endif
@@ -755,8 +761,12 @@ __device__ __forceinline__ void decode_tiles(const KParams& P, const TT& T) {
 // IPv6 + TCP; parsers with no Dot1Q/IPv6/TCP decoder and no L4 checksum (C2)
 // run a 4-chunk window whose smaller LDS slot and 64-VGPR budget give 8 waves
 // per SIMD (A/B: C2 -8.6 %, C4 and C3 no gain or worse with 4 chunks).
-template <bool kL4, bool kLayout, bool kCompact, bool kKeys = false, int W = kWinChunks>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W == 4 ? 8 : GPK_WAVES_PER_EU, 8))) void decode_kernel(
+// O: waves per SIMD the register budget is cut for. Batches of small packets
+// (mean < 1 KiB) are issue-bound in the header phase and run O = 7 (72 VGPRs;
+// with the table blob sized to the parser, 7 blocks fit a CU's LDS); big
+// packets keep O = 6 (A/B r02c: C4 -5.9 %, C1 -4.9 %, C3 +0.5 % at 7).
+template <bool kL4, bool kLayout, bool kCompact, bool kKeys = false, int W = kWinChunks, int O = GPK_WAVES_PER_EU>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W == 4 ? GPK_W4_WAVES : O, 8))) void decode_kernel(
     KParams P) {
   if ((uint64_t)blockIdx.x * kBlock * GPK_PPL >= P.n) return;  // uniform over the block
 #if !GPK_PERSISTENT && !GPK_PREFETCH
@@ -844,11 +854,17 @@ __global__ void list_kernel(KParams P, uint64_t index, int64_t* out, uint32_t ca
 
 namespace {
 
-template <bool kL4, bool kLayout, bool kCompact, bool kKeys = false, int W = gpk::kWinChunks>
+template <bool kL4, bool kLayout, bool kCompact, bool kKeys = false, int W = gpk::kWinChunks,
+          int O = GPK_WAVES_PER_EU>
 hipError_t launch(const gpk::KParams* P, hipStream_t stream) {
   using namespace gpk;
   constexpr int slot_lds = kBlock * slot_dw_of<W>() * 4;
+#if GPK_LDS_FIT
+  // the table blob takes only the words this parser's tables use (C3/C4: ~1.5 KB of 2.9)
+  const int lds = kCompact ? slot_lds + (int)((P->cg.words + 127) & ~127u) * 4 : slot_lds;
+#else
   constexpr int lds = kCompact ? slot_lds + kCtDwords * 4 : slot_lds;
+#endif
   // Resident blocks per CU for this specialisation (cached per device).
   static int cached_bpc[64], cached_cus[64];  // per instantiation
   int dev = 0;
@@ -857,7 +873,7 @@ hipError_t launch(const gpk::KParams* P, hipStream_t stream) {
   if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
   if (!cached_bpc[dev]) {
     int bpc = 0, cus = 0;
-    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, decode_kernel<kL4, kLayout, kCompact, kKeys, W>, kBlock,
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, decode_kernel<kL4, kLayout, kCompact, kKeys, W, O>, kBlock,
                                                      lds);
     if (e != hipSuccess) return e;
     e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
@@ -873,7 +889,7 @@ hipError_t launch(const gpk::KParams* P, hipStream_t stream) {
   if (ntiles < grid * 8) grid = (ntiles + 7) / 8;
   if (!GPK_PERSISTENT && !GPK_PREFETCH) grid = (ntiles + GPK_PPL - 1) / GPK_PPL;
   if (grid < 1) grid = 1;
-  hipLaunchKernelGGL((decode_kernel<kL4, kLayout, kCompact, kKeys, W>), dim3((unsigned)grid), dim3(kBlock), lds,
+  hipLaunchKernelGGL((decode_kernel<kL4, kLayout, kCompact, kKeys, W, O>), dim3((unsigned)grid), dim3(kBlock), lds,
                      stream, *P);
   return hipGetLastError();
 }
@@ -885,8 +901,11 @@ hipError_t launch_outputs(const gpk::KParams* P, int with_l4, int with_layout, h
     return with_l4 ? launch<true, false, kCompact, true>(P, stream) : launch<false, false, kCompact, true>(P, stream);
   }
   if (!with_l4 && !with_layout && P->small_headers) return launch<false, false, kCompact, false, 4>(P, stream);
+  constexpr int W = gpk::kWinChunks;
   if (with_l4 && with_layout) return launch<true, true, kCompact>(P, stream);
-  if (with_l4) return launch<true, false, kCompact>(P, stream);
+  if (with_l4)
+    return P->big_packets ? launch<true, false, kCompact>(P, stream) : launch<true, false, kCompact, false, W, 7>(P, stream);
+  if (!with_layout && !P->big_packets) return launch<false, false, kCompact, false, W, 7>(P, stream);
   if (with_layout) return launch<false, true, kCompact>(P, stream);
   return launch<false, false, kCompact>(P, stream);
 }

@@ -48,8 +48,11 @@ def main():
     stream = torch.cuda.current_stream()
     for name in a.configs.split(","):
         cfg = bench.CONFIGS[name]
-        n = a.packets
-        data, off, cap = synth.device_batch(cfg["synth"], 0, n, stream=stream)
+        n = cfg.get("packets", a.packets)
+        if "pcap" in cfg:
+            data, off, cap = bench.pcap_tiled(cfg["pcap"], n)
+        else:
+            data, off, cap = synth.device_batch(cfg["synth"], 0, n, stream=stream)
         rec = torch.empty(n * 16, dtype=torch.uint8, device="cuda")
         err = torch.zeros(2 * n, dtype=torch.int32, device="cuda")
         fl = torch.empty(3 * n, dtype=torch.int64, device="cuda")
