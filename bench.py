@@ -623,7 +623,7 @@ def main():
                        "parser": "+".join(CONFIGS[head]["decoders"])},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": load_traffic(head, r["n"]),
-                         "kernel": "gpk::decode_kernel<true,false,true,false>", "traffic_unit": "bytes per launch", "kernel_ms": round(r["kernel_ms"], 4),
+                         "kernel": "gpk::decode_kernel<true,false,true,false,5,6>", "traffic_unit": "bytes per launch", "kernel_ms": round(r["kernel_ms"], 4),
                          "algo_bytes_per_launch": r["algo_bytes"],
                          "probe_read_GBps": r["probe_gbs"] and round(r["probe_gbs"], 1)},
             "parity": r["parity"],
