@@ -45,17 +45,31 @@ CONFIGS = {
                                   "Payload"), outputs=7,
                workload="C4: 64M IMIX 64/594/1518 7:4:1, 40% Dot1Q/QinQ, 20% IPv6, all checksums + hashes"),
 }
+# diagnostics (not bench lines): C4 / C1 with subsets of the outputs (1 IPv4 checksum, 2 L4
+# checksum, 4 flow hashes), to split the kernel time between the parse and each output
+for _o in (1, 3, 5):
+    CONFIGS["c4x%d" % _o] = dict(CONFIGS["c4"], outputs=_o, workload="C4 packets, outputs %d (diagnostic)" % _o)
+CONFIGS["c1x1"] = dict(CONFIGS["c1"], outputs=1, workload="C1 packets, IPv4 checksum only (diagnostic)")
+# BASELINE configs[3] as written: ONE 64M IMIX batch split across the ranks at byte-balanced
+# cuts (shard.byte_balanced_bounds; strong scaling, run by default when world > 1)
+CONFIGS["c4s"] = dict(CONFIGS["c4"], strong=True,
+                      workload="C4 strong: one 64M IMIX batch sharded over the ranks (byte-balanced cuts)")
 
 
-def dist_init():
+def dist_init(backend="nccl", same_device=False):
+    """One process per GPU (torchrun env). backend "nccl" is RCCL on ROCm;
+    "gloo" + same_device=True rehearses N ranks on one GPU (tests only)."""
     import torch
     import torch.distributed as dist
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = 0 if same_device else int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     return rank, world, local
 
 
@@ -98,7 +112,21 @@ def run_config(name, n, steps, warmup, rank, world, ctx, check_sample=2048, prob
     parser = engine.ParserConfig(17, kinds, outputs=cfg["outputs"])
     if "pcap" in cfg:
         n = cfg["packets"]
-    first, n = shard.weak_range(rank, n)
+    strong = None
+    if cfg.get("strong"):
+        # every rank computes the same cuts from the batch's capture lengths
+        # (deterministic per packet index) and generates only its own range
+        caps = np.zeros(n, np.uint32)
+        from gopacket_amd import _lib
+        _lib.synth_lib().gpk_synth_batch_host(cfg["synth"], 0, n, None, None, caps.ctypes.data)
+        cuts = shard.byte_balanced_bounds(caps, world)
+        per = [int(caps[cuts[k]:cuts[k + 1]].sum(dtype=np.uint64)) for k in range(world)]
+        strong = dict(total_packets=n, cuts=cuts, bytes_per_rank=per,
+                      balance=round(max(per) / (sum(per) / world), 6))
+        first, n = cuts[rank], cuts[rank + 1] - cuts[rank]
+        del caps
+    else:
+        first, n = shard.weak_range(rank, n)
     stream = torch.cuda.current_stream()
     if "pcap" in cfg:
         data, off, cap = pcap_tiled(cfg["pcap"], n)
@@ -108,6 +136,7 @@ def run_config(name, n, steps, warmup, rank, world, ctx, check_sample=2048, prob
     err = torch.zeros(2 * n, dtype=torch.int32, device="cuda")
     fl = torch.empty(3 * n, dtype=torch.int64, device="cuda") if cfg["outputs"] & 4 else None
     payload_bytes = int(cap.sum(dtype=torch.int64).item())
+    kernel = ctx.kernel_name(parser, data, off, cap)
     torch.cuda.synchronize()
 
     def step():
@@ -132,7 +161,8 @@ def run_config(name, n, steps, warmup, rank, world, ctx, check_sample=2048, prob
     if check_sample:
         parity = sample_parity(name, cfg, rec, fl, err, first, n, check_sample)
     res = dict(n=n, payload_bytes=payload_bytes, wall_s=wall_max, kernel_ms=kernel_ms,
-               algo_bytes=payload_bytes + INDEX_BYTES * n, parity=parity, probe_gbs=probe_gbs)
+               algo_bytes=payload_bytes + INDEX_BYTES * n, parity=parity, probe_gbs=probe_gbs, strong=strong,
+               kernel=kernel)
     del data, off, cap, rec, err, fl
     torch.cuda.empty_cache()
     return res
@@ -197,37 +227,92 @@ def sample_parity(name, cfg, rec, fl, err, first, n, k):
     return "%s (%d sampled packets vs oracle)" % ("bit-exact" if ok else "MISMATCH", len(idx))
 
 
-def cpu_baseline(name, seconds=12.0, batch=262144):
-    """The oracle (CPU restatement, oracle/) on the host cores over a bounded
-    sample of the same synthetic workload, replayed until ~`seconds` elapse."""
+def host_cores():
+    """(threads used, nproc, CPU share, CPU model). The GPU box gives a
+    process a share of the host (its affinity mask / OMP_NUM_THREADS, 16 cores
+    per GPU on the driver's boxes) while nproc counts the whole machine; the
+    parallel CPU baseline runs one thread per core of the share."""
+    share = len(os.sched_getaffinity(0))
+    nproc = os.cpu_count() or share
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    threads = min(share, int(omp)) if omp.isdigit() and int(omp) > 0 else share
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return threads, nproc, share, model
+
+
+def host_sample(name, batch):
+    """A packed host batch of the config's first `batch` packets (synthetic
+    generator, or the pcap's packets tiled), as the CPU baseline's input."""
     from gopacket_amd import synth
+    cfg = CONFIGS[name]
+    if "synth" in cfg:
+        return synth.host_batch(cfg["synth"], 0, batch)
+    pk = pcap_packets(cfg["pcap"])
+    one = b"".join(pk)
+    reps = batch // len(pk)
+    cap = np.tile(np.array([len(p) for p in pk], np.uint32), reps)
+    off = np.concatenate([[0], np.cumsum(cap[:-1], dtype=np.uint64)]).astype(np.uint64)
+    return np.frombuffer(one * reps + bytes(16), np.uint8), off, cap
+
+
+def oracle_rate(name, data, off, cap, threads, secs):
+    """The oracle (CPU restatement, oracle/) over a host batch, replayed until
+    `secs` elapse: (Mpkts/s, replays, seconds)."""
     from oracle import oracle as O
     cfg = CONFIGS[name]
-    cores = min(16, len(os.sched_getaffinity(0)))
-    data, off, cap = synth.host_batch(cfg["synth"], 0, batch)
     dec = [{"Ethernet": "ETHERNET", "Dot1Q": "DOT1Q", "IPv4": "IPV4", "IPv6": "IPV6",
             "IPv6ExtensionSkipper": "IPV6_EXT", "TCP": "TCP", "UDP": "UDP", "Payload": "PAYLOAD"}[d]
            for d in cfg["decoders"]]
     p = O.OracleParser(17, dec, outputs=cfg["outputs"])
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        p.decode(data, off, cap, nthreads=threads, layouts=False)
+        reps += 1
+        el = time.perf_counter() - t0
+        if el >= secs:
+            return len(off) * reps / el / 1e6, reps, el
 
-    def timed(threads, secs, nb):
-        reps, t0 = 0, time.perf_counter()
-        while True:
-            p.decode(data[:int(off[nb - 1]) + int(cap[nb - 1]) + 16], off[:nb], cap[:nb], nthreads=threads,
-                     layouts=False)
-            reps += 1
-            el = time.perf_counter() - t0
-            if el >= secs:
-                return reps, el
 
-    reps, el = timed(cores, seconds, batch)
-    # SURVEY.md §8(d): single-thread beside the nproc-thread figure (a quarter of the time, 1/16 of the batch)
-    reps1, el1 = timed(1, seconds / 4, batch // 16)
-    return dict(value=reps * batch / el / 1e6, unit="Mpkts/s", cores=cores, kind="port",
-                single_thread=round(reps1 * (batch // 16) / el1 / 1e6, 3),
-                sample="%d x %d-packet %s batch (%.1f MB) replayed, %.1f s, oracle/gpk_oracle.c at %d threads; "
-                       "single_thread: %d x %d packets, %.1f s, 1 thread"
-                       % (reps, batch, name.upper(), len(data) / 1e6, el, cores, reps1, batch // 16, el1))
+def cpu_baseline(head, names, seconds=12.0, batch=262144):
+    """the reference's CPU path timed on this box's host
+    cores. Go is absent here, so the oracle (oracle/gpk_oracle.c, a bit-exact
+    C restatement of the path) stands in ("kind": "port"), one decoder per
+    thread over contiguous shards. Bounded samples of each config's workload,
+    single-thread and one thread per core of the CPU share. The headline
+    config gets `seconds` at full width + a quarter of it single-threaded;
+    every other config a quarter and an eighth."""
+    threads, nproc, share, model = host_cores()
+    out = dict(unit="Mpkts/s", cores=threads, kind="port", nproc=nproc, cpu_share=share, cpu_model=model,
+               configs={})
+    for name in [head] + [x for x in names if x != head]:
+        cfg = CONFIGS[name]
+        if cfg.get("strong") or name in ("c3h",) or "x" in name[2:]:
+            continue
+        full = name == head
+        data, off, cap = host_sample(name, batch)
+        rT, reps, el = oracle_rate(name, data, off, cap, threads, seconds if full else seconds / 4)
+        m = batch // 16
+        d1 = data[:int(off[m - 1]) + int(cap[m - 1]) + 16]
+        r1, reps1, el1 = oracle_rate(name, d1, off[:m], cap[:m], 1, seconds / 4 if full else seconds / 8)
+        mean = float(cap.mean()) + INDEX_BYTES
+        row = dict(value=round(rT, 3), threads=threads, single_thread=round(r1, 3),
+                   GBps=round(rT * mean / 1e3, 3), single_thread_GBps=round(r1 * mean / 1e3, 3),
+                   sample="%d x %d-packet %s sample (%.1f MB) replayed for %.1f s at %d threads; %d x %d packets "
+                          "for %.1f s on 1 thread" % (reps, batch, name.upper(), len(data) / 1e6, el, threads,
+                                                      reps1, m, el1))
+        out["configs"][name] = row
+    h = out["configs"][head]
+    out.update(value=h["value"], single_thread=h["single_thread"],
+               sample="headline %s: %s; oracle/gpk_oracle.c, Go absent on the box (configs: every BASELINE "
+                      "config, same method)" % (head.upper(), h["sample"]))
+    return out
 
 
 def pcie_inclusive(name, ctx, n=4 * 2**20, reps=5):
@@ -265,7 +350,47 @@ def pcie_inclusive(name, ctx, n=4 * 2**20, reps=5):
                 packets=n, note="gpk_decode_batch_host from pinned memory: HtoD + decode + DtoH")
 
 
-def c5_replay(ctx, gib=10.0, reps=2, threads=16):
+def c5_cpu(path, threads, nbytes=256 << 20):
+    """C5's CPU baseline: NgReader semantics + DecodeLayers
+    on the host, over the file's first `nbytes` (a bounded sample, page
+    cached): the record walk (gpk_capreader_index_all, the C++ restatement of
+    ngread.go:494-718) alone, and walk + the oracle's decode, at 1 thread and
+    one per core of the CPU share."""
+    import ctypes
+    from gopacket_amd import _lib
+    from oracle import oracle as O
+    L = _lib.lib()
+    with open(path, "rb") as f:
+        buf = np.frombuffer(f.read(nbytes), np.uint8)
+    dec = ["ETHERNET", "DOT1Q", "IPV4", "IPV6", "IPV6_EXT", "TCP", "UDP", "PAYLOAD"]
+    out = {}
+    for t in (1, threads):
+        walk = []
+        for _ in range(3):
+            h = ctypes.c_void_p()
+            _lib.check(L.gpk_capreader_create(ctypes.byref(h), 1, 0))
+            x, used = _lib.CapIndex(), ctypes.c_uint64()
+            t0 = time.perf_counter()
+            L.gpk_capreader_index_all(h, buf.ctypes.data, len(buf), 0, t, ctypes.byref(x), ctypes.byref(used))
+            walk.append(time.perf_counter() - t0)
+            n = x.n
+            off = np.ctypeslib.as_array(ctypes.cast(x.offsets, ctypes.POINTER(ctypes.c_uint64)), (n,)).copy()
+            cap = np.ctypeslib.as_array(ctypes.cast(x.caplens, ctypes.POINTER(ctypes.c_uint32)), (n,)).copy()
+            L.gpk_capindex_free(ctypes.byref(x))
+            L.gpk_capreader_destroy(h)
+        w = min(walk)
+        p = O.OracleParser(17, dec)
+        t0 = time.perf_counter()
+        p.decode(buf, off, cap, nthreads=t, layouts=False)
+        d = time.perf_counter() - t0
+        out["threads_%d" % t] = dict(walk_Mpkts_s=round(n / w / 1e6, 2), walk_decode_Mpkts_s=round(n / (w + d) / 1e6, 2),
+                                     walk_decode_GBps=round(len(buf) / (w + d) / 1e9, 3))
+    out["sample"] = "first %d MiB of the C5 file (%d packets), page cached; walk = gpk_capreader_index_all, " \
+                    "decode = oracle/gpk_oracle.c" % (nbytes >> 20, n)
+    return out
+
+
+def c5_replay(ctx, gib=10.0, reps=2, threads=16, cpu_threads=16):
     """BASELINE config C5: a pcapng of the C4 IMIX mix (~gib GiB, written once
     to $TMPDIR, in the page cache) replayed end to end by gpk_replay_file:
     file -> pinned staging slots -> record walk -> HtoD -> decode -> DtoH ->
@@ -297,12 +422,14 @@ def c5_replay(ctx, gib=10.0, reps=2, threads=16):
             picked[i] = (rec[j].copy(), fl[[j, k + j, 2 * k + j]].copy())
 
     runs = []
+    cpu = None
     try:
         for _ in range(reps):
             picked.clear()
             valid[0] = 0
             _, st = ctx.replay_file(parser, path, collect=False, on_batch=on_batch, read_threads=threads)
             runs.append(st)
+        cpu = c5_cpu(path, cpu_threads)
     finally:
         os.unlink(path)
     st = min(runs, key=lambda x: x["wall_s"])
@@ -326,7 +453,7 @@ def c5_replay(ctx, gib=10.0, reps=2, threads=16):
                                  deliver=round(st["deliver_s"], 4)),
                 batches=st["batches"], slots=st["slots"], l4_valid=valid[0], write_s=round(gen_s, 2),
                 parity="%s (%d sampled packets vs oracle)" % ("bit-exact" if ok else "MISMATCH", len(idx)),
-                source="page-cached file in %s" % os.path.dirname(path))
+                source="page-cached file in %s" % os.path.dirname(path), cpu_baseline=cpu)
 
 
 def afpacket_pump(ctx, packets=16 * 2**20, block_mib=4, blocks=64, reps=2, batch=1 << 18):
@@ -561,13 +688,15 @@ def bpf_filter_bench(ctx, n=64 * 2**20, reps=10):
 def load_traffic(name, n):
     """HBM bytes per launch of the decode kernel from the committed PMC
     profile (profiles/hbm_traffic.json, tools/make_profiles.py): measured
-    bytes per packet x packets per launch. None if not profiled."""
+    bytes per packet x packets per launch, and the profile's tag. (None,
+    None) if not profiled."""
     path = os.path.join(ROOT, "profiles", "hbm_traffic.json")
     try:
         t = json.load(open(path))[name]
-        return round((t["fetch_bytes_per_packet"] + t["write_bytes_per_packet"]) * n)
+        return (round((t["fetch_bytes_per_packet"] + t["write_bytes_per_packet"]) * n),
+                "profiles/%s_pmc.json (%s)" % (t["profile"], t.get("kernel", "decode_kernel")))
     except (OSError, KeyError, ValueError):
-        return None
+        return None, None
 
 
 def main():
@@ -576,14 +705,15 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--packets", type=int, default=64 * 2**20, help="packets per GPU")
-    ap.add_argument("--configs", default="c3,c2,c4,c1", help="first one is the headline")
+    ap.add_argument("--configs", default=None,
+                    help="first one is the headline (default c3,c2,c4,c1, plus c4s strong scaling when N > 1)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--no-probe", action="store_true", help="skip the streaming-read reference kernel")
     ap.add_argument("--pcie", action="store_true", help="also time the host-buffer path (PCIe-inclusive)")
-    ap.add_argument("--c5", type=float, default=0.0, metavar="GIB",
-                    help="also run config C5: replay a GIB-GiB pcapng end to end (gpk_replay_file)")
+    ap.add_argument("--c5", type=float, default=10.0, metavar="GIB",
+                    help="config C5: replay a GIB-GiB pcapng end to end (gpk_replay_file); 0 = skip")
     ap.add_argument("--afpacket", type=int, default=0, metavar="MPKTS",
                     help="also drain MPKTS Mi packets from an emulated TPACKET_V3 ring (gpk_tpacket_pump)")
     ap.add_argument("--flows", action="store_true",
@@ -591,16 +721,19 @@ def main():
     ap.add_argument("--bpf", action="store_true", help="also time row (f)4: classic BPF over 64M C4 packets")
     ap.add_argument("--tables", default="auto", choices=["auto", "global"],
                     help="next-layer tables: compact LDS copy (auto) or device-memory tables (global)")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl = RCCL (one rank per GPU); gloo + --same-device rehearses ranks on one GPU")
+    ap.add_argument("--same-device", action="store_true", help="every rank on cuda:0 (rehearsal only)")
     args = ap.parse_args()
 
     import torch
-    rank, world, local = dist_init()
+    rank, world, local = dist_init(args.dist_backend, args.same_device)
     from gopacket_amd import engine
     ctx = engine.Context(local)
     if args.tables == "global":
         from gopacket_amd import _lib
         ctx.set_table_mode(_lib.TABLES_GLOBAL)
-    names = args.configs.split(",")
+    names = (args.configs or ("c3,c2,c4,c1" + (",c4s" if world > 1 else ""))).split(",")
     results = {}
     for name in names:
         results[name] = run_config(name, args.packets, args.steps, args.warmup, rank, world, ctx,
@@ -612,6 +745,7 @@ def main():
         total_pkts = r["n"] * world * args.steps
         value = total_pkts / r["wall_s"] / 1e6
         achieved = r["algo_bytes"] / (r["kernel_ms"] * 1e-3) / 1e9
+        traffic, traffic_profile = load_traffic(head, r["n"])
         out = {
             "metric": "Mpkts/s device-resident Eth/IPv4/TCP decode+cksum+flow-hash; % HBM roofline",
             "value": round(value, 2), "unit": "Mpkts/s", "n_gpus": world, "steps": args.steps,
@@ -622,8 +756,9 @@ def main():
                        "payload_bytes_per_gpu": r["payload_bytes"], "parallelism": "shard%d" % world,
                        "parser": "+".join(CONFIGS[head]["decoders"])},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": load_traffic(head, r["n"]),
-                         "kernel": "gpk::decode_kernel<true,false,true,false,5,6>", "traffic_unit": "bytes per launch", "kernel_ms": round(r["kernel_ms"], 4),
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "traffic_profile": traffic_profile, "kernel": r["kernel"],
+                         "traffic_unit": "bytes per launch", "kernel_ms": round(r["kernel_ms"], 4),
                          "algo_bytes_per_launch": r["algo_bytes"],
                          "probe_read_GBps": r["probe_gbs"] and round(r["probe_gbs"], 1)},
             "parity": r["parity"],
@@ -632,16 +767,22 @@ def main():
         for name in names[1:]:
             s = results[name]
             ach = s["algo_bytes"] / (s["kernel_ms"] * 1e-3) / 1e9
-            out["configs"][name] = {
-                "workload": CONFIGS[name]["workload"],
-                "value": round(s["n"] * world * args.steps / s["wall_s"] / 1e6, 2), "unit": "Mpkts/s",
-                "kernel_ms": round(s["kernel_ms"], 4), "achieved_GBps": round(ach, 1),
-                "frac": round(ach / HBM_PEAK_GBS, 4), "parity": s["parity"],
-                "probe_read_GBps": s["probe_gbs"] and round(s["probe_gbs"], 1)}
+            st = s["strong"]
+            pk = st["total_packets"] if st else s["n"] * world
+            row = {"workload": CONFIGS[name]["workload"],
+                   "value": round(pk * args.steps / s["wall_s"] / 1e6, 2), "unit": "Mpkts/s",
+                   "kernel": s["kernel"], "kernel_ms": round(s["kernel_ms"], 4), "achieved_GBps": round(ach, 1),
+                   "frac": round(ach / HBM_PEAK_GBS, 4), "parity": s["parity"],
+                   "probe_read_GBps": s["probe_gbs"] and round(s["probe_gbs"], 1)}
+            if st:
+                row.update(scaling="strong", total_packets=st["total_packets"], byte_balance=st["balance"],
+                           note="one batch split at byte-balanced cuts; kernel_ms/achieved are rank 0's shard")
+            out["configs"][name] = row
         if args.pcie and world == 1:
             out["pcie_inclusive"] = pcie_inclusive(head, ctx)
+        threads = host_cores()[0]
         if args.c5 > 0 and world == 1:
-            out["c5"] = c5_replay(ctx, gib=args.c5)
+            out["c5"] = c5_replay(ctx, gib=args.c5, cpu_threads=threads)
         if args.bpf and world == 1:
             out["bpf"] = bpf_filter_bench(ctx)
         if args.flows and world == 1:
@@ -649,12 +790,13 @@ def main():
         if args.afpacket > 0 and world == 1:
             out["afpacket"] = afpacket_pump(ctx, packets=args.afpacket * 2**20)
         if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(head, seconds=args.cpu_seconds)
+            out["cpu_baseline"] = cpu_baseline(head, names, seconds=args.cpu_seconds)
         else:
             out["cpu_baseline"] = None
         print(json.dumps(out))
     if world > 1:
         import torch.distributed as dist
+        dist.barrier()
         dist.destroy_process_group()
 
 

@@ -1203,7 +1203,9 @@ extern "C" int gpk_tpacket_pump(gpk_ctx* ctx, const gpk_parser* parser, gpk_tpac
     if (!good) break;
     gpk_tpacket_release_seq(t, &b.rel_seq);
     b.h2d_pending = true;
-    gpk_batch db{dev, b.d_off, b.d_cap, n, ring_bytes + NB * side_cap};
+    // data_bytes: the batch's span as the mean-packet-size hint (gpk.h)
+    const uint64_t span = n ? b.h_off[n - 1] + b.h_cap[n - 1] - std::min(b.h_off[0], b.h_off[n - 1]) : 0;
+    gpk_batch db{dev, b.d_off, b.d_cap, n, span};
     gpk_results dr{b.d_rec, b.d_err, b.d_flow, nullptr};
     int drc = gpk_decode_batch(ctx, parser, &db, &dr, b.stream);
     if (drc) {

@@ -5,9 +5,9 @@
 // decoders below restate layers/{ethernet,dot1q,ip4,ip6,tcp,udp}.go; their
 // results must be bit-identical to the reference (checked against oracle/).
 //
-// Bytes come from a per-lane LDS window holding the first ~128 bytes of the
-// packet (filled by the kernel with coalesced 16-byte loads); positions past
-// the window fall back to global byte loads (deep stacks, long options).
+// Bytes come from a per-lane LDS window holding the packet's first 80 bytes
+// (five 16-byte chunks, filled by the kernel); positions past the window fall
+// back to global byte loads (deep stacks, long options).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -93,14 +93,8 @@ constexpr int kWaves = kBlock / 64;
 #define GPK_WIN_CHUNKS 5  // 80-byte header window: 6 blocks per CU (A/B r01: C2 -21%, C4 -17%, C3 -5% vs 9)
 #endif
 constexpr int kWinChunks = GPK_WIN_CHUNKS;
-#ifndef GPK_LINE_OWN
-#define GPK_LINE_OWN 0  // 1: each 128-byte line read from HBM once (LineOwn; A/B r01: FETCH -12%, time +4%)
-#endif
-// odd: lanes reading equal positions hit distinct banks. With line ownership
-// the three dwords after the window hold the lane's LineOwn sums (still 6
-// blocks of 256 lanes per CU: 23.5 KB + 2.9 KB of tables).
-constexpr int kSlotDw = kWinChunks * 4 + (GPK_LINE_OWN ? 3 : 1);
-constexpr int kOwnDw = kWinChunks * 4;  // LineOwn h, t, hx at slot + kOwnDw + 0..2
+// odd: lanes reading equal packet positions hit distinct banks
+constexpr int kSlotDw = kWinChunks * 4 + 1;
 constexpr int kLdsBytes = kBlock * kSlotDw * 4;
 
 // Dynamic LDS of the decode kernels (one declaration, aliased everywhere).

@@ -4,7 +4,8 @@
 //   * gpk_parser: the DecodingLayerContainer (parser.go:147-169, Map semantics:
 //     later Put overrides) + DecodingLayerParserOptions (parser.go:337-351) +
 //     the next-layer tables (layers/enums.go:294-353, layers/ports.go:54-183).
-//   * gpk_ctx: one device, its uploaded table copy and staging buffers.
+//   * gpk_ctx: one device, device copies of parser tables (one per parser
+//     version in use, see TabSlot) and staging buffers.
 //   * error text: the exact strings DecodeLayers returns (see gpk.h enum).
 // There is no CPU decode path here: every packet is decoded by the device.
 #include <hip/hip_runtime.h>
@@ -23,6 +24,7 @@
 #include "gpk_registry_gen.h"
 
 extern "C" hipError_t gpk_launch_decode(const gpk::KParams* P, int with_l4, int with_layout, hipStream_t stream);
+extern "C" int gpk_launch_describe(const gpk::KParams* P, int with_l4, int with_layout, char* buf, size_t cap);
 extern "C" hipError_t gpk_launch_list(const gpk::KParams* P, uint64_t index, int64_t* out, uint32_t cap,
                                       uint32_t* out_n, hipStream_t stream);
 
@@ -51,15 +53,31 @@ struct gpk_parser {
   gpk::DevTables tab;
 };
 
-struct gpk_ctx {
-  int device = 0;
+// Device copies of parser tables. A context keeps a few, keyed by the
+// parser's table version, so parsers used alternately (on one stream or on
+// several) each read their own copy: gopacket gives every parser its own
+// state (doc.go:211-228), and a launch on one stream must never see a table
+// rewritten for a launch on another. A copy is rewritten only for a new
+// version, and only after every launch that read it has completed (an event
+// recorded after each launch, per stream).
+struct TabSlot {
   gpk::DevTables* dtab = nullptr;
   uint32_t* dctab = nullptr;  // compact blob (gpk::kCtDwords), valid when compact
   bool compact = false;
-  bool force_global = false;  // gpk_ctx_set_table_mode(GPK_TABLES_GLOBAL)
+  bool global_mode = false;   // built under GPK_TABLES_GLOBAL
   gpk::CompactGeom cg{};
-  const gpk_parser* uploaded = nullptr;
-  uint64_t uploaded_version = 0;
+  uint64_t version = 0;       // parser table version held, 0 = empty
+  uint64_t last_use = 0;      // LRU tick
+  std::vector<std::pair<hipStream_t, hipEvent_t>> uses;  // last launch reading this copy, per stream
+};
+constexpr int kTabSlots = 8;
+constexpr size_t kMaxStreamsPerSlot = 16;
+
+struct gpk_ctx {
+  int device = 0;
+  bool force_global = false;  // gpk_ctx_set_table_mode(GPK_TABLES_GLOBAL)
+  TabSlot slots[kTabSlots];
+  uint64_t tick = 0;
   // staging for gpk_decode_batch_host / gpk_decoded_list
   void* dbuf = nullptr;
   size_t dbuf_bytes = 0;
@@ -189,6 +207,17 @@ int gpk_parser_set_udp_port(gpk_parser* p, uint32_t v, int32_t lt) {
 }
 
 // ---- context -----------------------------------------------------------------
+static void free_slots(gpk_ctx* c) {
+  for (TabSlot& t : c->slots) {
+    for (auto& u : t.uses) (void)hipEventDestroy(u.second);
+    t.uses.clear();
+    if (t.dtab) (void)hipFree(t.dtab);
+    if (t.dctab) (void)hipFree(t.dctab);
+    t.dtab = nullptr;
+    t.dctab = nullptr;
+  }
+}
+
 int gpk_ctx_create(gpk_ctx** out, int device) {
   if (!out) return GPK_EINVAL;
   int ndev = 0;
@@ -197,18 +226,7 @@ int gpk_ctx_create(gpk_ctx** out, int device) {
   gpk_ctx* c = new (std::nothrow) gpk_ctx;
   if (!c) return GPK_ENOMEM;
   c->device = device;
-  if (hipMalloc(&c->dtab, sizeof(gpk::DevTables)) != hipSuccess) {
-    delete c;
-    return GPK_ENOMEM;
-  }
-  if (hipMalloc(&c->dctab, gpk::kCtDwords * 4) != hipSuccess) {
-    (void)hipFree(c->dtab);
-    delete c;
-    return GPK_ENOMEM;
-  }
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
-    (void)hipFree(c->dtab);
-    (void)hipFree(c->dctab);
     delete c;
     return GPK_EHIP;
   }
@@ -219,9 +237,9 @@ int gpk_ctx_create(gpk_ctx** out, int device) {
 int gpk_ctx_destroy(gpk_ctx* c) {
   if (!c) return GPK_OK;
   (void)hipSetDevice(c->device);
+  (void)hipDeviceSynchronize();  // launches still reading the table copies
   if (c->stream) (void)hipStreamDestroy(c->stream);
-  if (c->dtab) (void)hipFree(c->dtab);
-  if (c->dctab) (void)hipFree(c->dctab);
+  free_slots(c);
   if (c->dbuf) (void)hipFree(c->dbuf);
   delete c;
   return GPK_OK;
@@ -314,8 +332,7 @@ static bool build_compact(const gpk::DevTables& t, int64_t first, uint32_t* blob
 int gpk_ctx_set_table_mode(gpk_ctx* c, int mode) {
   if (!c || (mode != GPK_TABLES_AUTO && mode != GPK_TABLES_GLOBAL)) return GPK_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
-  c->force_global = mode == GPK_TABLES_GLOBAL;
-  c->uploaded_version = 0;  // rebuild on the next call
+  c->force_global = mode == GPK_TABLES_GLOBAL;  // copies are keyed by mode too
   return GPK_OK;
 }
 
@@ -335,27 +352,73 @@ static uint32_t fast_flags(const gpk_parser* p) {
   return f;
 }
 
-static int upload(gpk_ctx* c, const gpk_parser* p, hipStream_t s, gpk::KParams& P) {
-  if (c->uploaded_version != p->version) {
-    static thread_local uint32_t blob[gpk::kCtDwords];
-    HIPCHK(hipMemcpyAsync(c->dtab, &p->tab, sizeof(gpk::DevTables), hipMemcpyHostToDevice, s));
-    c->compact = !c->force_global && build_compact(p->tab, p->first, blob, c->cg);
-    if (c->compact) HIPCHK(hipMemcpyAsync(c->dctab, blob, gpk::kCtDwords * 4, hipMemcpyHostToDevice, s));
-    HIPCHK(hipStreamSynchronize(s));  // p->tab and blob may change after we return
-    c->uploaded = p;
-    c->uploaded_version = p->version;
+// Wait until no launch reads slot t any more (it is about to be rewritten).
+static int drain_slot(TabSlot& t) {
+  for (auto& u : t.uses) {
+    HIPCHK(hipEventSynchronize(u.second));
+    (void)hipEventDestroy(u.second);
   }
-  P.tab = c->dtab;
-  P.ctab = c->compact ? c->dctab : nullptr;
-  P.cg = c->cg;
+  t.uses.clear();
+  return GPK_OK;
+}
+
+// The device copy of parser p's tables (found, or written into a free or the
+// least recently used slot), and the table fields of P. Returns the slot
+// index in *slot for note_launch.
+static int upload(gpk_ctx* c, const gpk_parser* p, gpk::KParams& P, int* slot) {
+  int k = -1;
+  for (int i = 0; i < kTabSlots; i++)
+    if (c->slots[i].version == p->version && c->slots[i].global_mode == c->force_global) k = i;
+  if (k < 0) {
+    for (int i = 0; i < kTabSlots; i++)
+      if (k < 0 || c->slots[i].last_use < c->slots[k].last_use) k = i;  // empty slots have last_use 0
+    TabSlot& t = c->slots[k];
+    int rc = drain_slot(t);
+    if (rc) return rc;
+    t.version = 0;
+    if (!t.dtab && hipMalloc(&t.dtab, sizeof(gpk::DevTables)) != hipSuccess) return GPK_ENOMEM;
+    if (!t.dctab && hipMalloc(&t.dctab, gpk::kCtDwords * 4) != hipSuccess) return GPK_ENOMEM;
+    static thread_local uint32_t blob[gpk::kCtDwords];
+    HIPCHK(hipMemcpyAsync(t.dtab, &p->tab, sizeof(gpk::DevTables), hipMemcpyHostToDevice, c->stream));
+    t.compact = !c->force_global && build_compact(p->tab, p->first, blob, t.cg);
+    if (t.compact) HIPCHK(hipMemcpyAsync(t.dctab, blob, gpk::kCtDwords * 4, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));  // on the device before any launch; p->tab and blob may change
+    t.version = p->version;
+    t.global_mode = c->force_global;
+  }
+  TabSlot& t = c->slots[k];
+  t.last_use = ++c->tick;
+  *slot = k;
+  P.tab = t.dtab;
+  P.ctab = t.compact ? t.dctab : nullptr;
+  P.cg = t.cg;
   P.first_kind = (p->first >= 0 && p->first < GPK_MAX_LAYER_TYPE) ? p->tab.dispatch[p->first] : GPK_DEC_NONE;
   P.fast = fast_flags(p);
   // headers that fit the 4-chunk window: no decoder that adds tags, IPv6, extension headers or TCP options
   P.small_headers = 1;
-  for (int t = 0; t < GPK_MAX_LAYER_TYPE; t++) {
-    const int k = p->tab.dispatch[t];
-    if (k == GPK_DEC_DOT1Q || k == GPK_DEC_IPV6 || k == GPK_DEC_IPV6_EXT || k == GPK_DEC_TCP) P.small_headers = 0;
+  for (int t2 = 0; t2 < GPK_MAX_LAYER_TYPE; t2++) {
+    const int kd = p->tab.dispatch[t2];
+    if (kd == GPK_DEC_DOT1Q || kd == GPK_DEC_IPV6 || kd == GPK_DEC_IPV6_EXT || kd == GPK_DEC_TCP) P.small_headers = 0;
   }
+  return GPK_OK;
+}
+
+// A launch on stream s reads slot k: record that, so the slot is rewritten
+// only after it completes.
+static int note_launch(gpk_ctx* c, int k, hipStream_t s) {
+  TabSlot& t = c->slots[k];
+  hipEvent_t ev = nullptr;
+  for (auto& u : t.uses)
+    if (u.first == s) ev = u.second;
+  if (!ev) {
+    if (t.uses.size() >= kMaxStreamsPerSlot) {
+      int rc = drain_slot(t);
+      if (rc) return rc;
+    }
+    HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    t.uses.emplace_back(s, ev);
+  }
+  HIPCHK(hipEventRecord(ev, s));
   return GPK_OK;
 }
 
@@ -400,10 +463,11 @@ int gpk_decode_batch(gpk_ctx* c, const gpk_parser* p, const gpk_batch* b, const 
   hipStream_t s = (hipStream_t)stream;
   std::lock_guard<std::mutex> g(c->mu);
   HIPCHK(hipSetDevice(c->device));
-  rc = upload(c, p, s, P);
+  int slot = 0;
+  rc = upload(c, p, P, &slot);
   if (rc) return rc;
   HIPCHK(gpk_launch_decode(&P, (p->outputs & GPK_OUT_L4_CSUM) != 0, o->layouts != nullptr, s));
-  return GPK_OK;
+  return note_launch(c, slot, s);
 }
 
 // gpk_decode_batch plus the fused grouping key per packet (gpk_flows.hip
@@ -423,10 +487,27 @@ extern "C" __attribute__((visibility("hidden"))) int gpk_decode_batch_keys(gpk_c
   hipStream_t s = (hipStream_t)stream;
   std::lock_guard<std::mutex> g(c->mu);
   HIPCHK(hipSetDevice(c->device));
-  rc = upload(c, p, s, P);
+  int slot = 0;
+  rc = upload(c, p, P, &slot);
   if (rc) return rc;
   HIPCHK(gpk_launch_decode(&P, (p->outputs & GPK_OUT_L4_CSUM) != 0, o->layouts != nullptr, s));
-  return GPK_OK;
+  return note_launch(c, slot, s);
+}
+
+int gpk_decode_kernel_name(gpk_ctx* c, const gpk_parser* p, const gpk_batch* b, int with_layouts, char* buf,
+                           size_t cap) {
+  if (!buf || !cap) return GPK_EINVAL;
+  gpk::KParams P;
+  gpk_results o{nullptr, nullptr, nullptr, nullptr};
+  int rc = make_params(c, p, b, nullptr, P);
+  if (rc) return rc;
+  (void)o;
+  std::lock_guard<std::mutex> g(c->mu);
+  HIPCHK(hipSetDevice(c->device));
+  int slot = 0;
+  rc = upload(c, p, P, &slot);
+  if (rc) return rc;
+  return gpk_launch_describe(&P, (p->outputs & GPK_OUT_L4_CSUM) != 0, with_layouts != 0, buf, cap);
 }
 
 static int ensure_dbuf(gpk_ctx* c, size_t bytes) {
@@ -468,9 +549,12 @@ int gpk_decode_batch_host(gpk_ctx* c, const gpk_parser* p, const gpk_batch* hb, 
   gpk::KParams P;
   rc = make_params(c, p, &db, &dr, P);
   if (rc) return rc;
-  rc = upload(c, p, s, P);
+  int slot = 0;
+  rc = upload(c, p, P, &slot);
   if (rc) return rc;
   HIPCHK(gpk_launch_decode(&P, (p->outputs & GPK_OUT_L4_CSUM) != 0, dr.layouts != nullptr, s));
+  rc = note_launch(c, slot, s);
+  if (rc) return rc;
   HIPCHK(hipMemcpyAsync(ho->records, dr.records, n * sizeof(gpk_record), hipMemcpyDeviceToHost, s));
   if (ho->err_args) HIPCHK(hipMemcpyAsync(ho->err_args, dr.err_args, n * 8, hipMemcpyDeviceToHost, s));
   if (flows) HIPCHK(hipMemcpyAsync(ho->flows, dr.flows, n * 24, hipMemcpyDeviceToHost, s));
@@ -493,9 +577,12 @@ int gpk_decoded_list(gpk_ctx* c, const gpk_parser* p, const gpk_batch* b, uint64
   int64_t* dl = (int64_t*)c->dbuf;
   uint32_t* dn = (uint32_t*)((char*)c->dbuf + align_up(8 * (size_t)cap));
   hipStream_t s = c->stream;
-  rc = upload(c, p, s, P);
+  int slot = 0;
+  rc = upload(c, p, P, &slot);
   if (rc) return rc;
   HIPCHK(gpk_launch_list(&P, index, dl, cap, dn, s));
+  rc = note_launch(c, slot, s);
+  if (rc) return rc;
   uint32_t n = 0;
   HIPCHK(hipMemcpyAsync(&n, dn, 4, hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
@@ -524,9 +611,12 @@ int gpk_decoded_list_host(gpk_ctx* c, const gpk_parser* p, const uint8_t* pkt, u
   gpk::KParams P;
   rc = make_params(c, p, &db, nullptr, P);
   if (rc) return rc;
-  rc = upload(c, p, s, P);
+  int slot = 0;
+  rc = upload(c, p, P, &slot);
   if (rc) return rc;
   HIPCHK(gpk_launch_list(&P, 0, (int64_t*)(d + o_list), cap, (uint32_t*)(d + o_n), s));
+  rc = note_launch(c, slot, s);
+  if (rc) return rc;
   uint32_t n = 0;
   HIPCHK(hipMemcpyAsync(&n, d + o_n, 4, hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));

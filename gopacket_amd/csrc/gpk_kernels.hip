@@ -2,24 +2,31 @@
 // hash for gfx950 (MI355X). Hand-written HIP; no MFMA (byte parse and integer
 // reduction, HBM-bandwidth bound).
 //
-// One workgroup = 256 packets = 4 waves. Per packet the bytes are read once:
+// One workgroup = 256 packets = 4 waves, one lane per packet.
 //
-//  Phase A (lane per packet): the packet's first 128 B (16-byte aligned
-//    chunks) are loaded with global_load_dwordx4 into the lane's LDS slot;
-//    the lane runs DecodeLayers (gpk_device.h) out of LDS, computes the IPv4
-//    header checksum (ip4.go:323-332), the three Flow.FastHash values
-//    (flows.go:167-174) and, when the whole TCP/UDP segment sits inside the
-//    window, the L4 checksum (tcpip.go:54-69) too.
-//  Phase B (wave-cooperative): TCP/UDP segments that extend past the window
-//    are summed by the whole wave. The wave's segments are cut into 16-byte
-//    chunks laid end to end (exclusive scan of chunk counts); lane l takes
-//    chunk t+l, so consecutive lanes load consecutive 16-byte chunks of the
-//    same packet (coalesced dwordx4). Partial sums are combined with a
-//    segmented scan keyed by packet and added into a per-packet LDS
-//    accumulator. RFC1071 sums are position independent except for byte
-//    parity, and ComputeChecksum wraps mod 2^32 (checksum.go:40-49), so
-//    summing mod 2^32 in any order is bit-exact.
+//  Phase A (lane per packet): the packet's first 80 bytes (five 16-byte
+//    aligned chunks) are loaded into the lane's LDS slot; the lane runs
+//    DecodeLayers (gpk_device.h) out of LDS, computes the IPv4 header checksum
+//    (ip4.go:323-332), the three Flow.FastHash values (flows.go:167-174) and,
+//    for the TCP/UDP checksum (tcpip.go:54-69), the pseudo-header sum and the
+//    byte range [s, e) of the segment.
+//  Phase B (wave-cooperative): the segments' byte sums. RFC1071 word sums are
+//    position independent except for byte parity, and ComputeChecksum wraps
+//    mod 2^32 (checksum.go:40-49), so the sum of [s, e) is assembled from
+//    even-/odd-address byte sums mod 2^32 in any order, bit-exactly:
+//    * dense waves (the usual packed batch: the wave's segments lie in one
+//      region not much larger than their total): the wave streams the whole
+//      region once, 2 KiB per pass (32 bytes per lane, coalesced raw-buffer
+//      loads), keeps a running wave-wide prefix sum of the even/odd byte sums
+//      per 32-byte granule (DPP scan), and every lane picks the prefix at its
+//      segment's first and last granule with ds_bpermute. Segment sum =
+//      prefix difference - the head granule's bytes before s + the tail
+//      granule's bytes before e. No per-packet reduction, no per-packet SALU.
+//    * sparse waves (scattered offsets): the segments are streamed one after
+//      another as whole-wave 1 KiB loads and reduced per packet (DPP).
 #include <hip/hip_runtime.h>
+
+#include <cstdio>
 
 #include "gpk_device.h"
 
@@ -27,53 +34,36 @@ namespace gpk {
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-#ifndef GPK_NT_A
-#define GPK_NT_A 0  // A/B (r01): temporal phase-A loads keep lines shared with phase B in L2: C3 +30%
-#endif
 #ifndef GPK_WAVES_PER_EU
 #define GPK_WAVES_PER_EU 6  // <= 80 VGPRs: 6 waves/SIMD, matching the 6 blocks per CU the LDS allows
-#endif
-#ifndef GPK_LDS_FIT
-#define GPK_LDS_FIT 1  // dynamic LDS sized to the parser's table blob (7 blocks/CU at 5 chunks)
 #endif
 #ifndef GPK_W4_WAVES
 #define GPK_W4_WAVES 8  // 4-chunk window kernel: 64 VGPRs
 #endif
-#ifndef GPK_PB_G
-#define GPK_PB_G 4  // phase B: pending packets per wave pass
-#endif
-#ifndef GPK_PREFETCH
-#define GPK_PREFETCH 0  // 1: next tile's windows in flight (persistent only; A/B r01: no gain)
-#endif
-#ifndef GPK_PERSISTENT
-#define GPK_PERSISTENT 0  // 1: blocks loop over tiles (A/B r01: +50 VGPRs from hoisting, no gain)
-#endif
-#ifndef GPK_PB_STREAM
-#define GPK_PB_STREAM 1  // phase B as a continuous stream of 1 KiB wave loads
+#ifndef GPK_PB_GRAN
+#define GPK_PB_GRAN 2  // dense phase B: 16-byte chunks per lane per pass (granule = 32 bytes)
 #endif
 #ifndef GPK_PB_DEPTH
-#define GPK_PB_DEPTH 8  // phase-B wave loads in flight
+#define GPK_PB_DEPTH 3  // dense phase B: passes in flight (2 in the 72-VGPR kernels)
+#endif
+#ifndef GPK_PB_SDEPTH
+#define GPK_PB_SDEPTH 4  // sparse phase B: 1 KiB wave loads in flight
 #endif
 #ifndef GPK_PB_NULL
-#define GPK_PB_NULL 0  // timing-only: phase-B loads read nothing (zero-record descriptors)
-#endif
-#ifndef GPK_PPL
-#define GPK_PPL 1  // packets per lane (tiles per block)
-#endif
-#ifndef GPK_NT_B
-#define GPK_NT_B 1
+#define GPK_PB_NULL 0  // timing only: phase-B stream loads read nothing (zero-record descriptors)
 #endif
 
-// 16-byte load; read-once packet bytes are non-temporal.
-template <bool kNT>
-__device__ __forceinline__ uint4 ld16t(const uint8_t* p) {
-  u32x4 x = kNT ? __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p))
-                : *reinterpret_cast<const u32x4*>(p);
+constexpr int kGran = GPK_PB_GRAN;
+constexpr uint32_t kGranBytes = 16u * kGran;
+constexpr uint32_t kPassBytes = 64u * kGranBytes;
+static_assert(kGran == 1 || kGran == 2 || kGran == 4, "granule of 1, 2 or 4 chunks");
+
+// Header-window loads keep the default (temporal) policy: the window's last
+// line is re-read by phase B (A/B r01: non-temporal window loads +11-23 %).
+__device__ __forceinline__ uint4 ld16(const uint8_t* p) {
+  const u32x4 x = *reinterpret_cast<const u32x4*>(p);
   return make_uint4(x.x, x.y, x.z, x.w);
 }
-// header window and partial edge chunks (phase A) / full chunks (phase B)
-__device__ __forceinline__ uint4 ld16(const uint8_t* p) { return ld16t<GPK_NT_A>(p); }
-__device__ __forceinline__ uint4 ld16b(const uint8_t* p) { return ld16t<GPK_NT_B>(p); }
 
 // Byte sums with v_dot4_u32_u8: bytes 0,2 (even addresses) and 1,3 (odd).
 __device__ __forceinline__ uint32_t dot_even(uint32_t w, uint32_t acc) {
@@ -116,29 +106,9 @@ __device__ __forceinline__ uint32_t sum_words(const Rd& r, uint32_t p, uint32_t 
   return s;
 }
 
-// 16 bytes of a 16-aligned chunk at absolute address A, restricted to
-// [s, e); a byte at address x counts <<8 when x has parity `par` (the parity
-// of the segment's first byte: BE16 words start there). Used for the at most
-// two partial chunks of a segment; full chunks go through chunk_eo.
-__device__ __forceinline__ uint32_t chunk_sum(uint4 v, uint64_t A, uint64_t s, uint64_t e, uint32_t par) {
-  uint32_t lo = s > A ? (uint32_t)(s - A) : 0u;        // 0..15
-  uint32_t hi = e < A + 16 ? (uint32_t)(e - A) : 16u;  // 1..16
-  uint32_t w[4] = {v.x, v.y, v.z, v.w};
-  uint32_t E = 0, O = 0;
-#pragma unroll
-  for (int d = 0; d < 4; d++) {
-    int l = (int)lo - 4 * d, h = (int)hi - 4 * d;
-    l = l < 0 ? 0 : (l > 4 ? 4 : l);
-    h = h < 0 ? 0 : (h > 4 ? 4 : h);
-    uint32_t m = h > l ? ((0xffffffffu >> (8 * (4 - (h - l)))) << (8 * l)) : 0u;
-    E = dot_even(w[d] & m, E);
-    O = dot_odd(w[d] & m, O);
-  }
-  return par ? (O << 8) + E : (E << 8) + O;
-}
-
-// Even/odd byte sums of a full chunk.
-__device__ __forceinline__ void chunk_eo(uint4 v, uint32_t& E, uint32_t& O) {
+// Even/odd byte sums of a 16-byte chunk (chunks are 16-byte aligned, so a
+// byte's index parity is its address parity).
+__device__ __forceinline__ void chunk_eo(const u32x4& v, uint32_t& E, uint32_t& O) {
   E = dot_even(v.x, E);
   O = dot_odd(v.x, O);
   E = dot_even(v.y, E);
@@ -147,6 +117,40 @@ __device__ __forceinline__ void chunk_eo(uint4 v, uint32_t& E, uint32_t& O) {
   O = dot_odd(v.z, O);
   E = dot_even(v.w, E);
   O = dot_odd(v.w, O);
+}
+
+// Even/odd byte sums of the chunk's bytes [0, n), n in 0..16.
+__device__ __forceinline__ void chunk_eo_below(const u32x4& v, uint32_t n, uint32_t& E, uint32_t& O) {
+  const uint32_t nl = n < 8 ? n : 8u, nh = n > 8 ? n - 8 : 0u;
+  const uint64_t ml = nl >= 8 ? ~0ull : (1ull << (8 * nl)) - 1;
+  const uint64_t mh = nh >= 8 ? ~0ull : (1ull << (8 * nh)) - 1;
+  const uint32_t w0 = v.x & (uint32_t)ml, w1 = v.y & (uint32_t)(ml >> 32);
+  const uint32_t w2 = v.z & (uint32_t)mh, w3 = v.w & (uint32_t)(mh >> 32);
+  E = dot_even(w0, E);
+  O = dot_odd(w0, O);
+  E = dot_even(w1, E);
+  O = dot_odd(w1, O);
+  E = dot_even(w2, E);
+  O = dot_odd(w2, O);
+  E = dot_even(w3, E);
+  O = dot_odd(w3, O);
+}
+
+// A granule: kGran consecutive 16-byte chunks.
+struct Gran {
+  u32x4 c[kGran];
+};
+__device__ __forceinline__ void gran_eo(const Gran& g, uint32_t& E, uint32_t& O) {
+#pragma unroll
+  for (int k = 0; k < kGran; k++) chunk_eo(g.c[k], E, O);
+}
+// The granule's bytes [0, n), n in 0..kGranBytes-1.
+__device__ __forceinline__ void gran_eo_below(const Gran& g, uint32_t n, uint32_t& E, uint32_t& O) {
+#pragma unroll
+  for (int k = 0; k < kGran; k++) {
+    const int m = (int)n - 16 * k;
+    chunk_eo_below(g.c[k], m < 0 ? 0u : (m > 16 ? 16u : (uint32_t)m), E, O);
+  }
 }
 
 // v_readlane_b32 returns int: widen through uint32_t, never through int
@@ -158,14 +162,48 @@ __device__ __forceinline__ uint64_t readlane64(uint64_t v, uint32_t lane) {
   return ((uint64_t)readlane32((uint32_t)(v >> 32), lane) << 32) | (uint64_t)readlane32((uint32_t)v, lane);
 }
 
-// Sum over the 64 lanes (all active): rotations inside each 16-lane row
-// (DPP row_ror 8,4,2,1), then the four row totals via readlane.
-__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
-  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xf, 0xf, false);
-  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x124, 0xf, 0xf, false);
-  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x122, 0xf, 0xf, false);
-  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x121, 0xf, 0xf, false);
-  return readlane32(v, 0) + readlane32(v, 16) + readlane32(v, 32) + readlane32(v, 48);
+// Inclusive prefix sum over the 64 lanes (all active): DPP row_shr 1,2,4,8
+// inside each 16-lane row, then row_bcast 15 / 31 across rows.
+__device__ __forceinline__ uint32_t wave_scan(uint32_t v) {
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);
+  return v;
+}
+// Wave-wide min / max (all lanes active), same pattern; result in every lane
+// via readlane 63 (an SGPR).
+__device__ __forceinline__ uint32_t wave_min(uint32_t v) {
+  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)v, 0x111, 0xf, 0xf, false));
+  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)v, 0x112, 0xf, 0xf, false));
+  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)v, 0x114, 0xf, 0xf, false));
+  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)v, 0x118, 0xf, 0xf, false));
+  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)v, 0x142, 0xa, 0xf, false));
+  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)v, 0x143, 0xc, 0xf, false));
+  return readlane32(v, 63);
+}
+__device__ __forceinline__ uint32_t wave_max(uint32_t v) {
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false));
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false));
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false));
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false));
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false));
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false));
+  return readlane32(v, 63);
+}
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) { return readlane32(wave_scan(v), 63); }
+
+// Raw-buffer descriptor over [base, base + bytes): loads at offsets >= bytes
+// return zeros without touching memory (hardware range check; a load that
+// crosses `bytes` returns zeros too, so `bytes` is a multiple of 16).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const uint8_t* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, GPK_PB_NULL ? 0 : bytes, 0x00020000);
+}
+// streamed (read-once) bytes: non-temporal (A/B r01: -7 % on C3)
+__device__ __forceinline__ u32x4 bload(__amdgpu_buffer_rsrc_t rs, uint32_t voff, uint32_t soff) {
+  return __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, 2);
 }
 
 // Header window of one packet in registers: chunks [0, nchunk) of the
@@ -174,11 +212,10 @@ template <int W>
 struct WinT {
   uint4 v[W];
 };
-using Win = WinT<kWinChunks>;
 // LDS dwords per lane for a window of W chunks (odd: see kSlotDw)
 template <int W>
 constexpr int slot_dw_of() {
-  return W * 4 + (GPK_LINE_OWN ? 3 : 1);
+  return W * 4 + 1;
 }
 
 struct Idx {
@@ -195,7 +232,7 @@ __device__ __forceinline__ Idx load_index(const KParams& P, uint64_t i) {
   return x;
 }
 
-template <int W = kWinChunks>
+template <int W>
 __device__ __forceinline__ uint32_t win_chunks(const Idx& x, bool active) {
   const uint32_t m = (uint32_t)(x.off & 15);
   uint32_t win = W * 16 - m;
@@ -221,97 +258,6 @@ __device__ __forceinline__ void store_window(uint32_t slot_dw, uint32_t nchunk, 
       gpk_smem[slot_dw + 4 * k + 2] = w.v[k].z;
       gpk_smem[slot_dw + 4 * k + 3] = w.v[k].w;
     }
-}
-
-// Line ownership (GPK_LINE_OWN). Phase B streams a packet's L4 bytes long
-// after its header window was read, by which time L2 has evicted the window's
-// lines: without care, the window's last 128-byte line and the packet's last
-// line (which holds the next packet's header) are each fetched from HBM twice.
-// So right after the window arrives (its lines are in L2) every lane also
-// loads the other chunks of the lines the window touched:
-//   head: [wend, he)  this packet's bytes after the window, up to the end of
-//         the window's last line: even/odd byte sums (hE, hO);
-//   tail: [L0, off)   the start of the window's first line, which is the END
-//         of the previous packet when packets are contiguous: even/odd sums
-//         (tE, tO) handed to lane-1, which then never touches that line.
-// Phase B then streams whole lines [he, L0 of the next packet) only. Sums
-// are by absolute byte parity, so the owner combines them with its segment
-// parity like every other partial sum.
-struct LineOwn {  // packed: three registers live across the parse
-  uint32_t h;    // head sums: even | odd << 16 (<= 112 bytes: each < 2^16)
-  uint32_t t;    // tail sums: even | odd << 16 (<= 127 bytes)
-  uint32_t hx;   // (he - off) | tok << 8: head end relative to the packet, tail valid
-};
-
-__device__ __forceinline__ void chunk_eo_masked(uint4 v, uint32_t lo, uint32_t hi, uint32_t& E, uint32_t& O) {
-  uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-  for (int d = 0; d < 4; d++) {
-    int l = (int)lo - 4 * d, h = (int)hi - 4 * d;
-    l = l < 0 ? 0 : (l > 4 ? 4 : l);
-    h = h < 0 ? 0 : (h > 4 ? 4 : h);
-    uint32_t m = h > l ? ((0xffffffffu >> (8 * (4 - (h - l)))) << (8 * l)) : 0u;
-    E = dot_even(w[d] & m, E);
-    O = dot_odd(w[d] & m, O);
-  }
-}
-
-// Round 2 of the header loads: issued after the window chunks arrived, so
-// these chunks (same lines) are L2 hits. prev_ok: the previous packet (lane-1)
-// ends exactly at this packet's start and covers [off & ~127, off).
-__device__ __forceinline__ LineOwn line_own(const KParams& P, uint64_t off, uint32_t cl, uint32_t nchunk,
-                                            const uint4& chunk0, bool active, bool prev_ok) {
-  const uint64_t A0 = off & ~15ull, wend = A0 + 16ull * nchunk, L0 = off & ~127ull;
-  const uint64_t pend = (off + cl) & ~15ull;
-  uint64_t he = (wend + 127) & ~127ull;
-  if (he > pend) he = pend;
-  if (he < wend || !active) he = wend;
-  const uint32_t nh = (uint32_t)((he - wend) >> 4);
-  const bool tok = active && prev_ok;
-  const uint32_t nt = tok ? (uint32_t)((A0 - L0) >> 4) : 0u;
-  uint32_t tE = 0, tO = 0, hE = 0, hO = 0;
-  if (tok) chunk_eo_masked(chunk0, 0, (uint32_t)(off & 15), tE, tO);  // [A0, off) of chunk 0
-  // the <= 11 non-window chunks of the <= 2 lines a window touches, in two
-  // batches (7 + 4) so the loads in flight fit the 80-VGPR budget
-#ifndef GPK_OWN_B2
-#define GPK_OWN_B2 1  // two load batches (7 + 4) instead of one of 11
-#endif
-  constexpr int kB1 = GPK_OWN_B2 ? 7 : 11, kB2 = GPK_OWN_B2 ? 4 : 0;
-#pragma unroll
-  for (int b = 0; b < (kB2 ? 2 : 1); b++) {
-    uint4 v[kB1];
-    const int j0 = b ? kB1 : 0, nb = b ? kB2 : kB1;
-    // batch 2 depends on batch 1's sums (an opaque zero): its loads cannot be
-    // hoisted next to batch 1's, which would double the registers in flight
-    uint32_t dep = 0;
-    if (b) asm volatile("v_and_b32 %0, 0, %1" : "=v"(dep) : "v"(hE + tE));
-#pragma unroll
-    for (int k = 0; k < nb; k++) {
-      const uint32_t j = (uint32_t)(j0 + k);
-      const uint64_t a = (j < nt ? L0 + 16ull * j : wend + 16ull * (j - nt)) + dep;
-      v[k] = j < nt + nh ? ld16(P.data + a) : make_uint4(0, 0, 0, 0);
-    }
-#pragma unroll
-    for (int k = 0; k < nb; k++) {
-      uint32_t e = 0, od = 0;
-      chunk_eo(v[k], e, od);
-      if ((uint32_t)(j0 + k) < nt) {
-        tE += e;
-        tO += od;
-      } else {
-        hE += e;
-        hO += od;
-      }
-    }
-  }
-  return LineOwn{hE | hO << 16, tE | tO << 16, (uint32_t)(he - off) | (tok ? 256u : 0u)};
-}
-
-__device__ __forceinline__ uint64_t shfl_up64(uint64_t v, int d) {
-  return ((uint64_t)(uint32_t)__shfl_up((int)(uint32_t)(v >> 32), d) << 32) | (uint32_t)__shfl_up((int)(uint32_t)v, d);
-}
-__device__ __forceinline__ uint64_t shfl_down64(uint64_t v, int d) {
-  return ((uint64_t)(uint32_t)__shfl_down((int)(uint32_t)(v >> 32), d) << 32) | (uint32_t)__shfl_down((int)(uint32_t)v, d);
 }
 
 // The grouping key of gpk_flows.hip's key_kernel, derived here from the parse
@@ -375,7 +321,210 @@ __device__ __forceinline__ int derive_key(const KParams& P, const Rd& r, const P
   return 0;
 }
 
-template <bool kL4, bool kLayout, class TT, bool kKeys = false, int W = kWinChunks>
+// ---- Phase B ---------------------------------------------------------------
+// Each lane with a job holds its segment [s, e) as batch byte offsets; the
+// result is the segment's word sum with words starting at s (mod 2^32).
+
+// Dense: the wave's segments lie in [R0, R0 + R) (R0 16-byte aligned). The
+// region is cut into 32-byte granules, lane l of pass p holds granule
+// 64p + l. P(g) = even/odd byte sums of granules [0, g], a wave-wide running
+// prefix. Segment sum over granules [gs, ge) = P(ge-1) - P(gs-1), corrected by
+// the head granule's bytes before s and the tail granule's bytes before e
+// (each lane loads those two granules itself).
+// One pass of the dense stream into a granule slot: kGran raw-buffer loads
+// (16 bytes per lane each, consecutive lanes -> consecutive 32-byte granules)
+// written in place ("+v": the slot keeps its registers across the loop, so
+// the stream needs no register rotation and no drain at the loop edge).
+// Issued as inline asm, which the compiler's wait-count pass does not see:
+// dense_segment_sums waits for the slots itself (slot_wait).
+__device__ __forceinline__ void slot_load(u32x4 (&c)[kGran], __amdgpu_buffer_rsrc_t rs, uint32_t vo,
+                                          uint32_t soff) {
+  asm volatile("buffer_load_dwordx4 %0, %1, %2, %3 offen nt" : "+v"(c[0]) : "v"(vo), "s"(rs), "s"(soff) : "memory");
+  if (kGran > 1)
+    asm volatile("buffer_load_dwordx4 %0, %1, %2, %3 offen offset:16 nt"
+                 : "+v"(c[kGran > 1 ? 1 : 0]) : "v"(vo), "s"(rs), "s"(soff) : "memory");
+  if (kGran > 2) {
+    asm volatile("buffer_load_dwordx4 %0, %1, %2, %3 offen offset:32 nt"
+                 : "+v"(c[kGran > 2 ? 2 : 0]) : "v"(vo), "s"(rs), "s"(soff) : "memory");
+    asm volatile("buffer_load_dwordx4 %0, %1, %2, %3 offen offset:48 nt"
+                 : "+v"(c[kGran > 3 ? 3 : 0]) : "v"(vo), "s"(rs), "s"(soff) : "memory");
+  }
+}
+// All but the youngest N vector-memory loads of this wave have completed.
+template <int N>
+__device__ __forceinline__ void slot_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int D>
+__device__ __forceinline__ uint32_t dense_segment_sums(const KParams& P, uint64_t R0, uint32_t R, bool job,
+                                                       uint64_t s, uint64_t e, uint32_t lane) {
+  // whole 16-byte chunks: the range check zeroes a 16-byte load that
+  // crosses the record limit, not just its bytes past it
+  const __amdgpu_buffer_rsrc_t rs = rsrc(P.data + R0, (R + 15) & ~15u);
+  const uint32_t rsl = job ? (uint32_t)(s - R0) : 0u, rel = job ? (uint32_t)(e - R0) : 0u;
+  // head / tail granules, summed before the stream starts (their wait must
+  // not drain the stream)
+  uint32_t E = 0, O = 0;
+  {
+    Gran hg, tg;
+    const uint32_t hoff = rsl & ~(kGranBytes - 1), toff = rel & ~(kGranBytes - 1);
+#pragma unroll
+    for (int k = 0; k < kGran; k++) {
+      hg.c[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, hoff + 16 * k, 0, 0);
+      tg.c[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, toff + 16 * k, 0, 0);
+    }
+    uint32_t hE = 0, hO = 0;
+    gran_eo_below(tg, rel & (kGranBytes - 1), E, O);
+    gran_eo_below(hg, rsl & (kGranBytes - 1), hE, hO);
+    E -= hE;
+    O -= hO;
+  }
+  const uint32_t np = (R + kPassBytes - 1) / kPassBytes;  // wave-uniform
+  const uint32_t vo = lane * kGranBytes;
+  Gran ring[D];
+#pragma unroll
+  for (int d = 0; d < D; d++) {
+#pragma unroll
+    for (int k = 0; k < kGran; k++) ring[d].c[k] = u32x4{0, 0, 0, 0};
+    slot_load(ring[d].c, rs, vo, d * kPassBytes);
+  }
+  // granule-sum targets: prefix through granule gs-1 (a) and ge-1 (b); -1 = empty prefix
+  const int32_t a = (int32_t)(rsl / kGranBytes) - 1, b = (int32_t)(rel / kGranBytes) - 1;
+  uint32_t cE = 0, cO = 0;
+  // E, O += P(ge-1) - P(gs-1) as the passes go. Whole rounds of D passes, no
+  // branch inside (passes past the region read range-checked zeros and change
+  // nothing); each slot is consumed, then refilled at once.
+  for (uint32_t p0 = 0; p0 < np; p0 += D) {
+#pragma unroll
+    for (int d = 0; d < D; d++) {
+      const uint32_t p = p0 + d;
+      slot_wait<(D - 1) * kGran>();  // slot d's loads are the oldest in flight
+      uint32_t gE = 0, gO = 0;
+      gran_eo(ring[d], gE, gO);
+      slot_load(ring[d].c, rs, vo, (p + D) * kPassBytes);
+      const uint32_t sE = wave_scan(gE), sO = wave_scan(gO);
+      const uint32_t PE = sE + cE, PO = sO + cO;
+      const int32_t ia = a - (int32_t)(64 * p), ib = b - (int32_t)(64 * p);
+      const uint32_t xaE = (uint32_t)__builtin_amdgcn_ds_bpermute(ia << 2, (int)PE);
+      const uint32_t xaO = (uint32_t)__builtin_amdgcn_ds_bpermute(ia << 2, (int)PO);
+      const uint32_t xbE = (uint32_t)__builtin_amdgcn_ds_bpermute(ib << 2, (int)PE);
+      const uint32_t xbO = (uint32_t)__builtin_amdgcn_ds_bpermute(ib << 2, (int)PO);
+      const bool ina = (uint32_t)ia < 64u, inb = (uint32_t)ib < 64u;
+      E += (inb ? xbE : 0u) - (ina ? xaE : 0u);
+      O += (inb ? xbO : 0u) - (ina ? xaO : 0u);
+      cE += readlane32(sE, 63);
+      cO += readlane32(sO, 63);
+    }
+  }
+  slot_wait<0>();  // the last round's refills (zeros) land before the slots' registers are reused
+  return (s & 1) ? (O << 8) + E : (E << 8) + O;
+}
+
+// Sparse: the segments one after another as whole-wave 1 KiB loads (16 bytes
+// per lane, consecutive lanes -> consecutive chunks), GPK_PB_SDEPTH always in
+// flight; at a segment's last load its even/odd sums are reduced across the
+// wave into the owning lane. Each segment is streamed over whole chunks
+// [s & ~15, e & ~15); its partial first and last chunks are the lane's own.
+__device__ __forceinline__ uint32_t sparse_segment_sums(const KParams& P, bool job, uint64_t s, uint64_t e,
+                                                        uint32_t lane) {
+  const uint64_t fa = s & ~15ull, fe = e & ~15ull;
+  u32x4 hc = {0, 0, 0, 0}, tc = {0, 0, 0, 0};
+  if (job) hc = *reinterpret_cast<const u32x4*>(P.data + fa);
+  if (job && (e & 15)) tc = *reinterpret_cast<const u32x4*>(P.data + fe);
+  uint32_t E = 0, O = 0;
+  chunk_eo_below(tc, (uint32_t)(e & 15), E, O);
+  uint32_t hE = 0, hO = 0;
+  chunk_eo_below(hc, (uint32_t)(s & 15), hE, hO);
+  E -= hE;
+  O -= hO;
+  uint32_t own = (s & 1) ? (O << 8) + E : (E << 8) + O;
+  uint64_t pend = __ballot(job && fe > fa);
+  const uint32_t vo = lane * 16;
+  constexpr int D = GPK_PB_SDEPTH;
+  uint32_t p_lane = 64, p_off = 0, p_len = 0;  // producer (wave-uniform)
+  __amdgpu_buffer_rsrc_t p_rs = rsrc(P.data, 0);
+  u32x4 ring[D];
+  uint32_t r_lane[D], r_last[D];
+  const uint32_t par = (uint32_t)(s & 1);
+#pragma unroll
+  for (int k = 0; k < D; k++) {
+    if (p_off >= p_len) {
+      p_lane = 64;
+      p_off = p_len = 0;
+      uint64_t b0 = 0;
+      if (pend) {
+        p_lane = (uint32_t)__builtin_ctzll(pend);
+        pend &= pend - 1;
+        b0 = readlane64(fa, p_lane);
+        p_len = (uint32_t)(readlane64(fe, p_lane) - b0);
+      }
+      p_rs = rsrc(P.data + b0, p_len);
+    }
+    ring[k] = bload(p_rs, vo, p_off);
+    r_lane[k] = p_lane;
+    r_last[k] = p_off + 1024 >= p_len;
+    p_off += 1024;
+  }
+  uint32_t sE = 0, sO = 0;
+  for (;;) {
+    uint32_t live = 0;
+#pragma unroll
+    for (int k = 0; k < D; k++) {
+      if (r_lane[k] < 64) {
+        chunk_eo(ring[k], sE, sO);
+        if (r_last[k]) {
+          const uint32_t pr = readlane32(par, r_lane[k]);
+          const uint32_t t = wave_sum(pr ? (sO << 8) + sE : (sE << 8) + sO);
+          if (lane == r_lane[k]) own += t;
+          sE = sO = 0;
+        }
+      }
+      if (p_off >= p_len) {
+        p_lane = 64;
+        p_off = p_len = 0;
+        uint64_t b0 = 0;
+        if (pend) {
+          p_lane = (uint32_t)__builtin_ctzll(pend);
+          pend &= pend - 1;
+          b0 = readlane64(fa, p_lane);
+          p_len = (uint32_t)(readlane64(fe, p_lane) - b0);
+        }
+        p_rs = rsrc(P.data + b0, p_len);
+      }
+      ring[k] = bload(p_rs, vo, p_off);
+      r_lane[k] = p_lane;
+      r_last[k] = p_off + 1024 >= p_len;
+      p_off += 1024;
+      live |= r_lane[k] < 64;
+    }
+    if (!live) break;
+  }
+  return own;
+}
+
+// Word sums of every job lane's segment [s, e): dense prefix stream when the
+// wave's segments share a compact region, else the per-segment stream.
+template <int D>
+__device__ __forceinline__ uint32_t segment_sums(const KParams& P, bool job, uint64_t s, uint64_t e, uint32_t lane) {
+  const uint64_t jobs = __ballot(job);
+  if (!jobs) return 0;
+  // region relative to a wave-uniform base (the first job lane's chunk), in
+  // 32-bit biased coordinates; lanes too far from it make the wave sparse
+  const uint64_t B = readlane64(s, (uint32_t)__builtin_ctzll(jobs)) & ~15ull;
+  constexpr uint64_t kBias = 0x80000000ull;
+  const uint64_t bs = s + kBias - B, be = e + kBias - B;
+  const bool far = job && (bs >> 32 || be >> 32);
+  const uint32_t lo = wave_min(job ? (uint32_t)bs : 0xffffffffu);
+  const uint32_t hi = wave_max(job ? (uint32_t)be : 0u);
+  const uint32_t tot = wave_sum(job ? (uint32_t)(e - s) : 0u);
+  const uint32_t lo16 = lo & ~15u;
+  const bool dense = !__ballot(far) && hi - lo16 <= 4u * tot + 8192u;
+  if (dense) return dense_segment_sums<D>(P, B + lo16 - kBias, hi - lo16, job, s, e, lane);
+  return sparse_segment_sums(P, job, s, e, lane);
+}
+
+template <bool kL4, bool kLayout, class TT, bool kKeys, int W, int O>
 __device__ __forceinline__ void decode_packet(const KParams& P, const TT& T, uint64_t i, bool active, uint64_t off,
                                               uint32_t cl, uint32_t slot_dw, uint32_t lane) {
   const uint32_t m = (uint32_t)(off & 15);
@@ -387,23 +536,17 @@ __device__ __forceinline__ void decode_packet(const KParams& P, const TT& T, uin
   Parse q;
   q.init();
   Outcome s{0, 0, 0, 0};
-#if GPK_FAST
   bool done = false;
   if (active && P.fast) done = fast_parser(P, T, r, cl, q, s);
   if (active && !done) s = run_parser<false>(P, T, r, cl, q);
-#else
-  if (active) s = run_parser<false>(P, T, r, cl, q);
-#endif
 
   uint32_t st = (s.err & GPK_ST_ERR_MASK) | (s.trunc ? GPK_ST_TRUNCATED : 0u) |
                 ((q.nlayers > GPK_ST_NLAYERS_MASK ? GPK_ST_NLAYERS_MASK : q.nlayers) << GPK_ST_NLAYERS_SHIFT);
   uint32_t ip4c = 0, l4c = 0;
-  uint64_t lflow = 0, nflow = 0, tflow = 0;
 
-  // L4 checksum: bytes of the segment inside the LDS window are summed here;
-  // the rest, [ja, je) of data, is a job for the wave-cooperative phase B.
-  uint64_t ja = 0, je = 0;
-  uint32_t jsum = 0, jexist = 0, jpar = 0;
+  // L4 checksum job: segment [js, je) of the batch, pseudo-header sum jinit
+  uint64_t js = 0, je = 0;
+  uint32_t jinit = 0, jexist = 0;
   bool job = false;
 
   if (active) {
@@ -415,71 +558,23 @@ __device__ __forceinline__ void decode_packet(const KParams& P, const TT& T, uin
       st |= GPK_ST_IP4_CSUM | (ip4c == existing ? GPK_ST_IP4_VALID : 0u);
     }
     const uint32_t tk = q.transport, nk = q.last_net;
-    if ((P.outputs & GPK_OUT_L4_CSUM) && tk && clean(q, tk) && nk && clean(q, nk)) {
-      // tcp.go:626-640 / udp.go:144-158 via tcpip.go:54-69
-      uint32_t t0 = q.start(tk);
-      uint32_t blen = tk == GPK_DEC_TCP ? q.end(tk) - t0 : q.udp_hlen;
-      uint32_t ns = q.start(nk);
+    if (kL4 && (P.outputs & GPK_OUT_L4_CSUM) && tk && clean(q, tk) && nk && clean(q, nk)) {
+      // tcp.go:626-640 / udp.go:144-158 via tcpip.go:54-69: bytes = Contents
+      // + Payload as decoded, csum = pseudo-header + proto + length
+      const uint32_t t0 = q.start(tk);
+      const uint32_t blen = tk == GPK_DEC_TCP ? q.end(tk) - t0 : q.udp_hlen;
+      const uint32_t ns = q.start(nk);
       uint32_t init = nk == GPK_DEC_IPV4 ? sum_words(r, ns + 12, 8) : sum_words(r, ns + 8, 32);
       init += (tk == GPK_DEC_TCP ? 6u : 17u) + (blen & 0xffff) + (blen >> 16);
+      jinit = init;
       jexist = rd16(r, t0 + (tk == GPK_DEC_TCP ? 16 : 6));
       st |= GPK_ST_L4_CSUM | (tk == GPK_DEC_UDP ? GPK_ST_L4_UDP : 0u);
-      uint32_t tend = t0 + blen;
-      uint32_t in_end = tend < win ? tend : win;
-      uint32_t part = t0 < in_end ? sum_words_lds(r.lb + t0, in_end - t0) : 0u;
-      if (tend <= win) {
-        l4c = fold(init + part - jexist);
-      } else if (kL4) {
-        // Remainder [ra, re) past the window: its partial first / last
-        // 16-byte chunks are summed here, the full chunks in phase B.
-        const uint64_t ra = off + (t0 > win ? t0 : win), re = off + tend;
-        const uint32_t par = (uint32_t)((off + t0) & 1);
-        const uint64_t fa = (ra + 15) & ~15ull, fe = re & ~15ull;
-        uint32_t edge = 0;
-#if GPK_LINE_OWN
-        // head: the window's last line after the window, summed at load time
-        // (LineOwn sums in this lane's LDS slot; the next packet's in lane+1's,
-        // written by that lane of this wave before the parse)
-        const uint32_t own_h = gpk_smem[slot_dw + kOwnDw], own_hx = gpk_smem[slot_dw + kOwnDw + 2];
-        const uint32_t nx_t = gpk_smem[slot_dw + kSlotDw + kOwnDw + 1];
-        const bool nx_tok = lane < 63 && (gpk_smem[slot_dw + kSlotDw + kOwnDw + 2] & 256u);
-        const uint64_t he = off + (own_hx & 255u);
-        const bool head_ok = t0 <= win && he > ra && he <= re;
-        const uint64_t bs = head_ok ? he : fa;
-        if (head_ok) edge += par ? ((own_h >> 16) << 8) + (own_h & 0xffff) : ((own_h & 0xffff) << 8) + (own_h >> 16);
-        // tail: the next packet's line head, summed by lane+1 (which saw this
-        // packet end exactly at its start)
-        const uint64_t nl0 = re & ~127ull;
-        const bool tail_ok = nx_tok && re == off + cl && nl0 >= bs && fa <= fe;
-        const uint64_t be = tail_ok ? nl0 : fe;
-        if (tail_ok) edge += par ? ((nx_t >> 16) << 8) + (nx_t & 0xffff) : ((nx_t & 0xffff) << 8) + (nx_t >> 16);
-        if (fa > fe) {  // remainder inside a single chunk
-          edge = chunk_sum(ld16(P.data + (ra & ~15ull)), ra & ~15ull, ra, re, par);
-        } else {
-          if (!head_ok && ra != fa) edge += chunk_sum(ld16(P.data + (ra & ~15ull)), ra & ~15ull, ra, re, par);
-          if (!tail_ok && re != fe) edge += chunk_sum(ld16(P.data + fe), fe, ra, re, par);
-        }
-        jsum = init + part + edge;
-        job = bs < be;
-        ja = bs;
-        je = be;
-#else
-        if (fa > fe) {  // remainder inside a single chunk
-          edge = chunk_sum(ld16(P.data + (ra & ~15ull)), ra & ~15ull, ra, re, par);
-        } else {
-          if (ra != fa) edge += chunk_sum(ld16(P.data + (ra & ~15ull)), ra & ~15ull, ra, re, par);
-          if (re != fe) edge += chunk_sum(ld16(P.data + fe), fe, ra, re, par);
-        }
-        jsum = init + part + edge;
-        job = fa < fe;
-        ja = fa;
-        je = fe;
-#endif
-        jpar = par;
-        if (!job) l4c = fold(jsum - jexist);
-      }
+      js = off + t0;
+      je = js + blen;
+      job = true;
     }
     if (P.outputs & GPK_OUT_FLOWS) {
+      uint64_t lflow = 0, nflow = 0, tflow = 0;
       if (clean(q, GPK_DEC_ETHERNET)) {  // ethernet.go:38-40 (EndpointMAC = 3)
         uint32_t e0 = q.start(GPK_DEC_ETHERNET);
         lflow = flow_hash(fnv_range(r, e0 + 6, 6), fnv_range(r, e0, 6), 3);
@@ -500,153 +595,16 @@ __device__ __forceinline__ void decode_packet(const KParams& P, const TT& T, uin
         tflow = flow_hash(fnv_range(r, t0, 2), fnv_range(r, t0 + 2, 2), tk == GPK_DEC_TCP ? 4 : 5);
         st |= GPK_ST_TRANSPORT_FLOW;
       }
+      if (P.flows) {
+        P.flows[i] = lflow;
+        P.flows[P.n + i] = nflow;
+        P.flows[2 * P.n + i] = tflow;
+      }
     }
   }
 
-  // ---- Phase B: L4 segments past the window, one packet per wave pass ------
-  // The wave takes up to four pending packets at a time; every lane loads
-  // 16-byte chunks of each (consecutive lanes -> consecutive chunks: whole
-  // cache lines per wave instruction), two 1 KiB rounds in flight per packet,
-  // then each packet's partial sums are reduced across the wave (DPP row
-  // rotations + four readlanes) into the owning lane. No LDS traffic.
-  if (kL4) {
-    uint32_t extra = 0;
-    uint64_t pend = __ballot(job);
-#if GPK_PB_STREAM
-    // The wave's pending segments as one stream of 1 KiB wave loads (items),
-    // packet after packet, GPK_PB_DEPTH items always in flight: a register
-    // ring, refilled as each item is consumed. Item = one raw-buffer load of
-    // 16 bytes per lane from the packet's remaining whole chunks; bytes past
-    // the packet's end come back as zeros (range check), so no predicates.
-    const uint32_t vo = lane * 16;
-    constexpr int D = GPK_PB_DEPTH;
-    uint32_t p_lane = 64, p_off = 0, p_len = 0;  // producer (wave-uniform)
-    __amdgpu_buffer_rsrc_t p_rs = __builtin_amdgcn_make_buffer_rsrc((void*)P.data, 0, 0, 0x00020000);
-    u32x4 ring[D];
-    uint32_t r_lane[D], r_last[D];
-#pragma unroll
-    for (int k = 0; k < D; k++) {
-      if (p_off >= p_len) {
-        p_lane = 64;
-        p_off = p_len = 0;
-        uint64_t b0 = 0;
-        if (pend) {
-          p_lane = (uint32_t)__builtin_ctzll(pend);
-          pend &= pend - 1;
-          b0 = readlane64(ja, p_lane);
-          p_len = (uint32_t)(readlane64(je, p_lane) - b0);
-        }
-        p_rs = __builtin_amdgcn_make_buffer_rsrc((void*)(P.data + b0), 0, GPK_PB_NULL ? 0 : p_len, 0x00020000);
-      }
-      ring[k] = __builtin_amdgcn_raw_buffer_load_b128(p_rs, vo, p_off, GPK_NT_B ? 2 : 0);
-      r_lane[k] = p_lane;
-      r_last[k] = p_off + 1024 >= p_len;
-      p_off += 1024;
-    }
-    uint32_t E = 0, O = 0;
-    for (;;) {
-      uint32_t live = 0;
-#pragma unroll
-      for (int k = 0; k < D; k++) {
-        if (r_lane[k] < 64) {
-          const u32x4 x = ring[k];
-          chunk_eo(make_uint4(x.x, x.y, x.z, x.w), E, O);
-          if (r_last[k]) {
-            const uint32_t pr = readlane32(jpar, r_lane[k]);
-            const uint32_t t = wave_sum(pr ? (O << 8) + E : (E << 8) + O);
-            if (lane == r_lane[k]) extra += t;
-            E = O = 0;
-          }
-        }
-        if (p_off >= p_len) {
-          p_lane = 64;
-          p_off = p_len = 0;
-          uint64_t b0 = 0;
-          if (pend) {
-            p_lane = (uint32_t)__builtin_ctzll(pend);
-            pend &= pend - 1;
-            b0 = readlane64(ja, p_lane);
-            p_len = (uint32_t)(readlane64(je, p_lane) - b0);
-          }
-          p_rs = __builtin_amdgcn_make_buffer_rsrc((void*)(P.data + b0), 0, GPK_PB_NULL ? 0 : p_len, 0x00020000);
-        }
-        ring[k] = __builtin_amdgcn_raw_buffer_load_b128(p_rs, vo, p_off, GPK_NT_B ? 2 : 0);
-        r_lane[k] = p_lane;
-        r_last[k] = p_off + 1024 >= p_len;
-        p_off += 1024;
-        live |= r_lane[k] < 64;
-      }
-      if (!live) break;
-    }
-#else
-    const uint32_t vo = lane * 16;
-    while (pend) {
-      constexpr int G = GPK_PB_G;
-      uint32_t jl[G];
-      uint32_t len[G];
-      __amdgpu_buffer_rsrc_t rs[G];
-      uint32_t pr[G];
-#pragma unroll
-      for (int g = 0; g < G; g++) {
-        jl[g] = 64;
-        len[g] = 0;  // empty slot: a zero-record descriptor, every load returns 0
-        pr[g] = 0;
-        uint64_t b0 = 0;
-        if (pend) {
-          uint32_t j = (uint32_t)__builtin_ctzll(pend);
-          pend &= pend - 1;
-          jl[g] = j;
-          b0 = readlane64(ja, j);
-          len[g] = (uint32_t)(readlane64(je, j) - b0);
-          pr[g] = readlane32(jpar, j);
-        }
-        // [b0, b0+len) as a raw buffer: loads past its end return zeros
-        // (hardware range check), so no lane needs a predicate or a mask
-        rs[g] = __builtin_amdgcn_make_buffer_rsrc((void*)(P.data + b0), 0, len[g], 0x00020000);
-      }
-      uint32_t E[G], O[G];
-#pragma unroll
-      for (int g = 0; g < G; g++) E[g] = O[g] = 0;
-      uint32_t maxlen = 0;
-#pragma unroll
-      for (int g = 0; g < G; g++) maxlen = len[g] > maxlen ? len[g] : maxlen;
-      for (uint32_t rr = 0; rr < maxlen; rr += 2048) {
-        u32x4 v[G][2];
-#pragma unroll
-        for (int g = 0; g < G; g++)
-#pragma unroll
-          for (int h = 0; h < 2; h++)
-            v[g][h] = __builtin_amdgcn_raw_buffer_load_b128(rs[g], vo + h * 1024, rr, GPK_NT_B ? 2 : 0);
-#pragma unroll
-        for (int g = 0; g < G; g++)
-#pragma unroll
-          for (int h = 0; h < 2; h++) chunk_eo(make_uint4(v[g][h].x, v[g][h].y, v[g][h].z, v[g][h].w), E[g], O[g]);
-      }
-#pragma unroll
-      for (int g = 0; g < G; g++) {
-        if (jl[g] < 64) {
-          uint32_t t = wave_sum(pr[g] ? (O[g] << 8) + E[g] : (E[g] << 8) + O[g]);
-          if (lane == jl[g]) extra += t;
-        }
-      }
-    }
-#endif
-    if (job) l4c = fold(jsum + extra - jexist);
-  }
-  if (active && (st & GPK_ST_L4_CSUM)) {
-    bool udp = (st & GPK_ST_L4_UDP) != 0;
-    if (l4c == jexist || (udp && jexist == 0)) st |= GPK_ST_L4_VALID;
-  }
-
-  // ---- outputs ---------------------------------------------------------------
+  // ---- outputs that do not wait for phase B (their registers die here) ------
   if (active) {
-    uint4 rec = make_uint4((uint32_t)q.layers, (uint32_t)(q.layers >> 32), st, ip4c | (l4c << 16));
-    reinterpret_cast<uint4*>(P.records)[i] = rec;
-    if (P.flows) {
-      P.flows[i] = lflow;
-      P.flows[P.n + i] = nflow;
-      P.flows[2 * P.n + i] = tflow;
-    }
     if (s.err && P.err_args) {
       P.err_args[2 * i] = s.a0;
       P.err_args[2 * i + 1] = s.a1;
@@ -670,7 +628,7 @@ __device__ __forceinline__ void decode_packet(const KParams& P, const TT& T, uin
     }
     if (kLayout) {
       const int slot_kind[8] = {GPK_DEC_ETHERNET, GPK_DEC_DOT1Q, GPK_DEC_IPV4, GPK_DEC_IPV6,
-                                       GPK_DEC_IPV6_EXT, GPK_DEC_TCP,  GPK_DEC_UDP,  GPK_DEC_PAYLOAD};
+                                GPK_DEC_IPV6_EXT, GPK_DEC_TCP,   GPK_DEC_UDP,  GPK_DEC_PAYLOAD};
       uint32_t so[8], eo[8];
 #pragma unroll
       for (int k = 0; k < 8; k++) {
@@ -687,76 +645,24 @@ __device__ __forceinline__ void decode_packet(const KParams& P, const TT& T, uin
       L[3] = make_uint4(eo[4], eo[5], eo[6], eo[7]);
     }
   }
-}
+  const uint32_t lay_lo = (uint32_t)q.layers, lay_hi = (uint32_t)(q.layers >> 32);
 
-// Persistent, software-pipelined over tiles of kBlock packets: block b takes
-// tiles b, b+grid, b+2*grid, ... (grid = resident blocks, gpk_launch_decode).
-// While tile t is decoded, the header windows of tile t+grid are in flight
-// (registers) and the offsets/caplens of tile t+2*grid too, so the global
-// load latency of the read-once header bytes is hidden behind decode work.
-// The LDS slot is lane-private: no barrier between tiles.
-template <bool kL4, bool kLayout, class TT, bool kKeys = false>
-__device__ __forceinline__ void decode_tiles(const KParams& P, const TT& T) {
-  const uint32_t tid = threadIdx.x;
-  const uint32_t lane = tid & 63;
-  const uint32_t slot_dw = tid * kSlotDw;
-  const uint64_t ntiles = (P.n + kBlock - 1) / kBlock;
-  [[maybe_unused]] const uint64_t stride = gridDim.x;
-  uint64_t t = blockIdx.x;
-  if (t >= ntiles) return;  // uniform over the block
-
-  uint64_t i = t * kBlock + tid;
-#if GPK_PREFETCH
-  Idx cur = load_index(P, i);
-  uint32_t nc = win_chunks(cur, i < P.n);
-  Win w;
-  load_window(P, cur, nc, w);
-  Idx nxt = load_index(P, i + stride * kBlock);
-  for (;;) {
-    store_window(slot_dw, nc, w);
-    const uint64_t i1 = i + stride * kBlock;
-    const uint32_t nc1 = win_chunks(nxt, i1 < P.n);
-    load_window(P, nxt, nc1, w);                         // tile t+grid, in flight
-    const Idx nn = load_index(P, i1 + stride * kBlock);  // tile t+2*grid
-    decode_packet<kL4, kLayout, TT, kKeys>(P, T, i, i < P.n, cur.off, cur.cl, slot_dw, lane);
-    t += stride;
-    if (t >= ntiles) break;
-    i = i1;
-    cur = nxt;
-    nc = nc1;
-    nxt = nn;
+  // ---- Phase B: segment sums ---------------------------------------------
+  if (kL4) {
+    const uint32_t sum = segment_sums<(O >= 7 ? 2 : GPK_PB_DEPTH)>(P, job, js, je, lane);
+    if (job) {
+      l4c = fold(jinit + sum - jexist);
+      const bool udp = (st & GPK_ST_L4_UDP) != 0;
+      if (l4c == jexist || (udp && jexist == 0)) st |= GPK_ST_L4_VALID;
+    }
   }
-#elif !GPK_PERSISTENT
-  {  // one tile per block
-    const Idx cur = load_index(P, i);
-    const uint32_t nc = win_chunks(cur, i < P.n);
-    Win w;
-    load_window(P, cur, nc, w);
-    store_window(slot_dw, nc, w);
-    decode_packet<kL4, kLayout, TT, kKeys>(P, T, i, i < P.n, cur.off, cur.cl, slot_dw, lane);
-  }
-#else
-  Idx nxt = load_index(P, i);
-  for (;;) {
-    const Idx cur = nxt;
-    const uint32_t nc = win_chunks(cur, i < P.n);
-    Win w;
-    load_window(P, cur, nc, w);
-    nxt = load_index(P, i + stride * kBlock);  // next tile's offsets/caplens
-    store_window(slot_dw, nc, w);
-    decode_packet<kL4, kLayout, TT, kKeys>(P, T, i, i < P.n, cur.off, cur.cl, slot_dw, lane);
-    t += stride;
-    if (t >= ntiles) break;
-    i += stride * kBlock;
-  }
-#endif
+  if (active) reinterpret_cast<uint4*>(P.records)[i] = make_uint4(lay_lo, lay_hi, st, ip4c | (l4c << 16));
 }
 
 // kCompact: the parser's lookup tables are copied into LDS once per block
 // (after the header-window slots) and every NextLayerType lookup is an LDS
 // read; otherwise they are read from the global DevTables. Either way the
-// only vector-memory traffic of the decode is the packet bytes themselves,
-// so waiting on a lookup never waits on the next tile's prefetch.
+// only vector-memory traffic of the decode is the packet bytes themselves.
 // W: header-window chunks. The 5-chunk default holds Ethernet + two tags +
 // IPv6 + TCP; parsers with no Dot1Q/IPv6/TCP decoder and no L4 checksum (C2)
 // run a 4-chunk window whose smaller LDS slot and 64-VGPR budget give 8 waves
@@ -764,79 +670,30 @@ __device__ __forceinline__ void decode_tiles(const KParams& P, const TT& T) {
 // O: waves per SIMD the register budget is cut for. Batches of small packets
 // (mean < 1 KiB) are issue-bound in the header phase and run O = 7 (72 VGPRs;
 // with the table blob sized to the parser, 7 blocks fit a CU's LDS); big
-// packets keep O = 6 (A/B r02c: C4 -5.9 %, C1 -4.9 %, C3 +0.5 % at 7).
+// packets keep O = 6.
 template <bool kL4, bool kLayout, bool kCompact, bool kKeys = false, int W = kWinChunks, int O = GPK_WAVES_PER_EU>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W == 4 ? GPK_W4_WAVES : O, 8))) void decode_kernel(
     KParams P) {
-  if ((uint64_t)blockIdx.x * kBlock * GPK_PPL >= P.n) return;  // uniform over the block
-#if !GPK_PERSISTENT && !GPK_PREFETCH
-  // GPK_PPL tiles per block, one packet of each per lane: every packet's
-  // index, then every header window (the first in LDS, the others held in
-  // registers) and the table blob are in flight together, so the two
-  // dependent memory round trips are paid once for GPK_PPL packets.
+  if ((uint64_t)blockIdx.x * kBlock >= P.n) return;  // uniform over the block
+  // Every packet's index, then its header window and the table blob are in
+  // flight together: two dependent memory round trips per packet.
   const uint32_t tid = threadIdx.x;
   const uint32_t slot_dw = tid * slot_dw_of<W>();
-  const uint64_t i0 = (uint64_t)blockIdx.x * (kBlock * GPK_PPL) + tid, i1 = i0 + kBlock;
-  static_assert(GPK_PPL == 1 || GPK_PPL == 2, "GPK_PPL is 1 or 2");
+  const uint64_t i0 = (uint64_t)blockIdx.x * kBlock + tid;
   const Idx c0 = load_index(P, i0);
-  const Idx c1 = GPK_PPL == 2 ? load_index(P, i1) : Idx{0, 0};
   const uint32_t n0 = win_chunks<W>(c0, i0 < P.n);
-  const uint32_t n1 = GPK_PPL == 2 ? win_chunks<W>(c1, i1 < P.n) : 0;
-  WinT<W> w0, w1;
+  WinT<W> w0;
   load_window(P, c0, n0, w0);
-  if (GPK_PPL == 2) load_window(P, c1, n1, w1);
   const uint32_t base = kBlock * slot_dw_of<W>();
   if (kCompact) {
     for (uint32_t k = tid; k < P.cg.words; k += kBlock) gpk_smem[base + k] = P.ctab[k];
     __syncthreads();
   }
-#ifndef GPK_OWN_EARLY
-#define GPK_OWN_EARLY 0  // 1: issue the line-ownership loads with the window loads
-#endif
-#if GPK_LINE_OWN && GPK_OWN_EARLY
-  LineOwn own{0, 0, 0};
-  if (kL4) {
-    const uint64_t poff = shfl_up64(c0.off, 1);
-    const uint32_t pcl = (uint32_t)__shfl_up((int)c0.cl, 1);
-    const bool prev_ok = (tid & 63) > 0 && poff + pcl == c0.off && poff <= (c0.off & ~127ull);
-    own = line_own(P, c0.off, c0.cl, n0, w0.v[0], i0 < P.n, prev_ok);
-  }
-#endif
   store_window(slot_dw, n0, w0);
-#if GPK_LINE_OWN
-  if (kL4) {
-#if !GPK_OWN_EARLY
-    const uint64_t poff = shfl_up64(c0.off, 1);
-    const uint32_t pcl = (uint32_t)__shfl_up((int)c0.cl, 1);
-    const bool prev_ok = (tid & 63) > 0 && poff + pcl == c0.off && poff <= (c0.off & ~127ull);
-    const LineOwn own = line_own(P, c0.off, c0.cl, n0, w0.v[0], i0 < P.n, prev_ok);
-#endif
-    gpk_smem[slot_dw + kOwnDw] = own.h;
-    gpk_smem[slot_dw + kOwnDw + 1] = own.t;
-    gpk_smem[slot_dw + kOwnDw + 2] = own.hx;
-  }
-#endif
   if (kCompact)
-    decode_packet<kL4, kLayout, LTab, kKeys, W>(P, LTab{P.cg, base}, i0, i0 < P.n, c0.off, c0.cl, slot_dw, tid & 63);
+    decode_packet<kL4, kLayout, LTab, kKeys, W, O>(P, LTab{P.cg, base}, i0, i0 < P.n, c0.off, c0.cl, slot_dw, tid & 63);
   else
-    decode_packet<kL4, kLayout, GTab, kKeys, W>(P, GTab{P.tab}, i0, i0 < P.n, c0.off, c0.cl, slot_dw, tid & 63);
-  if (GPK_PPL == 2) {
-    store_window(slot_dw, n1, w1);  // lane-private slot, reused
-    if (kCompact)
-      decode_packet<kL4, kLayout, LTab, kKeys, W>(P, LTab{P.cg, base}, i1, i1 < P.n, c1.off, c1.cl, slot_dw, tid & 63);
-    else
-      decode_packet<kL4, kLayout, GTab, kKeys, W>(P, GTab{P.tab}, i1, i1 < P.n, c1.off, c1.cl, slot_dw, tid & 63);
-  }
-#else
-  if (kCompact) {
-    const uint32_t base = kBlock * kSlotDw;
-    for (uint32_t w = threadIdx.x; w < P.cg.words; w += kBlock) gpk_smem[base + w] = P.ctab[w];
-    __syncthreads();
-    decode_tiles<kL4, kLayout, LTab, kKeys>(P, LTab{P.cg, base});
-  } else {
-    decode_tiles<kL4, kLayout, GTab, kKeys>(P, GTab{P.tab});
-  }
-#endif
+    decode_packet<kL4, kLayout, GTab, kKeys, W, O>(P, GTab{P.tab}, i0, i0 < P.n, c0.off, c0.cl, slot_dw, tid & 63);
 }
 
 // Full decoded list of one packet (lists longer than the 16 inline codes).
@@ -859,63 +716,58 @@ template <bool kL4, bool kLayout, bool kCompact, bool kKeys = false, int W = gpk
 hipError_t launch(const gpk::KParams* P, hipStream_t stream) {
   using namespace gpk;
   constexpr int slot_lds = kBlock * slot_dw_of<W>() * 4;
-#if GPK_LDS_FIT
   // the table blob takes only the words this parser's tables use (C3/C4: ~1.5 KB of 2.9)
   const int lds = kCompact ? slot_lds + (int)((P->cg.words + 127) & ~127u) * 4 : slot_lds;
-#else
-  constexpr int lds = kCompact ? slot_lds + kCtDwords * 4 : slot_lds;
-#endif
-  // Resident blocks per CU for this specialisation (cached per device).
-  static int cached_bpc[64], cached_cus[64];  // per instantiation
-  int dev = 0;
-  hipError_t e = hipGetDevice(&dev);
-  if (e != hipSuccess) return e;
-  if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
-  if (!cached_bpc[dev]) {
-    int bpc = 0, cus = 0;
-    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, decode_kernel<kL4, kLayout, kCompact, kKeys, W, O>, kBlock,
-                                                     lds);
-    if (e != hipSuccess) return e;
-    e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    if (e != hipSuccess) return e;
-    cached_cus[dev] = cus > 0 ? cus : 1;
-    cached_bpc[dev] = bpc > 0 ? bpc : 1;
-  }
-  // 8 rounds of resident blocks: if the occupancy figure is one block per CU
-  // high, the static tile schedule loses ~3% instead of running a second
-  // generation of late blocks; each block still pipelines >= 8 tiles.
-  const uint64_t ntiles = (P->n + kBlock - 1) / kBlock;
-  uint64_t grid = (uint64_t)cached_cus[dev] * cached_bpc[dev] * 8;
-  if (ntiles < grid * 8) grid = (ntiles + 7) / 8;
-  if (!GPK_PERSISTENT && !GPK_PREFETCH) grid = (ntiles + GPK_PPL - 1) / GPK_PPL;
-  if (grid < 1) grid = 1;
+  const uint64_t grid = (P->n + kBlock - 1) / kBlock;
+  if (grid > 0xffffffffull) return hipErrorInvalidValue;
   hipLaunchKernelGGL((decode_kernel<kL4, kLayout, kCompact, kKeys, W, O>), dim3((unsigned)grid), dim3(kBlock), lds,
                      stream, *P);
   return hipGetLastError();
 }
 
-template <bool kCompact>
-hipError_t launch_outputs(const gpk::KParams* P, int with_l4, int with_layout, hipStream_t stream) {
-  if (P->key_kind) {  // fused grouping keys: no layouts (gpk_decode_group_batch)
-    if (with_layout) return hipErrorInvalidValue;
-    return with_l4 ? launch<true, false, kCompact, true>(P, stream) : launch<false, false, kCompact, true>(P, stream);
+// The specialisation a launch uses (gpk_launch_decode, gpk_launch_name).
+struct Sel {
+  bool l4, layout, compact, keys;
+  int W, O;
+};
+Sel select(const gpk::KParams* P, int with_l4, int with_layout) {
+  Sel s{with_l4 != 0, with_layout != 0, P->ctab != nullptr, P->key_kind != 0, gpk::kWinChunks, GPK_WAVES_PER_EU};
+  if (s.keys) {  // fused grouping keys: no layouts (gpk_decode_group_batch)
+    s.layout = false;
+  } else if (!s.l4 && !s.layout && P->small_headers) {
+    s.W = 4;
+  } else if (!s.layout && !P->big_packets) {
+    s.O = 7;
   }
-  if (!with_l4 && !with_layout && P->small_headers) return launch<false, false, kCompact, false, 4>(P, stream);
+  return s;
+}
+
+template <bool kCompact>
+hipError_t launch_sel(const gpk::KParams* P, const Sel& s, hipStream_t stream) {
   constexpr int W = gpk::kWinChunks;
-  if (with_l4 && with_layout) return launch<true, true, kCompact>(P, stream);
-  if (with_l4)
-    return P->big_packets ? launch<true, false, kCompact>(P, stream) : launch<true, false, kCompact, false, W, 7>(P, stream);
-  if (!with_layout && !P->big_packets) return launch<false, false, kCompact, false, W, 7>(P, stream);
-  if (with_layout) return launch<false, true, kCompact>(P, stream);
-  return launch<false, false, kCompact>(P, stream);
+  if (s.keys) return s.l4 ? launch<true, false, kCompact, true>(P, stream) : launch<false, false, kCompact, true>(P, stream);
+  if (s.W == 4) return launch<false, false, kCompact, false, 4>(P, stream);
+  if (s.l4 && s.layout) return launch<true, true, kCompact>(P, stream);
+  if (s.l4) return s.O == 7 ? launch<true, false, kCompact, false, W, 7>(P, stream) : launch<true, false, kCompact>(P, stream);
+  if (s.layout) return launch<false, true, kCompact>(P, stream);
+  return s.O == 7 ? launch<false, false, kCompact, false, W, 7>(P, stream) : launch<false, false, kCompact>(P, stream);
 }
 
 }  // namespace
 
 extern "C" hipError_t gpk_launch_decode(const gpk::KParams* P, int with_l4, int with_layout, hipStream_t stream) {
   if (P->n == 0) return hipSuccess;
-  return P->ctab ? launch_outputs<true>(P, with_l4, with_layout, stream)
-                 : launch_outputs<false>(P, with_l4, with_layout, stream);
+  if (P->key_kind && with_layout) return hipErrorInvalidValue;
+  const Sel s = select(P, with_l4, with_layout);
+  return s.compact ? launch_sel<true>(P, s, stream) : launch_sel<false>(P, s, stream);
+}
+
+// Name of the kernel specialisation gpk_launch_decode would launch.
+extern "C" int gpk_launch_describe(const gpk::KParams* P, int with_l4, int with_layout, char* buf, size_t cap) {
+  const Sel s = select(P, with_l4, with_layout);
+  return snprintf(buf, cap, "gpk::decode_kernel<%s,%s,%s,%s,%d,%d>", s.l4 ? "true" : "false",
+                  s.layout ? "true" : "false", s.compact ? "true" : "false", s.keys ? "true" : "false", s.W,
+                  s.W == 4 ? 6 : s.O);
 }
 
 extern "C" hipError_t gpk_launch_list(const gpk::KParams* P, uint64_t index, int64_t* out, uint32_t cap,

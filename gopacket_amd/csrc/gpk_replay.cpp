@@ -364,7 +364,8 @@ extern "C" int gpk_replay_file(gpk_ctx* ctx, const gpk_parser* parser, const cha
         pl.free_bats.push_back(b);
         break;
       }
-      gpk_batch db{S.dev, B.d_off, B.d_cap, n, len + 16};
+      // data_bytes: the batch's span in the slot as the mean-packet-size hint (gpk.h)
+      gpk_batch db{S.dev, B.d_off, B.d_cap, n, n ? B.h_off[n - 1] + B.h_cap[n - 1] - B.h_off[0] : 0};
       gpk_results dr{B.d_rec, B.d_err, B.d_flow, nullptr};
       int drc = gpk_decode_batch(ctx, parser, &db, &dr, S.stream);
       if (drc) {

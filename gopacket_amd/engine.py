@@ -120,6 +120,16 @@ class Context:
             sp = stream.cuda_stream
         check(lib().gpk_decode_batch(self.h, parser.h, ctypes.byref(b), ctypes.byref(r), sp))
 
+    def kernel_name(self, parser, data, offsets, caplens, layouts=False):
+        """The decode kernel specialisation decode_device launches for this
+        parser and batch (gpk_decode_kernel_name): the name rocprofv3 lists."""
+        b = _lib.Batch(data.data_ptr(), offsets.data_ptr(), caplens.data_ptr(), offsets.numel(), data.numel())
+        buf = ctypes.create_string_buffer(256)
+        n = lib().gpk_decode_kernel_name(self.h, parser.h, ctypes.byref(b), int(layouts), buf, 256)
+        if n < 0:
+            raise _lib.GpkError("gpk_decode_kernel_name: %d" % n)
+        return buf.value.decode()
+
     def replay_file(self, parser, path, fmt=0, ng_flags=0, slot_bytes=0, slots=0, batch_pkts=0, read_threads=0,
                     collect=True, on_batch=None):
         """gpk_replay_file: the whole capture through HBM (BASELINE config C5).

@@ -40,6 +40,8 @@ def max_over_ranks(x, world, device=None):
         return x
     import torch
     import torch.distributed as dist
+    if dist.get_backend() == "gloo":
+        device = None  # gloo reduces host tensors
     t = torch.tensor([float(x)], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())

@@ -241,9 +241,15 @@ int gpk_ctx_destroy(gpk_ctx* ctx);
 int gpk_ctx_set_table_mode(gpk_ctx* ctx, int mode);
 
 /* A packed, offset-indexed packet batch. Packet i is data[offsets[i] ..
- * offsets[i]+caplens[i]). In gpk_decode_batch every pointer is DEVICE memory.
- * The kernels may read whole 16-byte-aligned chunks that contain a packet
- * byte; they never touch a chunk that contains none. */
+ * offsets[i]+caplens[i]). In gpk_decode_batch every pointer is DEVICE memory;
+ * data must be 16-byte aligned.
+ * Reads: whole 16-byte-aligned chunks of data. Every chunk read lies between
+ * the first and the last byte of the packets of one group of 64 consecutive
+ * packets (a wave), so data must be one allocation covering all packets.
+ * data_bytes: the size of data in bytes (gpk_decode_batch_host copies that
+ * many). gpk_decode_batch uses it only as a hint of the mean packet size
+ * (data_bytes / n selects a kernel variant; 0 = unknown): pass the summed
+ * capture lengths (or the packed buffer size) for best results. */
 typedef struct gpk_batch {
   const uint8_t* data;
   const uint64_t* offsets;
@@ -265,6 +271,13 @@ typedef struct gpk_results {
  * launch. The parser configuration is uploaded once per (ctx, parser change). */
 int gpk_decode_batch(gpk_ctx* ctx, const gpk_parser* p, const gpk_batch* batch,
                      const gpk_results* out, void* stream);
+
+/* Diagnostic: the name of the kernel specialisation gpk_decode_batch launches
+ * for this parser and batch (with or without layouts), e.g.
+ * "gpk::decode_kernel<true,false,true,false,5,6>" — the name rocprofv3 lists.
+ * Returns the name's length. */
+int gpk_decode_kernel_name(gpk_ctx* ctx, const gpk_parser* p, const gpk_batch* batch, int with_layouts,
+                           char* buf, size_t cap);
 
 /* Host-memory variant: batch and results live in host memory (ideally pinned
  * via gpk_host_alloc). Copies HtoD, decodes, copies DtoH; synchronous. */

@@ -1,0 +1,233 @@
+/* A C-language caller of the drop-in boundary, the way the cgo package in
+ * INTEGRATION.md uses it: only include/gpk.h, linked with -lgpk.
+ *
+ *   gpk_abi_test host <golden dir>     no GPU: struct layouts, error texts,
+ *                                      LayerType names, code mapping
+ *   gpk_abi_test decode <golden dir>   decodes the golden packets with
+ *                                      gpk_decode_batch_host under two parser
+ *                                      configurations and compares records,
+ *                                      error arguments, flow hashes and the
+ *                                      Go error text with the committed
+ *                                      expectations (tools/make_c_abi_golden.py)
+ * Exit status 0 = every check passed. */
+#include <stddef.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "gpk.h"
+
+/* the layouts cgo sees (INTEGRATION.md's Go structs mirror these offsets) */
+_Static_assert(sizeof(gpk_record) == 16, "gpk_record is 16 bytes");
+_Static_assert(offsetof(gpk_record, status) == 8, "status at 8");
+_Static_assert(offsetof(gpk_record, ip4_csum) == 12, "ip4_csum at 12");
+_Static_assert(offsetof(gpk_record, l4_csum) == 14, "l4_csum at 14");
+_Static_assert(sizeof(gpk_layout) == 64, "gpk_layout is 64 bytes");
+_Static_assert(sizeof(gpk_batch) == 40, "gpk_batch is 5 words");
+_Static_assert(sizeof(gpk_results) == 32, "gpk_results is 4 pointers");
+
+static int failures = 0;
+#define CHECK(c, ...)                            \
+  do {                                           \
+    if (!(c)) {                                  \
+      fprintf(stderr, "FAIL %s:%d: ", __FILE__, __LINE__); \
+      fprintf(stderr, __VA_ARGS__);              \
+      fprintf(stderr, "\n");                     \
+      failures++;                                \
+    }                                            \
+  } while (0)
+
+static void* slurp(const char* dir, const char* name, size_t* len) {
+  char path[4096];
+  snprintf(path, sizeof(path), "%s/%s", dir, name);
+  FILE* f = fopen(path, "rb");
+  if (!f) {
+    fprintf(stderr, "cannot open %s\n", path);
+    exit(2);
+  }
+  fseek(f, 0, SEEK_END);
+  long n = ftell(f);
+  fseek(f, 0, SEEK_SET);
+  void* p = malloc((size_t)n + 1);
+  if (fread(p, 1, (size_t)n, f) != (size_t)n) exit(2);
+  fclose(f);
+  ((char*)p)[n] = 0;
+  *len = (size_t)n;
+  return p;
+}
+
+static void host_checks(void) {
+  char buf[256];
+  CHECK(gpk_abi_version() == GPK_ABI_VERSION, "abi version %d", gpk_abi_version());
+  /* parser.go:325-327 and layer names (layertype.go:101-111) */
+  gpk_format_error(GPK_ERR_UNSUPPORTED, GPK_LT_PAYLOAD, 0, buf, sizeof(buf));
+  CHECK(strcmp(buf, "No decoder for layer type Payload") == 0, "[%s]", buf);
+  gpk_format_error(GPK_ERR_UNSUPPORTED, 107, 0, buf, sizeof(buf));
+  CHECK(strcmp(buf, "No decoder for layer type DNS") == 0, "[%s]", buf);
+  /* tcp_test.go:173-188: "MPTCP bad option length 0" */
+  gpk_format_error(GPK_ERR_MPTCP_LEN, 0, 0, buf, sizeof(buf));
+  CHECK(strcmp(buf, "MPTCP bad option length 0") == 0, "[%s]", buf);
+  /* ip4_test.go:102-113 */
+  gpk_format_error(GPK_ERR_IP4_OPT_BADLEN, 131, 2, buf, sizeof(buf));
+  CHECK(strcmp(buf, "Invalid IP option type 131 length 2. Must be greater than 2") == 0, "[%s]", buf);
+  /* panicToError parser.go:329-333 */
+  gpk_format_error(GPK_ERR_PANIC_INDEX, 3, 3, buf, sizeof(buf));
+  CHECK(strcmp(buf, "panic: runtime error: index out of range [3] with length 3") == 0, "[%s]", buf);
+  /* truncation to cap: NUL-terminated, full length returned */
+  char small[8];
+  int n = gpk_format_error(GPK_ERR_ETH_TOO_SMALL, 0, 0, small, sizeof(small));
+  CHECK(n == (int)strlen("Ethernet packet too small") && strlen(small) == 7, "truncation n=%d [%s]", n, small);
+  gpk_layer_type_name(GPK_LT_ETHERNET, buf, sizeof(buf));
+  CHECK(strcmp(buf, "Ethernet") == 0, "[%s]", buf);
+  gpk_layer_type_name(12345, buf, sizeof(buf));
+  CHECK(strcmp(buf, "12345") == 0, "[%s]", buf);
+  CHECK(gpk_code_layer_type(GPK_CODE_TCP) == GPK_LT_TCP, "code map");
+  CHECK(gpk_code_layer_type(GPK_CODE_FRAGMENT) == GPK_LT_FRAGMENT, "code map");
+  CHECK(gpk_code_layer_type(13) == -1, "code map bound");
+  CHECK(strcmp(gpk_strerror(GPK_EINVAL), "invalid argument") == 0, "strerror");
+  /* parser configuration needs no device */
+  gpk_parser* p = NULL;
+  CHECK(gpk_parser_create(&p, GPK_LT_ETHERNET) == GPK_OK && p, "parser_create");
+  CHECK(gpk_parser_add_decoder(p, GPK_DEC_TCP) == GPK_OK, "add TCP");
+  CHECK(gpk_parser_decoder_for(p, GPK_LT_TCP) == GPK_DEC_TCP, "decoder_for");
+  CHECK(gpk_parser_add_decoder(p, 99) == GPK_EUNSUPP, "unknown decoder kind");
+  CHECK(gpk_parser_set_outputs(p, 0x8) == GPK_EINVAL, "bad outputs");
+  CHECK(gpk_parser_set_tcp_port(p, 70000, 2) == GPK_EINVAL, "port range");
+  gpk_parser_destroy(p);
+}
+
+static gpk_parser* make_parser(int cfg) {
+  static const int stats[] = {GPK_DEC_ETHERNET, GPK_DEC_DOT1Q, GPK_DEC_IPV4, GPK_DEC_IPV6,
+                              GPK_DEC_IPV6_EXT, GPK_DEC_TCP,   GPK_DEC_UDP,  GPK_DEC_PAYLOAD};
+  static const int simple[] = {GPK_DEC_ETHERNET, GPK_DEC_IPV4, GPK_DEC_TCP, GPK_DEC_PAYLOAD};
+  gpk_parser* p = NULL;
+  if (gpk_parser_create(&p, GPK_LT_ETHERNET) != GPK_OK) return NULL;
+  const int* d = cfg == 0 ? stats : simple;
+  int nd = cfg == 0 ? 8 : 4;
+  for (int k = 0; k < nd; k++) gpk_parser_add_decoder(p, d[k]);
+  gpk_parser_set_outputs(p, GPK_OUT_ALL);
+  return p;
+}
+
+static int decode_checks(const char* dir) {
+  size_t plen, elen, tlen;
+  uint8_t* pk = (uint8_t*)slurp(dir, "packets.bin", &plen);
+  uint8_t* ex = (uint8_t*)slurp(dir, "expect.bin", &elen);
+  char* txt = (char*)slurp(dir, "errors.txt", &tlen);
+  uint32_t n;
+  memcpy(&n, pk, 4);
+  /* pack contiguously into pinned memory, as a capture source would */
+  size_t pos = 4, total = 0;
+  for (uint32_t i = 0; i < n; i++) {
+    uint32_t c;
+    memcpy(&c, pk + pos, 4);
+    pos += 4 + c;
+    total += c;
+  }
+  uint8_t* data;
+  uint64_t* off;
+  uint32_t* cap;
+  gpk_record* rec;
+  uint32_t* err;
+  uint64_t* fl;
+  if (gpk_host_alloc((void**)&data, total + 64) || gpk_host_alloc((void**)&off, 8 * (size_t)n) ||
+      gpk_host_alloc((void**)&cap, 4 * (size_t)n) || gpk_host_alloc((void**)&rec, 16 * (size_t)n) ||
+      gpk_host_alloc((void**)&err, 8 * (size_t)n) || gpk_host_alloc((void**)&fl, 24 * (size_t)n)) {
+    fprintf(stderr, "gpk_host_alloc: %s\n", gpk_last_hip_error());
+    return 2;
+  }
+  memset(data, 0, total + 64);
+  pos = 4;
+  size_t o = 0;
+  for (uint32_t i = 0; i < n; i++) {
+    memcpy(&cap[i], pk + pos, 4);
+    memcpy(data + o, pk + pos + 4, cap[i]);
+    off[i] = o;
+    o += cap[i];
+    pos += 4 + cap[i];
+  }
+  gpk_ctx* ctx = NULL;
+  int rc = gpk_ctx_create(&ctx, 0);
+  if (rc) {
+    fprintf(stderr, "gpk_ctx_create: %s %s\n", gpk_strerror(rc), gpk_last_hip_error());
+    return 2;
+  }
+  const char* names[2] = {"statsassembly", "eth_ip4_tcp_payload"};
+  const size_t per = (size_t)n * (16 + 8 + 24);
+  CHECK(elen == 2 * per, "expect.bin size %zu", elen);
+  for (int cfg = 0; cfg < 2; cfg++) {
+    gpk_parser* p = make_parser(cfg);
+    gpk_batch b = {data, off, cap, n, total};
+    memset(err, 0, 8 * (size_t)n);
+    gpk_results r = {rec, err, fl, NULL};
+    rc = gpk_decode_batch_host(ctx, p, &b, &r);
+    CHECK(rc == GPK_OK, "decode %s: %s %s", names[cfg], gpk_strerror(rc), gpk_last_hip_error());
+    const uint8_t* e = ex + cfg * per;
+    int bad = 0;
+    for (uint32_t i = 0; i < n && bad < 5; i++) {
+      if (memcmp(&rec[i], e + 16 * (size_t)i, 16) != 0) {
+        CHECK(0, "%s packet %u: record differs", names[cfg], i);
+        bad++;
+        continue;
+      }
+      const uint32_t* ea = (const uint32_t*)(e + 16 * (size_t)n) + 2 * (size_t)i;
+      if (gpk_record_err(&rec[i]) && (err[2 * i] != ea[0] || err[2 * i + 1] != ea[1])) {
+        CHECK(0, "%s packet %u: err_args differ", names[cfg], i);
+        bad++;
+      }
+    }
+    CHECK(memcmp(fl, e + 24 * (size_t)n, 24 * (size_t)n) == 0, "%s: flow hashes differ", names[cfg]);
+    /* the Go error text of every packet that failed */
+    char want_prefix[64];
+    snprintf(want_prefix, sizeof(want_prefix), "%s ", names[cfg]);
+    int texts = 0;
+    for (char* line = txt; line && *line;) {
+      char* nl = strchr(line, '\n');
+      if (nl) *nl = 0;
+      if (strncmp(line, want_prefix, strlen(want_prefix)) == 0) {
+        char* q = line + strlen(want_prefix);
+        uint32_t i = (uint32_t)strtoul(q, &q, 10);
+        q++;
+        char got[512];
+        CHECK(i < n, "index");
+        gpk_format_error(gpk_record_err(&rec[i]), err[2 * i], err[2 * i + 1], got, sizeof(got));
+        CHECK(strcmp(got, q) == 0, "%s packet %u: [%s] vs [%s]", names[cfg], i, got, q);
+        texts++;
+      }
+      if (nl) *nl = '\n';
+      line = nl ? nl + 1 : NULL;
+    }
+    printf("%s: %u packets, %d error texts checked\n", names[cfg], n, texts);
+    gpk_parser_destroy(p);
+  }
+  gpk_ctx_destroy(ctx);
+  gpk_host_free(data);
+  gpk_host_free(off);
+  gpk_host_free(cap);
+  gpk_host_free(rec);
+  gpk_host_free(err);
+  gpk_host_free(fl);
+  free(pk);
+  free(ex);
+  free(txt);
+  return 0;
+}
+
+int main(int argc, char** argv) {
+  if (argc < 3) {
+    fprintf(stderr, "usage: %s host|decode <golden dir>\n", argv[0]);
+    return 2;
+  }
+  host_checks();
+  if (strcmp(argv[1], "decode") == 0) {
+    int rc = decode_checks(argv[2]);
+    if (rc) return rc;
+  }
+  if (failures) {
+    fprintf(stderr, "%d check(s) failed\n", failures);
+    return 1;
+  }
+  printf("gpk C ABI: all checks passed (%s)\n", argv[1]);
+  return 0;
+}

@@ -233,3 +233,27 @@ def test_port_traffic_hits_table_entries(gpu_ctx):
         pk.append(b"\x02" * 12 + b"\x08\x00" + ip + struct.pack(">HHHH", port, 7, 11, 0) + b"abc")
     dev, ref = run_both(gpu_ctx, cfg, pk)
     assert_same(dev, ref, "many_ports keys")
+
+
+@pytest.mark.parametrize("layout", ["sparse4k", "shuffled", "reversed"])
+def test_phase_b_layouts(gpu_ctx, layout):
+    """The L4 segment sums take the dense prefix stream when a wave's segments
+    share a compact region and the per-segment stream otherwise: packets 4 KiB
+    apart (sparse), packets in shuffled or reversed order inside one packed
+    buffer (dense, unordered) must all give the oracle's results."""
+    packets = pktutil.fuzz_packets(4242, 12000) + golden_packets()
+    if layout == "sparse4k":
+        data, off, cap = pktutil.pack(packets, align=4096)
+    else:
+        data, off, cap = pktutil.pack(packets)
+        order = np.arange(len(packets))
+        if layout == "shuffled":
+            order = np.random.default_rng(9).permutation(len(packets))
+        else:
+            order = order[::-1].copy()
+        off, cap = off[order], cap[order]
+    for name in ("statsassembly", "eth_ip4_tcp_payload", "raw_ip6"):
+        cfg = CONFIGS[name]
+        dev = gpu_ctx.decode_host(device_parser(cfg), data, off, cap, layouts=True)
+        ref = oracle_parser(cfg).decode(data, off, cap, nthreads=8, layouts=True)
+        assert_same(dev, ref, "%s/%s" % (layout, name))
