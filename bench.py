@@ -50,6 +50,8 @@ CONFIGS = {
 for _o in (1, 3, 5):
     CONFIGS["c4x%d" % _o] = dict(CONFIGS["c4"], outputs=_o, workload="C4 packets, outputs %d (diagnostic)" % _o)
 CONFIGS["c1x1"] = dict(CONFIGS["c1"], outputs=1, workload="C1 packets, IPv4 checksum only (diagnostic)")
+CONFIGS["c4x0"] = dict(CONFIGS["c4"], outputs=0, workload="C4 packets, decode only (diagnostic)")
+CONFIGS["c2x0"] = dict(CONFIGS["c2"], outputs=0, workload="C2 packets, decode only (diagnostic)")
 # BASELINE configs[3] as written: ONE 64M IMIX batch split across the ranks at byte-balanced
 # cuts (shard.byte_balanced_bounds; strong scaling, run by default when world > 1)
 CONFIGS["c4s"] = dict(CONFIGS["c4"], strong=True,

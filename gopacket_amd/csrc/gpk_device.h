@@ -117,16 +117,31 @@ struct Rd {
   uint32_t win;      // packet bytes present in LDS
 };
 
+// Four LDS bytes from any byte address: one ds_read_b32 (gfx950 serves
+// unaligned LDS dword reads exactly: tools/probes/lds_unaligned.hip, 64/64
+// byte offsets on MI355X). A read may run up to 3 bytes past the bytes a
+// caller uses (into the next slot or the table blob; past the allocation
+// the hardware returns zeros); those bytes are never used.
+typedef uint32_t u32_ua __attribute__((aligned(1)));
+__device__ __forceinline__ uint32_t lds32u(uint32_t byte_addr) {
+  return *reinterpret_cast<const u32_ua*>(reinterpret_cast<const uint8_t*>(gpk_smem) + byte_addr);
+}
+// big-endian 16 / 32 bits of the four bytes w = b0 | b1 << 8 | ... (v_perm_b32)
+__device__ __forceinline__ uint32_t be16_of(uint32_t w) { return __builtin_amdgcn_perm(0u, w, 0x0c0c0001u); }
+__device__ __forceinline__ uint32_t be32_of(uint32_t w) { return __builtin_amdgcn_perm(0u, w, 0x00010203u); }
+
 __device__ __forceinline__ uint32_t rd8(const RdL& r, uint32_t p) { return lds8(r.lb + p); }
 __device__ __forceinline__ uint32_t rd8(const Rd& r, uint32_t p) {
   return p < r.win ? lds8(r.lb + p) : (uint32_t)r.g[p];
 }
-template <class R>
-__device__ __forceinline__ uint32_t rd16(const R& r, uint32_t p) {
+__device__ __forceinline__ uint32_t rd16(const RdL& r, uint32_t p) { return be16_of(lds32u(r.lb + p)); }
+__device__ __forceinline__ uint32_t rd32(const RdL& r, uint32_t p) { return be32_of(lds32u(r.lb + p)); }
+__device__ __forceinline__ uint32_t rd16(const Rd& r, uint32_t p) {
+  if (p + 2 <= r.win) return rd16(RdL{r.lb}, p);
   return (rd8(r, p) << 8) | rd8(r, p + 1);
 }
-template <class R>
-__device__ __forceinline__ uint32_t rd32(const R& r, uint32_t p) {
+__device__ __forceinline__ uint32_t rd32(const Rd& r, uint32_t p) {
+  if (p + 4 <= r.win) return rd32(RdL{r.lb}, p);
   return (rd16(r, p) << 16) | rd16(r, p + 2);
 }
 
@@ -784,7 +799,10 @@ __device__ __forceinline__ bool fast_parser(const KParams& P, const TT& T, const
     if (len < 20 || off + 20 > W) return false;
     const uint32_t ds = (rd8(rl, off + 12) >> 4) * 4;
     if (ds < 20 || ds > len || off + ds > W) return false;
-    for (uint32_t p = off + 20, e = off + ds; p < e;) {  // options: EOL, NOP, TLV
+    // the common option block NOP, NOP, Timestamps (kind 8, length 10) is
+    // well formed as it stands; anything else walks the TLVs
+    const bool nop_nop_ts = ds == 32 && lds32u(rl.lb + off + 20) == 0x0a080101u;
+    for (uint32_t p = off + 20, e = nop_nop_ts ? p : off + ds; p < e;) {  // options: EOL, NOP, TLV
       const uint32_t t = rd8(rl, p);
       if (t == 0) break;
       if (t == 1) {
@@ -868,9 +886,22 @@ __device__ __forceinline__ uint64_t fnv_bytes(const R& r, uint32_t p, uint32_t n
   for (uint32_t i = 0; i < n; i++) h = fnv_step(h, rd8(r, p + i));
   return h;
 }
-__device__ __forceinline__ uint64_t fnv_range(const Rd& r, uint32_t p, uint32_t n) {
-  if (p + n <= r.win) return fnv_bytes(RdL{r.lb}, p, n);
-  return fnv_bytes(r, p, n);
+// N bytes from the LDS window: dword reads, bytes taken in order
+template <int N>
+__device__ __forceinline__ uint64_t fnv_lds(uint32_t a) {
+  uint64_t h = 14695981039346656037ull;
+#pragma unroll
+  for (int k = 0; k < N; k += 4) {
+    const uint32_t w = lds32u(a + k);
+#pragma unroll
+    for (int j = 0; j < 4 && k + j < N; j++) h = fnv_step(h, (w >> (8 * j)) & 0xffu);
+  }
+  return h;
+}
+template <int N>
+__device__ __forceinline__ uint64_t fnv_range(const Rd& r, uint32_t p) {
+  if (p + N <= r.win) return fnv_lds<N>(r.lb + p);
+  return fnv_bytes(r, p, N);
 }
 // Flow.FastHash flows.go:167-174
 __device__ __forceinline__ uint64_t flow_hash(uint64_t hs, uint64_t hd, uint32_t typ) {

@@ -16,9 +16,9 @@
 //    even-/odd-address byte sums mod 2^32 in any order, bit-exactly:
 //    * dense waves (the usual packed batch: the wave's segments lie in one
 //      region not much larger than their total): the wave streams the whole
-//      region once, 2 KiB per pass (32 bytes per lane, coalesced raw-buffer
-//      loads), keeps a running wave-wide prefix sum of the even/odd byte sums
-//      per 32-byte granule (DPP scan), and every lane picks the prefix at its
+//      region once, 1 KiB per pass (16 bytes per lane, one coalesced
+//      raw-buffer load), keeps a running wave-wide prefix sum of the even/odd
+//      byte sums per 16-byte granule (DPP scan), and every lane picks the prefix at its
 //      segment's first and last granule with ds_bpermute. Segment sum =
 //      prefix difference - the head granule's bytes before s + the tail
 //      granule's bytes before e. No per-packet reduction, no per-packet SALU.
@@ -41,13 +41,20 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 #define GPK_W4_WAVES 8  // 4-chunk window kernel: 64 VGPRs
 #endif
 #ifndef GPK_PB_GRAN
-#define GPK_PB_GRAN 2  // dense phase B: 16-byte chunks per lane per pass (granule = 32 bytes)
+#define GPK_PB_GRAN 1  // dense phase B: 16-byte chunks per lane per pass (A/B r03: 1 KiB passes, whole
+                       // lines per load instruction, beat 2 KiB passes of two half-coalesced loads by 20 %)
 #endif
 #ifndef GPK_PB_DEPTH
-#define GPK_PB_DEPTH 3  // dense phase B: passes in flight (2 in the 72-VGPR kernels)
+#define GPK_PB_DEPTH 6  // dense phase B: passes in flight (80-VGPR kernels)
+#endif
+#ifndef GPK_PB_DEPTH7
+#define GPK_PB_DEPTH7 4  // ... in the 72-VGPR kernels (7 waves per SIMD)
 #endif
 #ifndef GPK_PB_SDEPTH
 #define GPK_PB_SDEPTH 4  // sparse phase B: 1 KiB wave loads in flight
+#endif
+#ifndef GPK_DIAG_NOPARSE
+#define GPK_DIAG_NOPARSE 0  // timing only: skip DecodeLayers (fixed layout)
 #endif
 #ifndef GPK_PB_NULL
 #define GPK_PB_NULL 0  // timing only: phase-B stream loads read nothing (zero-record descriptors)
@@ -74,27 +81,36 @@ __device__ __forceinline__ uint32_t dot_odd(uint32_t w, uint32_t acc) {
 }
 
 // Sum of big-endian 16-bit words over LDS bytes [q, q+n) (ComputeChecksum
-// with csum = 0, checksum.go:35-50; an odd tail byte counts <<8). Only the
-// first and last dword are masked; interior dwords are two dot4s each.
+// with csum = 0, checksum.go:35-50; an odd tail byte counts <<8): unaligned
+// dword reads starting at q, so byte q+4k is always a word's high byte; only
+// the last dword is masked.
 __device__ __forceinline__ uint32_t sum_words_lds(uint32_t q, uint32_t n) {
-  if (n == 0) return 0;
-  const uint32_t last = q + n - 1;
-  const uint32_t a0 = q & ~3u, a1 = last & ~3u;
-  const uint32_t mhi = 0xffffffffu >> (8 * (3 - (last & 3)));
-  uint32_t w = gpk_smem[a0 >> 2] & (0xffffffffu << (8 * (q & 3)));
-  if (a0 == a1) w &= mhi;
-  uint32_t E = dot_even(w, 0), O = dot_odd(w, 0);
-  for (uint32_t a = a0 + 4; a < a1; a += 4) {
-    w = gpk_smem[a >> 2];
+  uint32_t E = 0, O = 0;
+  const uint32_t nd = n >> 2, t = n & 3;
+  for (uint32_t k = 0; k < nd; k++) {
+    const uint32_t w = lds32u(q + 4 * k);
     E = dot_even(w, E);
     O = dot_odd(w, O);
   }
-  if (a1 != a0) {
-    w = gpk_smem[a1 >> 2] & mhi;
+  if (t) {
+    const uint32_t w = lds32u(q + 4 * nd) & (0xffffffffu >> (8 * (4 - t)));
     E = dot_even(w, E);
     O = dot_odd(w, O);
   }
-  return (q & 1) ? (O << 8) + E : (E << 8) + O;
+  return (E << 8) + O;
+}
+// Fixed-length form (IPv4 header without options, pseudo-header addresses).
+template <int N>
+__device__ __forceinline__ uint32_t sum_words_lds(uint32_t q) {
+  static_assert(N % 4 == 0, "whole dwords");
+  uint32_t E = 0, O = 0;
+#pragma unroll
+  for (int k = 0; k < N; k += 4) {
+    const uint32_t w = lds32u(q + k);
+    E = dot_even(w, E);
+    O = dot_odd(w, O);
+  }
+  return (E << 8) + O;
 }
 
 // Same over packet positions [p, p+n), from LDS when inside the window.
@@ -223,13 +239,14 @@ struct Idx {
   uint32_t cl;
 };
 
+// Branch-free prologue: every lane loads an index entry (lanes past the batch
+// re-read the last one) and all W window chunks (chunks past the packet's
+// window re-read its last window chunk, which holds a packet byte; a packet
+// with no window chunk reads the parser's table copy instead, 16 valid bytes
+// that are never used). No exec-mask juggling, one round trip each.
 __device__ __forceinline__ Idx load_index(const KParams& P, uint64_t i) {
-  Idx x{0, 0};
-  if (i < P.n) {
-    x.off = P.offsets[i];
-    x.cl = P.caplens[i];
-  }
-  return x;
+  const uint64_t j = i < P.n ? i : P.n - 1;
+  return Idx{P.offsets[j], P.caplens[j]};
 }
 
 template <int W>
@@ -242,22 +259,21 @@ __device__ __forceinline__ uint32_t win_chunks(const Idx& x, bool active) {
 
 template <int W>
 __device__ __forceinline__ void load_window(const KParams& P, const Idx& x, uint32_t nchunk, WinT<W>& w) {
-  const uint8_t* src = P.data + (x.off & ~15ull);
+  const uint8_t* src = nchunk ? P.data + (x.off & ~15ull) : reinterpret_cast<const uint8_t*>(P.tab);
+  const uint32_t last = nchunk ? nchunk - 1 : 0;
 #pragma unroll
-  for (int k = 0; k < W; k++)
-    if ((uint32_t)k < nchunk) w.v[k] = ld16(src + 16 * k);
+  for (int k = 0; k < W; k++) w.v[k] = ld16(src + 16 * ((uint32_t)k < last ? (uint32_t)k : last));
 }
 
 template <int W>
-__device__ __forceinline__ void store_window(uint32_t slot_dw, uint32_t nchunk, const WinT<W>& w) {
+__device__ __forceinline__ void store_window(uint32_t slot_dw, const WinT<W>& w) {
 #pragma unroll
-  for (int k = 0; k < W; k++)
-    if ((uint32_t)k < nchunk) {
-      gpk_smem[slot_dw + 4 * k + 0] = w.v[k].x;
-      gpk_smem[slot_dw + 4 * k + 1] = w.v[k].y;
-      gpk_smem[slot_dw + 4 * k + 2] = w.v[k].z;
-      gpk_smem[slot_dw + 4 * k + 3] = w.v[k].w;
-    }
+  for (int k = 0; k < W; k++) {
+    gpk_smem[slot_dw + 4 * k + 0] = w.v[k].x;
+    gpk_smem[slot_dw + 4 * k + 1] = w.v[k].y;
+    gpk_smem[slot_dw + 4 * k + 2] = w.v[k].z;
+    gpk_smem[slot_dw + 4 * k + 3] = w.v[k].w;
+  }
 }
 
 // The grouping key of gpk_flows.hip's key_kernel, derived here from the parse
@@ -326,13 +342,13 @@ __device__ __forceinline__ int derive_key(const KParams& P, const Rd& r, const P
 // result is the segment's word sum with words starting at s (mod 2^32).
 
 // Dense: the wave's segments lie in [R0, R0 + R) (R0 16-byte aligned). The
-// region is cut into 32-byte granules, lane l of pass p holds granule
+// region is cut into granules (16 bytes), lane l of pass p holds granule
 // 64p + l. P(g) = even/odd byte sums of granules [0, g], a wave-wide running
 // prefix. Segment sum over granules [gs, ge) = P(ge-1) - P(gs-1), corrected by
 // the head granule's bytes before s and the tail granule's bytes before e
 // (each lane loads those two granules itself).
 // One pass of the dense stream into a granule slot: kGran raw-buffer loads
-// (16 bytes per lane each, consecutive lanes -> consecutive 32-byte granules)
+// (16 bytes per lane each, consecutive lanes -> consecutive granules)
 // written in place ("+v": the slot keeps its registers across the loop, so
 // the stream needs no register rotation and no drain at the loop edge).
 // Issued as inline asm, which the compiler's wait-count pass does not see:
@@ -351,9 +367,18 @@ __device__ __forceinline__ void slot_load(u32x4 (&c)[kGran], __amdgpu_buffer_rsr
   }
 }
 // All but the youngest N vector-memory loads of this wave have completed.
+// The slot's registers are operands, so no use of them moves above the wait.
 template <int N>
-__device__ __forceinline__ void slot_wait() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+__device__ __forceinline__ void slot_wait(u32x4 (&c)[kGran]) {
+  if (kGran == 1)
+    asm volatile("s_waitcnt vmcnt(%1)" : "+v"(c[0]) : "n"(N) : "memory");
+  else if (kGran == 2)
+    asm volatile("s_waitcnt vmcnt(%2)" : "+v"(c[0]), "+v"(c[kGran > 1 ? 1 : 0]) : "n"(N) : "memory");
+  else
+    asm volatile("s_waitcnt vmcnt(%4)"
+                 : "+v"(c[0]), "+v"(c[kGran > 1 ? 1 : 0]), "+v"(c[kGran > 2 ? 2 : 0]), "+v"(c[kGran > 3 ? 3 : 0])
+                 : "n"(N)
+                 : "memory");
 }
 
 template <int D>
@@ -399,7 +424,7 @@ __device__ __forceinline__ uint32_t dense_segment_sums(const KParams& P, uint64_
 #pragma unroll
     for (int d = 0; d < D; d++) {
       const uint32_t p = p0 + d;
-      slot_wait<(D - 1) * kGran>();  // slot d's loads are the oldest in flight
+      slot_wait<(D - 1) * kGran>(ring[d].c);  // slot d's loads are the oldest in flight
       uint32_t gE = 0, gO = 0;
       gran_eo(ring[d], gE, gO);
       slot_load(ring[d].c, rs, vo, (p + D) * kPassBytes);
@@ -417,7 +442,8 @@ __device__ __forceinline__ uint32_t dense_segment_sums(const KParams& P, uint64_
       cO += readlane32(sO, 63);
     }
   }
-  slot_wait<0>();  // the last round's refills (zeros) land before the slots' registers are reused
+#pragma unroll
+  for (int d = 0; d < D; d++) slot_wait<0>(ring[d].c);  // the last refills land before the registers are reused
   return (s & 1) ? (O << 8) + E : (E << 8) + O;
 }
 
@@ -537,8 +563,25 @@ __device__ __forceinline__ void decode_packet(const KParams& P, const TT& T, uin
   q.init();
   Outcome s{0, 0, 0, 0};
   bool done = false;
+#if GPK_DIAG_NOPARSE  // timing only: a fixed Eth/IPv4/UDP|TCP layout, no decoding
+  if (active) {
+    q.s_eth = 0;
+    q.e_eth = cl;
+    q.s_ip4 = 14;
+    q.e_ip4 = cl;
+    q.last_net = GPK_DEC_IPV4;
+    q.transport = lds8(r.lb + 23) == 6 ? GPK_DEC_TCP : GPK_DEC_UDP;
+    q.s_tcp = q.s_udp = 34;
+    q.e_tcp = q.e_udp = cl;
+    q.udp_hlen = cl - 34;
+    q.layers = 0x931;
+    q.nlayers = 3;
+  }
+  (void)done;
+#else
   if (active && P.fast) done = fast_parser(P, T, r, cl, q, s);
   if (active && !done) s = run_parser<false>(P, T, r, cl, q);
+#endif
 
   uint32_t st = (s.err & GPK_ST_ERR_MASK) | (s.trunc ? GPK_ST_TRUNCATED : 0u) |
                 ((q.nlayers > GPK_ST_NLAYERS_MASK ? GPK_ST_NLAYERS_MASK : q.nlayers) << GPK_ST_NLAYERS_SHIFT);
@@ -554,7 +597,8 @@ __device__ __forceinline__ void decode_packet(const KParams& P, const TT& T, uin
       uint32_t s4 = q.start(GPK_DEC_IPV4);
       uint32_t hl = (rd8(r, s4) & 15) * 4;
       uint32_t existing = rd16(r, s4 + 10);
-      ip4c = fold(sum_words(r, s4, hl) - existing);
+      const uint32_t sum = hl == 20 && s4 + 20 <= win ? sum_words_lds<20>(r.lb + s4) : sum_words(r, s4, hl);
+      ip4c = fold(sum - existing);
       st |= GPK_ST_IP4_CSUM | (ip4c == existing ? GPK_ST_IP4_VALID : 0u);
     }
     const uint32_t tk = q.transport, nk = q.last_net;
@@ -564,7 +608,11 @@ __device__ __forceinline__ void decode_packet(const KParams& P, const TT& T, uin
       const uint32_t t0 = q.start(tk);
       const uint32_t blen = tk == GPK_DEC_TCP ? q.end(tk) - t0 : q.udp_hlen;
       const uint32_t ns = q.start(nk);
-      uint32_t init = nk == GPK_DEC_IPV4 ? sum_words(r, ns + 12, 8) : sum_words(r, ns + 8, 32);
+      uint32_t init;
+      if (nk == GPK_DEC_IPV4)
+        init = ns + 20 <= win ? sum_words_lds<8>(r.lb + ns + 12) : sum_words(r, ns + 12, 8);
+      else
+        init = ns + 40 <= win ? sum_words_lds<32>(r.lb + ns + 8) : sum_words(r, ns + 8, 32);
       init += (tk == GPK_DEC_TCP ? 6u : 17u) + (blen & 0xffff) + (blen >> 16);
       jinit = init;
       jexist = rd16(r, t0 + (tk == GPK_DEC_TCP ? 16 : 6));
@@ -577,28 +625,28 @@ __device__ __forceinline__ void decode_packet(const KParams& P, const TT& T, uin
       uint64_t lflow = 0, nflow = 0, tflow = 0;
       if (clean(q, GPK_DEC_ETHERNET)) {  // ethernet.go:38-40 (EndpointMAC = 3)
         uint32_t e0 = q.start(GPK_DEC_ETHERNET);
-        lflow = flow_hash(fnv_range(r, e0 + 6, 6), fnv_range(r, e0, 6), 3);
+        lflow = flow_hash(fnv_range<6>(r, e0 + 6), fnv_range<6>(r, e0), 3);
         st |= GPK_ST_LINK_FLOW;
       }
       if (nk && clean(q, nk)) {
         uint32_t ns = q.start(nk);
         if (nk == GPK_DEC_IPV4) {  // ip4.go:63-65 (EndpointIPv4 = 1)
-          nflow = flow_hash(fnv_range(r, ns + 12, 4), fnv_range(r, ns + 16, 4), 1);
+          nflow = flow_hash(fnv_range<4>(r, ns + 12), fnv_range<4>(r, ns + 16), 1);
         } else {  // ip6.go:49-51 (EndpointIPv6 = 2)
-          nflow = flow_hash(fnv_range(r, ns + 8, 16), fnv_range(r, ns + 24, 16), 2);
+          nflow = flow_hash(fnv_range<16>(r, ns + 8), fnv_range<16>(r, ns + 24), 2);
           st |= GPK_ST_NET_IPV6;
         }
         st |= GPK_ST_NET_FLOW;
       }
       if (tk && clean(q, tk)) {  // tcp.go:614-616 (4), udp.go:132-134 (5)
         uint32_t t0 = q.start(tk);
-        tflow = flow_hash(fnv_range(r, t0, 2), fnv_range(r, t0 + 2, 2), tk == GPK_DEC_TCP ? 4 : 5);
+        tflow = flow_hash(fnv_range<2>(r, t0), fnv_range<2>(r, t0 + 2), tk == GPK_DEC_TCP ? 4 : 5);
         st |= GPK_ST_TRANSPORT_FLOW;
       }
       if (P.flows) {
-        P.flows[i] = lflow;
-        P.flows[P.n + i] = nflow;
-        P.flows[2 * P.n + i] = tflow;
+        __builtin_nontemporal_store(lflow, P.flows + i);
+        __builtin_nontemporal_store(nflow, P.flows + P.n + i);
+        __builtin_nontemporal_store(tflow, P.flows + 2 * P.n + i);
       }
     }
   }
@@ -649,14 +697,15 @@ __device__ __forceinline__ void decode_packet(const KParams& P, const TT& T, uin
 
   // ---- Phase B: segment sums ---------------------------------------------
   if (kL4) {
-    const uint32_t sum = segment_sums<(O >= 7 ? 2 : GPK_PB_DEPTH)>(P, job, js, je, lane);
+    const uint32_t sum = segment_sums<(O >= 7 ? GPK_PB_DEPTH7 : GPK_PB_DEPTH)>(P, job, js, je, lane);
     if (job) {
       l4c = fold(jinit + sum - jexist);
       const bool udp = (st & GPK_ST_L4_UDP) != 0;
       if (l4c == jexist || (udp && jexist == 0)) st |= GPK_ST_L4_VALID;
     }
   }
-  if (active) reinterpret_cast<uint4*>(P.records)[i] = make_uint4(lay_lo, lay_hi, st, ip4c | (l4c << 16));
+  if (active)  // written once, never read back here: non-temporal
+    __builtin_nontemporal_store(u32x4{lay_lo, lay_hi, st, ip4c | (l4c << 16)}, reinterpret_cast<u32x4*>(P.records) + i);
 }
 
 // kCompact: the parser's lookup tables are copied into LDS once per block
@@ -685,11 +734,17 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W == 4 ?
   WinT<W> w0;
   load_window(P, c0, n0, w0);
   const uint32_t base = kBlock * slot_dw_of<W>();
-  if (kCompact) {
-    for (uint32_t k = tid; k < P.cg.words; k += kBlock) gpk_smem[base + k] = P.ctab[k];
+  if (kCompact) {  // the table blob (<= kCtDwords): clamped indices, duplicate writes of equal values
+    static_assert(kCtDwords <= 3 * kBlock, "three blob words per thread");
+    const uint32_t last = P.cg.words - 1;
+#pragma unroll
+    for (uint32_t k = 0; k < 3; k++) {
+      const uint32_t j = tid + k * kBlock < last ? tid + k * kBlock : last;
+      gpk_smem[base + j] = P.ctab[j];
+    }
     __syncthreads();
   }
-  store_window(slot_dw, n0, w0);
+  store_window(slot_dw, w0);
   if (kCompact)
     decode_packet<kL4, kLayout, LTab, kKeys, W, O>(P, LTab{P.cg, base}, i0, i0 < P.n, c0.off, c0.cl, slot_dw, tid & 63);
   else

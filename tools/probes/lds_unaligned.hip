@@ -12,9 +12,9 @@ __global__ void k(uint32_t* out) {
   out[a] = v == w;
 }
 int main() {
-  uint32_t* d; hipMalloc(&d, 256);
+  uint32_t* d; (void)hipMalloc(&d, 256);
   hipLaunchKernelGGL(k, dim3(1), dim3(64), 0, 0, d);
-  uint32_t h[64]; hipMemcpy(h, d, 256, hipMemcpyDeviceToHost);
+  uint32_t h[64]; (void)hipMemcpy(h, d, 256, hipMemcpyDeviceToHost);
   int ok = 0; for (int i = 0; i < 64; i++) ok += h[i];
   printf("unaligned ds_read_b32 exact on %d/64 byte offsets\n", ok);
   return 0;
