@@ -37,6 +37,9 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 #ifndef GPK_WAVES_PER_EU
 #define GPK_WAVES_PER_EU 6  // <= 80 VGPRs: 6 waves/SIMD, matching the 6 blocks per CU the LDS allows
 #endif
+#ifndef GPK_SMALL_WAVES
+#define GPK_SMALL_WAVES 7  // register budget of batches with a mean packet under 1 KiB (waves per SIMD)
+#endif
 #ifndef GPK_W4_WAVES
 #define GPK_W4_WAVES 8  // 4-chunk window kernel: 64 VGPRs
 #endif
@@ -150,6 +153,13 @@ __device__ __forceinline__ void chunk_eo_below(const u32x4& v, uint32_t n, uint3
   O = dot_odd(w2, O);
   E = dot_even(w3, E);
   O = dot_odd(w3, O);
+}
+
+// 16 bytes of an LDS window chunk (dword-aligned byte address; ~0 = none,
+// reads zeros at 0 then).
+__device__ __forceinline__ u32x4 lds_chunk(uint32_t a) {
+  const uint32_t* p = gpk_smem + ((a == ~0u ? 0u : a) >> 2);
+  return u32x4{p[0], p[1], p[2], p[3]};
 }
 
 // A granule: kGran consecutive 16-byte chunks.
@@ -383,25 +393,24 @@ __device__ __forceinline__ void slot_wait(u32x4 (&c)[kGran]) {
 
 template <int D>
 __device__ __forceinline__ uint32_t dense_segment_sums(const KParams& P, uint64_t R0, uint32_t R, bool job,
-                                                       uint64_t s, uint64_t e, uint32_t lane) {
+                                                       uint64_t s, uint64_t e, uint32_t lane, uint32_t hlds,
+                                                       uint32_t tlds) {
+  static_assert(kGran == 1, "head/tail chunks from the LDS window need 16-byte granules");
   // whole 16-byte chunks: the range check zeroes a 16-byte load that
   // crosses the record limit, not just its bytes past it
   const __amdgpu_buffer_rsrc_t rs = rsrc(P.data + R0, (R + 15) & ~15u);
   const uint32_t rsl = job ? (uint32_t)(s - R0) : 0u, rel = job ? (uint32_t)(e - R0) : 0u;
-  // head / tail granules, summed before the stream starts (their wait must
-  // not drain the stream)
+  // head / tail chunks, summed before the stream starts (their wait must
+  // not drain the stream): from the LDS header windows when a window holds
+  // them (hlds / tlds = LDS byte address, else ~0), else from memory
   uint32_t E = 0, O = 0;
   {
-    Gran hg, tg;
-    const uint32_t hoff = rsl & ~(kGranBytes - 1), toff = rel & ~(kGranBytes - 1);
-#pragma unroll
-    for (int k = 0; k < kGran; k++) {
-      hg.c[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, hoff + 16 * k, 0, 0);
-      tg.c[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, toff + 16 * k, 0, 0);
-    }
+    u32x4 hc = lds_chunk(hlds), tc = lds_chunk(tlds);
+    if (hlds == ~0u) hc = __builtin_amdgcn_raw_buffer_load_b128(rs, rsl & ~15u, 0, 0);
+    if (tlds == ~0u) tc = __builtin_amdgcn_raw_buffer_load_b128(rs, rel & ~15u, 0, 0);
     uint32_t hE = 0, hO = 0;
-    gran_eo_below(tg, rel & (kGranBytes - 1), E, O);
-    gran_eo_below(hg, rsl & (kGranBytes - 1), hE, hO);
+    chunk_eo_below(tc, rel & 15u, E, O);
+    chunk_eo_below(hc, rsl & 15u, hE, hO);
     E -= hE;
     O -= hO;
   }
@@ -414,34 +423,40 @@ __device__ __forceinline__ uint32_t dense_segment_sums(const KParams& P, uint64_
     for (int k = 0; k < kGran; k++) ring[d].c[k] = u32x4{0, 0, 0, 0};
     slot_load(ring[d].c, rs, vo, d * kPassBytes);
   }
-  // granule-sum targets: prefix through granule gs-1 (a) and ge-1 (b); -1 = empty prefix
+  // granule-sum targets: prefix through granule gs-1 (a) and ge-1 (b); -1 =
+  // the empty prefix. Target t sits in pass t >> 6 at lane t & 63: the
+  // ds_bpermute address is fixed, only the pass test changes.
   const int32_t a = (int32_t)(rsl / kGranBytes) - 1, b = (int32_t)(rel / kGranBytes) - 1;
-  uint32_t cE = 0, cO = 0;
-  // E, O += P(ge-1) - P(gs-1) as the passes go. Whole rounds of D passes, no
-  // branch inside (passes past the region read range-checked zeros and change
-  // nothing); each slot is consumed, then refilled at once.
+  const int32_t pa = a >> 6, pb = b >> 6;  // -1 never matches
+  const int32_t la = (a & 63) << 2, lb = (b & 63) << 2;
+  uint32_t aE = 0, aO = 0, bE = 0, bO = 0, cE = 0, cO = 0;
+  // Whole rounds of D passes, no branch inside (passes past the region read
+  // range-checked zeros and change nothing); each slot is consumed, then
+  // refilled at once.
   for (uint32_t p0 = 0; p0 < np; p0 += D) {
 #pragma unroll
     for (int d = 0; d < D; d++) {
-      const uint32_t p = p0 + d;
+      const int32_t p = (int32_t)(p0 + d);
       slot_wait<(D - 1) * kGran>(ring[d].c);  // slot d's loads are the oldest in flight
       uint32_t gE = 0, gO = 0;
       gran_eo(ring[d], gE, gO);
-      slot_load(ring[d].c, rs, vo, (p + D) * kPassBytes);
+      slot_load(ring[d].c, rs, vo, (uint32_t)(p + D) * kPassBytes);
       const uint32_t sE = wave_scan(gE), sO = wave_scan(gO);
       const uint32_t PE = sE + cE, PO = sO + cO;
-      const int32_t ia = a - (int32_t)(64 * p), ib = b - (int32_t)(64 * p);
-      const uint32_t xaE = (uint32_t)__builtin_amdgcn_ds_bpermute(ia << 2, (int)PE);
-      const uint32_t xaO = (uint32_t)__builtin_amdgcn_ds_bpermute(ia << 2, (int)PO);
-      const uint32_t xbE = (uint32_t)__builtin_amdgcn_ds_bpermute(ib << 2, (int)PE);
-      const uint32_t xbO = (uint32_t)__builtin_amdgcn_ds_bpermute(ib << 2, (int)PO);
-      const bool ina = (uint32_t)ia < 64u, inb = (uint32_t)ib < 64u;
-      E += (inb ? xbE : 0u) - (ina ? xaE : 0u);
-      O += (inb ? xbO : 0u) - (ina ? xaO : 0u);
+      const uint32_t xaE = (uint32_t)__builtin_amdgcn_ds_bpermute(la, (int)PE);
+      const uint32_t xaO = (uint32_t)__builtin_amdgcn_ds_bpermute(la, (int)PO);
+      const uint32_t xbE = (uint32_t)__builtin_amdgcn_ds_bpermute(lb, (int)PE);
+      const uint32_t xbO = (uint32_t)__builtin_amdgcn_ds_bpermute(lb, (int)PO);
+      aE = pa == p ? xaE : aE;
+      aO = pa == p ? xaO : aO;
+      bE = pb == p ? xbE : bE;
+      bO = pb == p ? xbO : bO;
       cE += readlane32(sE, 63);
       cO += readlane32(sO, 63);
     }
   }
+  E += bE - aE;
+  O += bO - aO;
 #pragma unroll
   for (int d = 0; d < D; d++) slot_wait<0>(ring[d].c);  // the last refills land before the registers are reused
   return (s & 1) ? (O << 8) + E : (E << 8) + O;
@@ -532,7 +547,8 @@ __device__ __forceinline__ uint32_t sparse_segment_sums(const KParams& P, bool j
 // Word sums of every job lane's segment [s, e): dense prefix stream when the
 // wave's segments share a compact region, else the per-segment stream.
 template <int D>
-__device__ __forceinline__ uint32_t segment_sums(const KParams& P, bool job, uint64_t s, uint64_t e, uint32_t lane) {
+__device__ __forceinline__ uint32_t segment_sums(const KParams& P, bool job, uint64_t s, uint64_t e, uint32_t lane,
+                                                 uint32_t hlds, uint32_t tlds) {
   const uint64_t jobs = __ballot(job);
   if (!jobs) return 0;
   // region relative to a wave-uniform base (the first job lane's chunk), in
@@ -546,7 +562,7 @@ __device__ __forceinline__ uint32_t segment_sums(const KParams& P, bool job, uin
   const uint32_t tot = wave_sum(job ? (uint32_t)(e - s) : 0u);
   const uint32_t lo16 = lo & ~15u;
   const bool dense = !__ballot(far) && hi - lo16 <= 4u * tot + 8192u;
-  if (dense) return dense_segment_sums<D>(P, B + lo16 - kBias, hi - lo16, job, s, e, lane);
+  if (dense) return dense_segment_sums<D>(P, B + lo16 - kBias, hi - lo16, job, s, e, lane, hlds, tlds);
   return sparse_segment_sums(P, job, s, e, lane);
 }
 
@@ -697,7 +713,22 @@ __device__ __forceinline__ void decode_packet(const KParams& P, const TT& T, uin
 
   // ---- Phase B: segment sums ---------------------------------------------
   if (kL4) {
-    const uint32_t sum = segment_sums<(O >= 7 ? GPK_PB_DEPTH7 : GPK_PB_DEPTH)>(P, job, js, je, lane);
+    // the segment's first and last chunk in an LDS header window: its own,
+    // or (the segment ending where the next packet starts) the next lane's
+    const uint32_t nch = active ? (m + win + 15) >> 4 : 0u;
+    const uint32_t noff_lo = (uint32_t)__shfl_down((int)(uint32_t)off, 1);
+    const uint32_t noff_hi = (uint32_t)__shfl_down((int)(uint32_t)(off >> 32), 1);
+    const uint32_t nnch = (uint32_t)__shfl_down((int)nch, 1);
+    const uint64_t noff = (uint64_t)noff_hi << 32 | noff_lo;
+    const uint64_t c0 = off >> 4;
+    uint32_t hlds = ~0u, tlds = ~0u;
+    if (job && (js >> 4) - c0 < nch) hlds = slot_dw * 4 + 16 * (uint32_t)((js >> 4) - c0);
+    if (job && (je >> 4) - c0 < nch)
+      tlds = slot_dw * 4 + 16 * (uint32_t)((je >> 4) - c0);
+    else if (job && lane < 63 && nnch && (noff >> 4) == (je >> 4))
+      tlds = (slot_dw + slot_dw_of<W>()) * 4;
+    constexpr int D = kLayout ? 4 : (O > 6 ? GPK_PB_DEPTH7 : GPK_PB_DEPTH);  // layouts: fewer registers left
+    const uint32_t sum = segment_sums<D>(P, job, js, je, lane, hlds, tlds);
     if (job) {
       l4c = fold(jinit + sum - jexist);
       const bool udp = (st & GPK_ST_L4_UDP) != 0;
@@ -792,7 +823,7 @@ Sel select(const gpk::KParams* P, int with_l4, int with_layout) {
   } else if (!s.l4 && !s.layout && P->small_headers) {
     s.W = 4;
   } else if (!s.layout && !P->big_packets) {
-    s.O = 7;
+    s.O = GPK_SMALL_WAVES;
   }
   return s;
 }
@@ -803,9 +834,12 @@ hipError_t launch_sel(const gpk::KParams* P, const Sel& s, hipStream_t stream) {
   if (s.keys) return s.l4 ? launch<true, false, kCompact, true>(P, stream) : launch<false, false, kCompact, true>(P, stream);
   if (s.W == 4) return launch<false, false, kCompact, false, 4>(P, stream);
   if (s.l4 && s.layout) return launch<true, true, kCompact>(P, stream);
-  if (s.l4) return s.O == 7 ? launch<true, false, kCompact, false, W, 7>(P, stream) : launch<true, false, kCompact>(P, stream);
+  if (s.l4)
+    return s.O != GPK_WAVES_PER_EU ? launch<true, false, kCompact, false, W, GPK_SMALL_WAVES>(P, stream)
+                                   : launch<true, false, kCompact>(P, stream);
   if (s.layout) return launch<false, true, kCompact>(P, stream);
-  return s.O == 7 ? launch<false, false, kCompact, false, W, 7>(P, stream) : launch<false, false, kCompact>(P, stream);
+  return s.O != GPK_WAVES_PER_EU ? launch<false, false, kCompact, false, W, GPK_SMALL_WAVES>(P, stream)
+                                 : launch<false, false, kCompact>(P, stream);
 }
 
 }  // namespace
