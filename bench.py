@@ -370,10 +370,12 @@ def c5_cpu(path, threads, nbytes=256 << 20):
         walk = []
         for _ in range(3):
             h = ctypes.c_void_p()
-            _lib.check(L.gpk_capreader_create(ctypes.byref(h), 1, 0))
+            _lib.check(L.gpk_capreader_create(ctypes.byref(h), 2, 0))  # GPK_CAP_PCAPNG
             x, used = _lib.CapIndex(), ctypes.c_uint64()
             t0 = time.perf_counter()
-            L.gpk_capreader_index_all(h, buf.ctypes.data, len(buf), 0, t, ctypes.byref(x), ctypes.byref(used))
+            rc = L.gpk_capreader_index_all(h, buf.ctypes.data, len(buf), 0, t, ctypes.byref(x), ctypes.byref(used))
+            if rc < 0 or not x.n:
+                raise RuntimeError("c5_cpu: gpk_capreader_index_all returned %d with %d packets" % (rc, x.n))
             walk.append(time.perf_counter() - t0)
             n = x.n
             off = np.ctypeslib.as_array(ctypes.cast(x.offsets, ctypes.POINTER(ctypes.c_uint64)), (n,)).copy()

@@ -17,11 +17,14 @@
 //    * dense waves (the usual packed batch: the wave's segments lie in one
 //      region not much larger than their total): the wave streams the whole
 //      region once, 1 KiB per pass (16 bytes per lane, one coalesced
-//      raw-buffer load), keeps a running wave-wide prefix sum of the even/odd
-//      byte sums per 16-byte granule (DPP scan), and every lane picks the prefix at its
+//      raw-buffer load), keeps a running wave-wide prefix sum of one 32-bit
+//      L-form sum per 16-byte granule (little-endian words at even addresses:
+//      v_sad_u16; one DPP scan), and every lane picks the prefix at its
 //      segment's first and last granule with ds_bpermute. Segment sum =
 //      prefix difference - the head granule's bytes before s + the tail
-//      granule's bytes before e. No per-packet reduction, no per-packet SALU.
+//      granule's bytes before e, turned into the big-endian word sum of the
+//      segment's alignment (exact mod 65535 for segments <= 64 KiB, which
+//      is all the fold needs; see l_to_words). No per-packet reduction.
 //    * sparse waves (scattered offsets): the segments are streamed one after
 //      another as whole-wave 1 KiB loads and reduced per packet (DPP).
 #include <hip/hip_runtime.h>
@@ -48,10 +51,13 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
                        // lines per load instruction, beat 2 KiB passes of two half-coalesced loads by 20 %)
 #endif
 #ifndef GPK_PB_DEPTH
-#define GPK_PB_DEPTH 6  // dense phase B: passes in flight (80-VGPR kernels)
+#define GPK_PB_DEPTH 8  // dense phase B: passes in flight (80-VGPR kernels; A/B r04b: 8 vs 6 -0.4 % C3, 10 no better)
 #endif
 #ifndef GPK_PB_DEPTH7
-#define GPK_PB_DEPTH7 4  // ... in the 72-VGPR kernels (7 waves per SIMD)
+#define GPK_PB_DEPTH7 6  // ... in the 72-VGPR kernels (7 waves per SIMD; A/B r04b: 6 vs 4 -0.9 % C4, -2.8 % C1)
+#endif
+#ifndef GPK_PB_IDPERM
+#define GPK_PB_IDPERM 1  // dense phase B: lanes outside their target pass pull their own prefix (no LDS bank conflicts)
 #endif
 #ifndef GPK_PB_SDEPTH
 #define GPK_PB_SDEPTH 4  // sparse phase B: 1 KiB wave loads in flight
@@ -153,6 +159,40 @@ __device__ __forceinline__ void chunk_eo_below(const u32x4& v, uint32_t n, uint3
   O = dot_odd(w2, O);
   E = dot_even(w3, E);
   O = dot_odd(w3, O);
+}
+
+// The same sums in one word ("L form"): little-endian 16-bit words at even
+// addresses, i.e. even-address bytes + 256 * odd-address bytes (v_sad_u16
+// against 0 adds a dword's two halves).
+__device__ __forceinline__ uint32_t chunk_l(const u32x4& v, uint32_t acc) {
+  acc = __builtin_amdgcn_sad_u16(v.x, 0u, acc);
+  acc = __builtin_amdgcn_sad_u16(v.y, 0u, acc);
+  acc = __builtin_amdgcn_sad_u16(v.z, 0u, acc);
+  return __builtin_amdgcn_sad_u16(v.w, 0u, acc);
+}
+__device__ __forceinline__ uint32_t chunk_l_below(const u32x4& v, uint32_t n, uint32_t acc) {
+  const uint32_t nl = n < 8 ? n : 8u, nh = n > 8 ? n - 8 : 0u;
+  const uint64_t ml = nl >= 8 ? ~0ull : (1ull << (8 * nl)) - 1;
+  const uint64_t mh = nh >= 8 ? ~0ull : (1ull << (8 * nh)) - 1;
+  return chunk_l(u32x4{v.x & (uint32_t)ml, v.y & (uint32_t)(ml >> 32), v.z & (uint32_t)mh, v.w & (uint32_t)(mh >> 32)},
+                 acc);
+}
+// An L-form segment sum L (mod 2^32) as ComputeChecksum's word sum of the
+// segment (words start at its first byte, checksum.go:35-50):
+//  * the segment starts at an odd address: its words are the little-endian
+//    words at even addresses, so the word sum is L itself, exactly;
+//  * it starts at an even address: the word sum is the byte-swapped sum,
+//    congruent to 256 * L mod 65535 (2^16 = 1): swap16(fold(L)) + 65535, a
+//    value congruent to the word sum and >= any one word. For segments of at
+//    most 64 KiB the word sum does not wrap 2^32, so every later step the
+//    caller takes (add the pseudo-header, subtract the checksum field, fold;
+//    tcpip.go:54-69) yields the same 16 bits; segment_sums sends waves with a
+//    longer segment to the exact per-segment stream.
+__device__ __forceinline__ uint32_t l_to_words(uint32_t L, uint32_t odd) {
+  if (odd) return L;
+  uint32_t f = (L & 0xffffu) + (L >> 16);
+  f = (f & 0xffffu) + (f >> 16);
+  return ((f & 0xffu) << 8 | f >> 8) + 0xffffu;
 }
 
 // 16 bytes of an LDS window chunk (dword-aligned byte address; ~0 = none,
@@ -353,10 +393,11 @@ __device__ __forceinline__ int derive_key(const KParams& P, const Rd& r, const P
 
 // Dense: the wave's segments lie in [R0, R0 + R) (R0 16-byte aligned). The
 // region is cut into granules (16 bytes), lane l of pass p holds granule
-// 64p + l. P(g) = even/odd byte sums of granules [0, g], a wave-wide running
+// 64p + l. P(g) = L-form sum (chunk_l) of granules [0, g], a wave-wide running
 // prefix. Segment sum over granules [gs, ge) = P(ge-1) - P(gs-1), corrected by
 // the head granule's bytes before s and the tail granule's bytes before e
-// (each lane loads those two granules itself).
+// (from the LDS header windows, else loaded), then turned into the word sum
+// of the segment's own alignment (l_to_words).
 // One pass of the dense stream into a granule slot: kGran raw-buffer loads
 // (16 bytes per lane each, consecutive lanes -> consecutive granules)
 // written in place ("+v": the slot keeps its registers across the loop, so
@@ -391,6 +432,25 @@ __device__ __forceinline__ void slot_wait(u32x4 (&c)[kGran]) {
                  : "memory");
 }
 
+// slot_wait with a count known after unrolling (the tail's per-slot counts)
+__device__ __forceinline__ void slot_wait_n(u32x4 (&c)[kGran], int n) {
+  static_assert(kGran == 1, "counts in loads");
+  switch (n) {
+    case 0: slot_wait<0>(c); break;
+    case 1: slot_wait<1>(c); break;
+    case 2: slot_wait<2>(c); break;
+    case 3: slot_wait<3>(c); break;
+    case 4: slot_wait<4>(c); break;
+    case 5: slot_wait<5>(c); break;
+    case 6: slot_wait<6>(c); break;
+    case 7: slot_wait<7>(c); break;
+    case 8: slot_wait<8>(c); break;
+    case 9: slot_wait<9>(c); break;
+    case 10: slot_wait<10>(c); break;
+    default: slot_wait<0>(c); break;  // deeper rings: wait for everything
+  }
+}
+
 template <int D>
 __device__ __forceinline__ uint32_t dense_segment_sums(const KParams& P, uint64_t R0, uint32_t R, bool job,
                                                        uint64_t s, uint64_t e, uint32_t lane, uint32_t hlds,
@@ -403,16 +463,12 @@ __device__ __forceinline__ uint32_t dense_segment_sums(const KParams& P, uint64_
   // head / tail chunks, summed before the stream starts (their wait must
   // not drain the stream): from the LDS header windows when a window holds
   // them (hlds / tlds = LDS byte address, else ~0), else from memory
-  uint32_t E = 0, O = 0;
+  uint32_t L = 0;
   {
     u32x4 hc = lds_chunk(hlds), tc = lds_chunk(tlds);
     if (hlds == ~0u) hc = __builtin_amdgcn_raw_buffer_load_b128(rs, rsl & ~15u, 0, 0);
     if (tlds == ~0u) tc = __builtin_amdgcn_raw_buffer_load_b128(rs, rel & ~15u, 0, 0);
-    uint32_t hE = 0, hO = 0;
-    chunk_eo_below(tc, rel & 15u, E, O);
-    chunk_eo_below(hc, rsl & 15u, hE, hO);
-    E -= hE;
-    O -= hO;
+    L = chunk_l_below(tc, rel & 15u, 0u) - chunk_l_below(hc, rsl & 15u, 0u);
   }
   const uint32_t np = (R + kPassBytes - 1) / kPassBytes;  // wave-uniform
   const uint32_t vo = lane * kGranBytes;
@@ -423,43 +479,49 @@ __device__ __forceinline__ uint32_t dense_segment_sums(const KParams& P, uint64_
     for (int k = 0; k < kGran; k++) ring[d].c[k] = u32x4{0, 0, 0, 0};
     slot_load(ring[d].c, rs, vo, d * kPassBytes);
   }
-  // granule-sum targets: prefix through granule gs-1 (a) and ge-1 (b); -1 =
-  // the empty prefix. Target t sits in pass t >> 6 at lane t & 63: the
-  // ds_bpermute address is fixed, only the pass test changes.
+  // prefix targets: through granule gs-1 (a) and ge-1 (b); -1 = the empty
+  // prefix. Target t sits in pass t >> 6 at lane t & 63. In its pass a lane
+  // pulls lane t's prefix; in every other pass it pulls its own (identity
+  // ds_bpermute: no bank conflicts), which the select drops.
   const int32_t a = (int32_t)(rsl / kGranBytes) - 1, b = (int32_t)(rel / kGranBytes) - 1;
   const int32_t pa = a >> 6, pb = b >> 6;  // -1 never matches
-  const int32_t la = (a & 63) << 2, lb = (b & 63) << 2;
-  uint32_t aE = 0, aO = 0, bE = 0, bO = 0, cE = 0, cO = 0;
-  // Whole rounds of D passes, no branch inside (passes past the region read
-  // range-checked zeros and change nothing); each slot is consumed, then
-  // refilled at once.
-  for (uint32_t p0 = 0; p0 < np; p0 += D) {
+  const int32_t la = (a & 63) << 2, lb = (b & 63) << 2, ll = (int32_t)lane << 2;
+  uint32_t xa = 0, xb = 0, c = 0;
+  // One pass: slot d holds pass p; refill it with pass p + D when asked.
+  auto pass = [&](const int d, const int32_t p, const bool refill) __attribute__((always_inline)) {
+    const uint32_t g = chunk_l(ring[d].c[0], 0u);
+    if (refill) slot_load(ring[d].c, rs, vo, (uint32_t)(p + D) * kPassBytes);
+    const uint32_t sc = wave_scan(g);
+    const uint32_t Pf = sc + c;
+    const bool ma = pa == p, mb = pb == p;
+    const uint32_t ya = (uint32_t)__builtin_amdgcn_ds_bpermute(GPK_PB_IDPERM ? (ma ? la : ll) : la, (int)Pf);
+    const uint32_t yb = (uint32_t)__builtin_amdgcn_ds_bpermute(GPK_PB_IDPERM ? (mb ? lb : ll) : lb, (int)Pf);
+    xa = ma ? ya : xa;
+    xb = mb ? yb : xb;
+    c += readlane32(sc, 63);
+  };
+  // Whole rounds of D passes, no branch inside; each slot is consumed, then
+  // refilled at once (refills past the region read range-checked zeros).
+  uint32_t p0 = 0;
+  for (; p0 + D <= np; p0 += D) {
 #pragma unroll
     for (int d = 0; d < D; d++) {
-      const int32_t p = (int32_t)(p0 + d);
       slot_wait<(D - 1) * kGran>(ring[d].c);  // slot d's loads are the oldest in flight
-      uint32_t gE = 0, gO = 0;
-      gran_eo(ring[d], gE, gO);
-      slot_load(ring[d].c, rs, vo, (uint32_t)(p + D) * kPassBytes);
-      const uint32_t sE = wave_scan(gE), sO = wave_scan(gO);
-      const uint32_t PE = sE + cE, PO = sO + cO;
-      const uint32_t xaE = (uint32_t)__builtin_amdgcn_ds_bpermute(la, (int)PE);
-      const uint32_t xaO = (uint32_t)__builtin_amdgcn_ds_bpermute(la, (int)PO);
-      const uint32_t xbE = (uint32_t)__builtin_amdgcn_ds_bpermute(lb, (int)PE);
-      const uint32_t xbO = (uint32_t)__builtin_amdgcn_ds_bpermute(lb, (int)PO);
-      aE = pa == p ? xaE : aE;
-      aO = pa == p ? xaO : aO;
-      bE = pb == p ? xbE : bE;
-      bO = pb == p ? xbO : bO;
-      cE += readlane32(sE, 63);
-      cO += readlane32(sO, 63);
+      pass(d, (int32_t)(p0 + d), true);
     }
   }
-  E += bE - aE;
-  O += bO - aO;
+  // The last np - p0 < D passes are in flight already: no refills, so slot
+  // d waits for all but the D-1-d younger slots.
+#pragma unroll
+  for (int d = 0; d < D - 1; d++) {
+    if (p0 + d >= np) break;
+    slot_wait_n(ring[d].c, D - 1 - d);
+    pass(d, (int32_t)(p0 + d), false);
+  }
+  L += xb - xa;
 #pragma unroll
   for (int d = 0; d < D; d++) slot_wait<0>(ring[d].c);  // the last refills land before the registers are reused
-  return (s & 1) ? (O << 8) + E : (E << 8) + O;
+  return l_to_words(L, (uint32_t)s & 1u);
 }
 
 // Sparse: the segments one after another as whole-wave 1 KiB loads (16 bytes
@@ -552,11 +614,12 @@ __device__ __forceinline__ uint32_t segment_sums(const KParams& P, bool job, uin
   const uint64_t jobs = __ballot(job);
   if (!jobs) return 0;
   // region relative to a wave-uniform base (the first job lane's chunk), in
-  // 32-bit biased coordinates; lanes too far from it make the wave sparse
+  // 32-bit biased coordinates; lanes too far from it (or with a segment over
+  // 64 KiB) make the wave sparse
   const uint64_t B = readlane64(s, (uint32_t)__builtin_ctzll(jobs)) & ~15ull;
   constexpr uint64_t kBias = 0x80000000ull;
   const uint64_t bs = s + kBias - B, be = e + kBias - B;
-  const bool far = job && (bs >> 32 || be >> 32);
+  const bool far = job && (bs >> 32 || be >> 32 || e - s > 65536u);  // far, or too long for l_to_words
   const uint32_t lo = wave_min(job ? (uint32_t)bs : 0xffffffffu);
   const uint32_t hi = wave_max(job ? (uint32_t)be : 0u);
   const uint32_t tot = wave_sum(job ? (uint32_t)(e - s) : 0u);
