@@ -403,7 +403,10 @@ __device__ __forceinline__ int derive_key(const KParams& P, const Rd& r, const P
 // written in place ("+v": the slot keeps its registers across the loop, so
 // the stream needs no register rotation and no drain at the loop edge).
 // Issued as inline asm, which the compiler's wait-count pass does not see:
-// dense_segment_sums waits for the slots itself (slot_wait).
+// dense_segment_sums waits for the slots itself (slot_wait). The register
+// allocator believes the asm wrote the slot at once and could copy or spill
+// it while the load is in flight; every build's device code is therefore
+// checked for that (tools/check_stream_isa.py, run by the Makefile).
 __device__ __forceinline__ void slot_load(u32x4 (&c)[kGran], __amdgpu_buffer_rsrc_t rs, uint32_t vo,
                                           uint32_t soff) {
   asm volatile("buffer_load_dwordx4 %0, %1, %2, %3 offen nt" : "+v"(c[0]) : "v"(vo), "s"(rs), "s"(soff) : "memory");
@@ -481,8 +484,8 @@ __device__ __forceinline__ uint32_t dense_segment_sums(const KParams& P, uint64_
   }
   // prefix targets: through granule gs-1 (a) and ge-1 (b); -1 = the empty
   // prefix. Target t sits in pass t >> 6 at lane t & 63. In its pass a lane
-  // pulls lane t's prefix; in every other pass it pulls its own (identity
-  // ds_bpermute: no bank conflicts), which the select drops.
+  // pulls lane t's prefix with ds_bpermute; in every other pass it pulls its
+  // own (identity permutation: no bank conflicts), which the select drops.
   const int32_t a = (int32_t)(rsl / kGranBytes) - 1, b = (int32_t)(rel / kGranBytes) - 1;
   const int32_t pa = a >> 6, pb = b >> 6;  // -1 never matches
   const int32_t la = (a & 63) << 2, lb = (b & 63) << 2, ll = (int32_t)lane << 2;
