@@ -139,6 +139,7 @@ def run_config(name, n, steps, warmup, rank, world, ctx, check_sample=2048, prob
     fl = torch.empty(3 * n, dtype=torch.int64, device="cuda") if cfg["outputs"] & 4 else None
     payload_bytes = int(cap.sum(dtype=torch.int64).item())
     kernel = ctx.kernel_name(parser, data, off, cap)
+    blocks_per_cu = ctx.occupancy(parser, data, off, cap)
     torch.cuda.synchronize()
 
     def step():
@@ -164,7 +165,7 @@ def run_config(name, n, steps, warmup, rank, world, ctx, check_sample=2048, prob
         parity = sample_parity(name, cfg, rec, fl, err, first, n, check_sample)
     res = dict(n=n, payload_bytes=payload_bytes, wall_s=wall_max, kernel_ms=kernel_ms,
                algo_bytes=payload_bytes + INDEX_BYTES * n, parity=parity, probe_gbs=probe_gbs, strong=strong,
-               kernel=kernel)
+               kernel=kernel, blocks_per_cu=blocks_per_cu)
     del data, off, cap, rec, err, fl
     torch.cuda.empty_cache()
     return res
@@ -762,6 +763,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "traffic_profile": traffic_profile, "kernel": r["kernel"],
+                         "blocks_per_cu": r["blocks_per_cu"],
                          "traffic_unit": "bytes per launch", "kernel_ms": round(r["kernel_ms"], 4),
                          "algo_bytes_per_launch": r["algo_bytes"],
                          "probe_read_GBps": r["probe_gbs"] and round(r["probe_gbs"], 1)},
@@ -775,7 +777,7 @@ def main():
             pk = st["total_packets"] if st else s["n"] * world
             row = {"workload": CONFIGS[name]["workload"],
                    "value": round(pk * args.steps / s["wall_s"] / 1e6, 2), "unit": "Mpkts/s",
-                   "kernel": s["kernel"], "kernel_ms": round(s["kernel_ms"], 4), "achieved_GBps": round(ach, 1),
+                   "kernel": s["kernel"], "blocks_per_cu": s["blocks_per_cu"], "kernel_ms": round(s["kernel_ms"], 4), "achieved_GBps": round(ach, 1),
                    "frac": round(ach / HBM_PEAK_GBS, 4), "parity": s["parity"],
                    "probe_read_GBps": s["probe_gbs"] and round(s["probe_gbs"], 1)}
             if st:

@@ -25,6 +25,7 @@
 
 extern "C" hipError_t gpk_launch_decode(const gpk::KParams* P, int with_l4, int with_layout, hipStream_t stream);
 extern "C" int gpk_launch_describe(const gpk::KParams* P, int with_l4, int with_layout, char* buf, size_t cap);
+extern "C" hipError_t gpk_launch_occupancy(const gpk::KParams* P, int with_l4, int with_layout, int* blocks);
 extern "C" hipError_t gpk_launch_list(const gpk::KParams* P, uint64_t index, int64_t* out, uint32_t cap,
                                       uint32_t* out_n, hipStream_t stream);
 
@@ -508,6 +509,20 @@ int gpk_decode_kernel_name(gpk_ctx* c, const gpk_parser* p, const gpk_batch* b, 
   rc = upload(c, p, P, &slot);
   if (rc) return rc;
   return gpk_launch_describe(&P, (p->outputs & GPK_OUT_L4_CSUM) != 0, with_layouts != 0, buf, cap);
+}
+
+int gpk_decode_occupancy(gpk_ctx* c, const gpk_parser* p, const gpk_batch* b, int with_layouts, int* blocks_per_cu) {
+  if (!blocks_per_cu) return GPK_EINVAL;
+  gpk::KParams P;
+  int rc = make_params(c, p, b, nullptr, P);
+  if (rc) return rc;
+  std::lock_guard<std::mutex> g(c->mu);
+  HIPCHK(hipSetDevice(c->device));
+  int slot = 0;
+  rc = upload(c, p, P, &slot);
+  if (rc) return rc;
+  HIPCHK(gpk_launch_occupancy(&P, (p->outputs & GPK_OUT_L4_CSUM) != 0, with_layouts != 0, blocks_per_cu));
+  return GPK_OK;
 }
 
 static int ensure_dbuf(gpk_ctx* c, size_t bytes) {

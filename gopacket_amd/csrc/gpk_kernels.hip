@@ -59,6 +59,12 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 #ifndef GPK_PB_IDPERM
 #define GPK_PB_IDPERM 1  // dense phase B: lanes outside their target pass pull their own prefix (no LDS bank conflicts)
 #endif
+#ifndef GPK_PB_LDS_HT
+#define GPK_PB_LDS_HT 1  // segment head/tail chunks from the LDS header windows when they hold them
+#endif
+#ifndef GPK_BLOB_ROUND
+#define GPK_BLOB_ROUND 128  // dwords: the table blob's LDS share is rounded to this
+#endif
 #ifndef GPK_PB_SDEPTH
 #define GPK_PB_SDEPTH 4  // sparse phase B: 1 KiB wave loads in flight
 #endif
@@ -788,10 +794,10 @@ __device__ __forceinline__ void decode_packet(const KParams& P, const TT& T, uin
     const uint64_t noff = (uint64_t)noff_hi << 32 | noff_lo;
     const uint64_t c0 = off >> 4;
     uint32_t hlds = ~0u, tlds = ~0u;
-    if (job && (js >> 4) - c0 < nch) hlds = slot_dw * 4 + 16 * (uint32_t)((js >> 4) - c0);
-    if (job && (je >> 4) - c0 < nch)
+    if (GPK_PB_LDS_HT && job && (js >> 4) - c0 < nch) hlds = slot_dw * 4 + 16 * (uint32_t)((js >> 4) - c0);
+    if (GPK_PB_LDS_HT && job && (je >> 4) - c0 < nch)
       tlds = slot_dw * 4 + 16 * (uint32_t)((je >> 4) - c0);
-    else if (job && lane < 63 && nnch && (noff >> 4) == (je >> 4))
+    else if (GPK_PB_LDS_HT && job && lane < 63 && nnch && (noff >> 4) == (je >> 4))
       tlds = (slot_dw + slot_dw_of<W>()) * 4;
     constexpr int D = kLayout ? 4 : (O > 6 ? GPK_PB_DEPTH7 : GPK_PB_DEPTH);  // layouts: fewer registers left
     const uint32_t sum = segment_sums<D>(P, job, js, je, lane, hlds, tlds);
@@ -820,17 +826,17 @@ __device__ __forceinline__ void decode_packet(const KParams& P, const TT& T, uin
 template <bool kL4, bool kLayout, bool kCompact, bool kKeys = false, int W = kWinChunks, int O = GPK_WAVES_PER_EU>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W == 4 ? GPK_W4_WAVES : O, 8))) void decode_kernel(
     KParams P) {
+  const uint32_t tid = threadIdx.x;
+  const uint32_t slot_dw = tid * slot_dw_of<W>();
+  const uint32_t base = kBlock * slot_dw_of<W>();
   if ((uint64_t)blockIdx.x * kBlock >= P.n) return;  // uniform over the block
   // Every packet's index, then its header window and the table blob are in
   // flight together: two dependent memory round trips per packet.
-  const uint32_t tid = threadIdx.x;
-  const uint32_t slot_dw = tid * slot_dw_of<W>();
   const uint64_t i0 = (uint64_t)blockIdx.x * kBlock + tid;
   const Idx c0 = load_index(P, i0);
   const uint32_t n0 = win_chunks<W>(c0, i0 < P.n);
   WinT<W> w0;
   load_window(P, c0, n0, w0);
-  const uint32_t base = kBlock * slot_dw_of<W>();
   if (kCompact) {  // the table blob (<= kCtDwords): clamped indices, duplicate writes of equal values
     static_assert(kCtDwords <= 3 * kBlock, "three blob words per thread");
     const uint32_t last = P.cg.words - 1;
@@ -863,13 +869,17 @@ __global__ void list_kernel(KParams P, uint64_t index, int64_t* out, uint32_t ca
 
 namespace {
 
+// Launch one specialisation on `stream`, or (occ != nullptr) report how many of
+// its blocks fit a CU with this launch's LDS size instead.
 template <bool kL4, bool kLayout, bool kCompact, bool kKeys = false, int W = gpk::kWinChunks,
           int O = GPK_WAVES_PER_EU>
-hipError_t launch(const gpk::KParams* P, hipStream_t stream) {
+hipError_t launch(const gpk::KParams* P, hipStream_t stream, int* occ) {
   using namespace gpk;
   constexpr int slot_lds = kBlock * slot_dw_of<W>() * 4;
-  // the table blob takes only the words this parser's tables use (C3/C4: ~1.5 KB of 2.9)
-  const int lds = kCompact ? slot_lds + (int)((P->cg.words + 127) & ~127u) * 4 : slot_lds;
+  // the table blob takes only the words this parser's tables use
+  const int lds = kCompact ? slot_lds + (int)((P->cg.words + GPK_BLOB_ROUND - 1) & ~(GPK_BLOB_ROUND - 1u)) * 4 : slot_lds;
+  if (occ) return hipOccupancyMaxActiveBlocksPerMultiprocessor(occ, decode_kernel<kL4, kLayout, kCompact, kKeys, W, O>,
+                                                              kBlock, lds);
   const uint64_t grid = (P->n + kBlock - 1) / kBlock;
   if (grid > 0xffffffffull) return hipErrorInvalidValue;
   hipLaunchKernelGGL((decode_kernel<kL4, kLayout, kCompact, kKeys, W, O>), dim3((unsigned)grid), dim3(kBlock), lds,
@@ -895,17 +905,18 @@ Sel select(const gpk::KParams* P, int with_l4, int with_layout) {
 }
 
 template <bool kCompact>
-hipError_t launch_sel(const gpk::KParams* P, const Sel& s, hipStream_t stream) {
+hipError_t launch_sel(const gpk::KParams* P, const Sel& s, hipStream_t stream, int* occ) {
   constexpr int W = gpk::kWinChunks;
-  if (s.keys) return s.l4 ? launch<true, false, kCompact, true>(P, stream) : launch<false, false, kCompact, true>(P, stream);
-  if (s.W == 4) return launch<false, false, kCompact, false, 4>(P, stream);
-  if (s.l4 && s.layout) return launch<true, true, kCompact>(P, stream);
+  if (s.keys)
+    return s.l4 ? launch<true, false, kCompact, true>(P, stream, occ) : launch<false, false, kCompact, true>(P, stream, occ);
+  if (s.W == 4) return launch<false, false, kCompact, false, 4>(P, stream, occ);
+  if (s.l4 && s.layout) return launch<true, true, kCompact>(P, stream, occ);
   if (s.l4)
-    return s.O != GPK_WAVES_PER_EU ? launch<true, false, kCompact, false, W, GPK_SMALL_WAVES>(P, stream)
-                                   : launch<true, false, kCompact>(P, stream);
-  if (s.layout) return launch<false, true, kCompact>(P, stream);
-  return s.O != GPK_WAVES_PER_EU ? launch<false, false, kCompact, false, W, GPK_SMALL_WAVES>(P, stream)
-                                 : launch<false, false, kCompact>(P, stream);
+    return s.O != GPK_WAVES_PER_EU ? launch<true, false, kCompact, false, W, GPK_SMALL_WAVES>(P, stream, occ)
+                                   : launch<true, false, kCompact>(P, stream, occ);
+  if (s.layout) return launch<false, true, kCompact>(P, stream, occ);
+  return s.O != GPK_WAVES_PER_EU ? launch<false, false, kCompact, false, W, GPK_SMALL_WAVES>(P, stream, occ)
+                                 : launch<false, false, kCompact>(P, stream, occ);
 }
 
 }  // namespace
@@ -914,7 +925,13 @@ extern "C" hipError_t gpk_launch_decode(const gpk::KParams* P, int with_l4, int 
   if (P->n == 0) return hipSuccess;
   if (P->key_kind && with_layout) return hipErrorInvalidValue;
   const Sel s = select(P, with_l4, with_layout);
-  return s.compact ? launch_sel<true>(P, s, stream) : launch_sel<false>(P, s, stream);
+  return s.compact ? launch_sel<true>(P, s, stream, nullptr) : launch_sel<false>(P, s, stream, nullptr);
+}
+
+// Blocks of that specialisation resident per CU (registers and this launch's LDS).
+extern "C" hipError_t gpk_launch_occupancy(const gpk::KParams* P, int with_l4, int with_layout, int* blocks) {
+  const Sel s = select(P, with_l4, with_layout);
+  return s.compact ? launch_sel<true>(P, s, nullptr, blocks) : launch_sel<false>(P, s, nullptr, blocks);
 }
 
 // Name of the kernel specialisation gpk_launch_decode would launch.

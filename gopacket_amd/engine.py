@@ -130,6 +130,14 @@ class Context:
             raise _lib.GpkError("gpk_decode_kernel_name: %d" % n)
         return buf.value.decode()
 
+    def occupancy(self, parser, data, offsets, caplens, layouts=False):
+        """Blocks of that kernel resident per CU with this parser's LDS table
+        blob (gpk_decode_occupancy)."""
+        b = _lib.Batch(data.data_ptr(), offsets.data_ptr(), caplens.data_ptr(), offsets.numel(), data.numel())
+        out = ctypes.c_int()
+        check(lib().gpk_decode_occupancy(self.h, parser.h, ctypes.byref(b), int(layouts), ctypes.byref(out)))
+        return out.value
+
     def replay_file(self, parser, path, fmt=0, ng_flags=0, slot_bytes=0, slots=0, batch_pkts=0, read_threads=0,
                     collect=True, on_batch=None):
         """gpk_replay_file: the whole capture through HBM (BASELINE config C5).

@@ -279,6 +279,11 @@ int gpk_decode_batch(gpk_ctx* ctx, const gpk_parser* p, const gpk_batch* batch,
 int gpk_decode_kernel_name(gpk_ctx* ctx, const gpk_parser* p, const gpk_batch* batch, int with_layouts,
                            char* buf, size_t cap);
 
+/* Diagnostic: how many 256-packet blocks of that specialisation are resident
+ * per CU with this parser's LDS table blob (hipOccupancyMaxActiveBlocksPerMultiprocessor). */
+int gpk_decode_occupancy(gpk_ctx* ctx, const gpk_parser* p, const gpk_batch* batch, int with_layouts,
+                         int* blocks_per_cu);
+
 /* Host-memory variant: batch and results live in host memory (ideally pinned
  * via gpk_host_alloc). Copies HtoD, decodes, copies DtoH; synchronous. */
 int gpk_decode_batch_host(gpk_ctx* ctx, const gpk_parser* p, const gpk_batch* host_batch,

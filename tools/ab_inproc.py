@@ -70,6 +70,16 @@ def main():
                 assert L.gpk_parser_add_decoder(p, engine.DECODER_KINDS[d]) == 0
             assert L.gpk_parser_set_outputs(p, cfg["outputs"]) == 0
             handles[v] = (ctx, p)
+        occ = {}
+        for v, L in libs.items():
+            try:
+                f = L.gpk_decode_occupancy
+            except AttributeError:  # a library from before the diagnostic
+                occ[v] = "?"
+                continue
+            o = ctypes.c_int()
+            f.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
+            occ[v] = o.value if f(handles[v][0], handles[v][1], ctypes.byref(b), 0, ctypes.byref(o)) == 0 else "?"
         times = {v: [] for v in libs}
         for rnd in range(a.rounds + 1):
             for v, L in libs.items():
@@ -85,9 +95,9 @@ def main():
                     times[v].append(e0.elapsed_time(e1) / a.steps)
         for v in libs:
             t = np.array(times[v])
-            print("%-4s %-10s median %8.3f ms  min %8.3f ms  %7.1f GB/s (%.1f%% of 8 TB/s)" % (
+            print("%-4s %-10s median %8.3f ms  min %8.3f ms  %7.1f GB/s (%.1f%% of 8 TB/s)  blocks/CU %s" % (
                 name, v, np.median(t), t.min(), algo / (np.median(t) * 1e-3) / 1e9,
-                algo / (np.median(t) * 1e-3) / 8e12 * 100), flush=True)
+                algo / (np.median(t) * 1e-3) / 8e12 * 100, occ[v]), flush=True)
         del data, off, cap, rec, err, fl
         torch.cuda.empty_cache()
 
