@@ -885,13 +885,14 @@ __device__ __forceinline__ uint32_t fold(uint32_t c) {
   return (~c) & 0xffff;
 }
 
-// FNV-1a 64 step (flows.go:60-70): h = (h ^ b) * 0x100000001b3.
+// FNV-1a 64 step (flows.go:60-70): h = (h ^ b) * 0x100000001b3 mod 2^64.
+// With x = lo ^ b: x * 0x1b3 + ((hi * 0x1b3 + (x << 8)) << 32), i.e. one
+// v_mul_lo_u32, one v_lshl_add_u32 and one v_mad_u64_u32 whose 64-bit addend
+// carries the high word (the b byte only reaches the low word).
 __device__ __forceinline__ uint64_t fnv_step(uint64_t h, uint32_t b) {
-  h ^= b;
-  uint32_t lo = (uint32_t)h, hi = (uint32_t)(h >> 32);
-  uint64_t m = (uint64_t)lo * 0x1b3u;  // v_mad_u64_u32
-  uint32_t rhi = (uint32_t)(m >> 32) + hi * 0x1b3u + (lo << 8);
-  return ((uint64_t)rhi << 32) | (uint32_t)m;
+  const uint32_t x = (uint32_t)h ^ b, hi = (uint32_t)(h >> 32);
+  const uint32_t s = hi * 0x1b3u + (x << 8);
+  return (uint64_t)x * 0x1b3u + ((uint64_t)s << 32);
 }
 template <class R>
 __device__ __forceinline__ uint64_t fnv_bytes(const R& r, uint32_t p, uint32_t n) {
@@ -916,9 +917,51 @@ __device__ __forceinline__ uint64_t fnv_range(const Rd& r, uint32_t p) {
   if (p + N <= r.win) return fnv_lds<N>(r.lb + p);
   return fnv_bytes(r, p, N);
 }
+// NetworkFlow().FastHash() of an IPv4 (ip4.go:63-65, EndpointIPv4 = 1) or
+// IPv6 (ip6.go:49-51, EndpointIPv6 = 2) header at packet offset ns: source
+// and destination addresses (4 or 16 bytes each) hashed in one loop of 1 or
+// 4 dwords, so a wave holding both kinds runs 16 steps per address, not
+// 4 + 16. The dword count is uniform over the active lanes; IPv4 lanes keep
+// the state after their first dword.
+__device__ __forceinline__ uint64_t net_flow_hash(const Rd& r, uint32_t ns, bool v6);
 // Flow.FastHash flows.go:167-174
 __device__ __forceinline__ uint64_t flow_hash(uint64_t hs, uint64_t hd, uint32_t typ) {
   return ((hs + hd) ^ (uint64_t)typ) * 1099511628211ull;
+}
+__device__ __forceinline__ uint64_t net_flow_hash(const Rd& r, uint32_t ns, bool v6) {
+  const uint32_t n = v6 ? 16u : 4u, a = ns + (v6 ? 8u : 12u);
+  const bool inwin = a + 2 * n <= r.win;
+  uint64_t hs = 14695981039346656037ull, hd = hs;
+  if (__ballot(!inwin)) {  // rare: an address past the LDS window (deep stacks)
+    if (!inwin) {
+      hs = fnv_bytes(r, a, n);
+      hd = fnv_bytes(r, a + n, n);
+    }
+  }
+  if (inwin) {
+    const uint32_t nd = __ballot(inwin && v6) ? 4u : 1u;
+    uint64_t hs4 = 0, hd4 = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 4; k++) {
+      if (k < nd) {
+        const uint32_t ws = lds32u(r.lb + a + 4 * k), wd = lds32u(r.lb + a + n + 4 * k);
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          hs = fnv_step(hs, (ws >> (8 * j)) & 0xffu);
+          hd = fnv_step(hd, (wd >> (8 * j)) & 0xffu);
+        }
+        if (k == 0) {
+          hs4 = hs;
+          hd4 = hd;
+        }
+      }
+    }
+    if (!v6) {
+      hs = hs4;
+      hd = hd4;
+    }
+  }
+  return flow_hash(hs, hd, v6 ? 2u : 1u);
 }
 
 }  // namespace gpk

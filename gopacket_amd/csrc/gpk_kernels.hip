@@ -716,15 +716,9 @@ __device__ __forceinline__ void decode_packet(const KParams& P, const TT& T, uin
         lflow = flow_hash(fnv_range<6>(r, e0 + 6), fnv_range<6>(r, e0), 3);
         st |= GPK_ST_LINK_FLOW;
       }
-      if (nk && clean(q, nk)) {
-        uint32_t ns = q.start(nk);
-        if (nk == GPK_DEC_IPV4) {  // ip4.go:63-65 (EndpointIPv4 = 1)
-          nflow = flow_hash(fnv_range<4>(r, ns + 12), fnv_range<4>(r, ns + 16), 1);
-        } else {  // ip6.go:49-51 (EndpointIPv6 = 2)
-          nflow = flow_hash(fnv_range<16>(r, ns + 8), fnv_range<16>(r, ns + 24), 2);
-          st |= GPK_ST_NET_IPV6;
-        }
-        st |= GPK_ST_NET_FLOW;
+      if (nk && clean(q, nk)) {  // ip4.go:63-65 / ip6.go:49-51
+        nflow = net_flow_hash(r, q.start(nk), nk == GPK_DEC_IPV6);
+        st |= GPK_ST_NET_FLOW | (nk == GPK_DEC_IPV6 ? GPK_ST_NET_IPV6 : 0u);
       }
       if (tk && clean(q, tk)) {  // tcp.go:614-616 (4), udp.go:132-134 (5)
         uint32_t t0 = q.start(tk);

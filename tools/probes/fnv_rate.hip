@@ -1,7 +1,7 @@
 // Probe: cost of one FNV-1a 64 step (flows.go:60-70) on gfx950, two forms:
-//   mul: v_mad_u64_u32 + v_mul_lo_u32 (what the compiler makes of h * prime)
-//   sha: x * (2^40 + 435) as four v_lshl_add_u64 (435x = 3x + 48x + 384x), inline asm
-// 4 independent chains per lane, 8 waves per SIMD on every CU.
+//   0 mul: (h ^ b) * prime as the compiler makes it (v_mad_u64_u32 + v_mul_lo_u32 + adds)
+//   1 mad: lo' : hi' = mad_u64(x, 0x1b3, (hi * 0x1b3 + (x << 8)) << 32), x = lo ^ b
+// 4 independent chains per lane, 8 waves per SIMD on every CU. Both forms must agree.
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdint>
@@ -13,14 +13,10 @@ __device__ __forceinline__ uint64_t step_mul(uint64_t h, uint32_t b) {
   uint32_t rhi = (uint32_t)(m >> 32) + hi * 0x1b3u + (lo << 8);
   return ((uint64_t)rhi << 32) | (uint32_t)m;
 }
-__device__ __forceinline__ uint64_t step_sha(uint64_t h, uint32_t b) {
-  const uint64_t x = h ^ b;
-  uint64_t a, r, o;
-  asm volatile("v_lshl_add_u64 %0, %1, 1, %1" : "=v"(a) : "v"(x));
-  asm volatile("v_lshl_add_u64 %0, %1, 4, %1" : "=v"(r) : "v"(a));
-  asm volatile("v_lshl_add_u64 %0, %1, 7, %2" : "=v"(o) : "v"(a), "v"(r));
-  asm volatile("v_lshl_add_u64 %0, %1, 40, %2" : "=v"(r) : "v"(x), "v"(o));
-  return r;
+__device__ __forceinline__ uint64_t step_mad(uint64_t h, uint32_t b) {
+  const uint32_t x = (uint32_t)h ^ b, hi = (uint32_t)(h >> 32);
+  const uint32_t s = hi * 0x1b3u + (x << 8);
+  return (uint64_t)x * 0x1b3u + ((uint64_t)s << 32);
 }
 template <int K>
 __global__ void k(uint64_t* out, uint32_t n) {
@@ -30,7 +26,7 @@ __global__ void k(uint64_t* out, uint32_t n) {
     if (K == 0) {
       h0 = step_mul(h0, b); h1 = step_mul(h1, b); h2 = step_mul(h2, b); h3 = step_mul(h3, b);
     } else {
-      h0 = step_sha(h0, b); h1 = step_sha(h1, b); h2 = step_sha(h2, b); h3 = step_sha(h3, b);
+      h0 = step_mad(h0, b); h1 = step_mad(h1, b); h2 = step_mad(h2, b); h3 = step_mad(h3, b);
     }
   }
   out[blockIdx.x * blockDim.x + threadIdx.x] = h0 ^ h1 ^ h2 ^ h3;
@@ -45,23 +41,23 @@ int main() {
     (void)hipEventCreate(&e0);
     (void)hipEventCreate(&e1);
     const uint32_t n = 4096;
-    for (int rep = 0; rep < 2; rep++) {
+    float ms = 0;
+    for (int rep = 0; rep < 3; rep++) {
       (void)hipEventRecord(e0);
       if (kind == 0) hipLaunchKernelGGL(k<0>, dim3(blocks), dim3(threads), 0, 0, d, n);
       else hipLaunchKernelGGL(k<1>, dim3(blocks), dim3(threads), 0, 0, d, n);
       (void)hipEventRecord(e1);
       (void)hipEventSynchronize(e1);
+      (void)hipEventElapsedTime(&ms, e0, e1);
     }
-    float ms = 0;
-    (void)hipEventElapsedTime(&ms, e0, e1);
-    uint64_t h;
-    (void)hipMemcpy(&h, d + 12345, 8, hipMemcpyDeviceToHost);
+    uint64_t h = 0;
+    (void)hipMemcpy(&h, d, 8, hipMemcpyDeviceToHost);
     ref[kind] = h;
-    // steps per wave per SIMD-cycle at an assumed 2.4 GHz, 1024 SIMDs
-    const double steps = (double)blocks * threads / 64 * 4 * n;
-    printf("%s: %.3f ms, %.2f cycles per wave-step (2.4 GHz, 1024 SIMDs)\n", kind ? "shift-add" : "mul", ms,
-           ms * 1e-3 * 2.4e9 * 1024 / steps);
+    // steps per SIMD: blocks*threads/64 waves * 4 chains * n over 1024 SIMDs
+    const double waves = (double)blocks * threads / 64, steps = waves * 4 * n;
+    const double cyc = ms * 1e-3 * 2.4e9 * 1024;  // SIMD-cycles at 2.4 GHz
+    printf("kind %d (%s): %.3f ms, %.2f SIMD-cycles per wave-step\n", kind, kind ? "mad" : "mul", ms, cyc / steps);
   }
-  printf("same hashes: %s\n", ref[0] == ref[1] ? "yes" : "NO");
-  return 0;
+  printf("agree: %s\n", ref[0] == ref[1] ? "yes" : "NO");
+  return ref[0] == ref[1] ? 0 : 1;
 }
