@@ -900,68 +900,77 @@ __device__ __forceinline__ uint64_t fnv_bytes(const R& r, uint32_t p, uint32_t n
   for (uint32_t i = 0; i < n; i++) h = fnv_step(h, rd8(r, p + i));
   return h;
 }
-// N bytes from the LDS window: dword reads, bytes taken in order
-template <int N>
-__device__ __forceinline__ uint64_t fnv_lds(uint32_t a) {
-  uint64_t h = 14695981039346656037ull;
-#pragma unroll
-  for (int k = 0; k < N; k += 4) {
-    const uint32_t w = lds32u(a + k);
-#pragma unroll
-    for (int j = 0; j < 4 && k + j < N; j++) h = fnv_step(h, (w >> (8 * j)) & 0xffu);
-  }
-  return h;
-}
-template <int N>
-__device__ __forceinline__ uint64_t fnv_range(const Rd& r, uint32_t p) {
-  if (p + N <= r.win) return fnv_lds<N>(r.lb + p);
-  return fnv_bytes(r, p, N);
-}
-// NetworkFlow().FastHash() of an IPv4 (ip4.go:63-65, EndpointIPv4 = 1) or
-// IPv6 (ip6.go:49-51, EndpointIPv6 = 2) header at packet offset ns: source
-// and destination addresses (4 or 16 bytes each) hashed in one loop of 1 or
-// 4 dwords, so a wave holding both kinds runs 16 steps per address, not
-// 4 + 16. The dword count is uniform over the active lanes; IPv4 lanes keep
-// the state after their first dword.
-__device__ __forceinline__ uint64_t net_flow_hash(const Rd& r, uint32_t ns, bool v6);
 // Flow.FastHash flows.go:167-174
 __device__ __forceinline__ uint64_t flow_hash(uint64_t hs, uint64_t hd, uint32_t typ) {
   return ((hs + hd) ^ (uint64_t)typ) * 1099511628211ull;
 }
-__device__ __forceinline__ uint64_t net_flow_hash(const Rd& r, uint32_t ns, bool v6) {
+// The three Flow.FastHash values of a packet (flows.go:167-174):
+//   LinkFlow       ethernet.go:38-40  source MAC at e0+6, destination at e0 (EndpointMAC = 3)
+//   NetworkFlow    ip4.go:63-65 / ip6.go:49-51  addresses at ns+12 (4 bytes each, EndpointIPv4 = 1)
+//                  or ns+8 (16 bytes each, EndpointIPv6 = 2)
+//   TransportFlow  tcp.go:614-616 / udp.go:132-134  ports at t0, t0+2 (4 / 5)
+// All six FNV chains are computed in one block of straight-line code so
+// their multiplies interleave; the caller keeps the ones whose layer exists.
+// Addresses are hashed one dword per step: 1 dword for IPv4, 4 for IPv6,
+// with the count uniform over the active lanes (IPv4 lanes keep the state
+// after their first dword), so a wave holding both runs 16 steps per address,
+// not 4 + 16. Bytes past the LDS window (deep stacks) go through the mixed
+// reader.
+__device__ __forceinline__ void fnv_dword(uint64_t& h, uint32_t w, int j0, int j1) {
+#pragma unroll
+  for (int j = j0; j < j1; j++) h = fnv_step(h, (w >> (8 * j)) & 0xffu);
+}
+// fl / fn / ft: which of the three layers exist (their offsets are 0 otherwise
+// and their chains hash window bytes that are then dropped).
+__device__ __forceinline__ void flow_hashes(const Rd& r, bool fl, uint32_t e0, bool fn, uint32_t ns, bool v6, bool ft,
+                                            uint32_t t0, uint32_t tcode, uint64_t& lflow, uint64_t& nflow,
+                                            uint64_t& tflow) {
+  constexpr uint64_t kBasis = 14695981039346656037ull;
   const uint32_t n = v6 ? 16u : 4u, a = ns + (v6 ? 8u : 12u);
-  const bool inwin = a + 2 * n <= r.win;
-  uint64_t hs = 14695981039346656037ull, hd = hs;
-  if (__ballot(!inwin)) {  // rare: an address past the LDS window (deep stacks)
-    if (!inwin) {
+  const bool inwin = (!fl || e0 + 12 <= r.win) && (!fn || a + 2 * n <= r.win) && (!ft || t0 + 4 <= r.win);
+  uint64_t ls = kBasis, ld = kBasis, ts = kBasis, td = kBasis, hs = kBasis, hd = kBasis;
+  if (__ballot(!inwin)) {  // rare: a field past the window; only the layers that exist are read
+    if (!inwin && fl) {
+      ls = fnv_bytes(r, e0 + 6, 6);
+      ld = fnv_bytes(r, e0, 6);
+    }
+    if (!inwin && fn) {
       hs = fnv_bytes(r, a, n);
       hd = fnv_bytes(r, a + n, n);
     }
+    if (!inwin && ft) {
+      ts = fnv_bytes(r, t0, 2);
+      td = fnv_bytes(r, t0 + 2, 2);
+    }
   }
   if (inwin) {
-    const uint32_t nd = __ballot(inwin && v6) ? 4u : 1u;
-    uint64_t hs4 = 0, hd4 = 0;
+    const uint32_t wl0 = lds32u(r.lb + e0), wl1 = lds32u(r.lb + e0 + 4), wl2 = lds32u(r.lb + e0 + 8);
+    const uint32_t wt = lds32u(r.lb + t0);
+    const uint32_t ws0 = lds32u(r.lb + a), wd0 = lds32u(r.lb + a + n);
+    fnv_dword(ld, wl0, 0, 4);
+    fnv_dword(ld, wl1, 0, 2);
+    fnv_dword(ls, wl1, 2, 4);
+    fnv_dword(ls, wl2, 0, 4);
+    fnv_dword(ts, wt, 0, 2);
+    fnv_dword(td, wt, 2, 4);
+    fnv_dword(hs, ws0, 0, 4);
+    fnv_dword(hd, wd0, 0, 4);
+    if (__ballot(inwin && v6)) {
+      const uint64_t hs4 = hs, hd4 = hd;
 #pragma unroll
-    for (uint32_t k = 0; k < 4; k++) {
-      if (k < nd) {
-        const uint32_t ws = lds32u(r.lb + a + 4 * k), wd = lds32u(r.lb + a + n + 4 * k);
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-          hs = fnv_step(hs, (ws >> (8 * j)) & 0xffu);
-          hd = fnv_step(hd, (wd >> (8 * j)) & 0xffu);
-        }
-        if (k == 0) {
-          hs4 = hs;
-          hd4 = hd;
-        }
+      for (uint32_t k = 1; k < 4; k++) {
+        fnv_dword(hs, lds32u(r.lb + a + 4 * k), 0, 4);
+        fnv_dword(hd, lds32u(r.lb + a + n + 4 * k), 0, 4);
+      }
+      if (!v6) {
+        hs = hs4;
+        hd = hd4;
       }
     }
-    if (!v6) {
-      hs = hs4;
-      hd = hd4;
-    }
   }
-  return flow_hash(hs, hd, v6 ? 2u : 1u);
+  lflow = flow_hash(ls, ld, 3);
+  nflow = flow_hash(hs, hd, v6 ? 2u : 1u);
+  tflow = flow_hash(ts, td, tcode);
 }
 
 }  // namespace gpk

@@ -710,21 +710,15 @@ __device__ __forceinline__ void decode_packet(const KParams& P, const TT& T, uin
       job = true;
     }
     if (P.outputs & GPK_OUT_FLOWS) {
-      uint64_t lflow = 0, nflow = 0, tflow = 0;
-      if (clean(q, GPK_DEC_ETHERNET)) {  // ethernet.go:38-40 (EndpointMAC = 3)
-        uint32_t e0 = q.start(GPK_DEC_ETHERNET);
-        lflow = flow_hash(fnv_range<6>(r, e0 + 6), fnv_range<6>(r, e0), 3);
-        st |= GPK_ST_LINK_FLOW;
-      }
-      if (nk && clean(q, nk)) {  // ip4.go:63-65 / ip6.go:49-51
-        nflow = net_flow_hash(r, q.start(nk), nk == GPK_DEC_IPV6);
-        st |= GPK_ST_NET_FLOW | (nk == GPK_DEC_IPV6 ? GPK_ST_NET_IPV6 : 0u);
-      }
-      if (tk && clean(q, tk)) {  // tcp.go:614-616 (4), udp.go:132-134 (5)
-        uint32_t t0 = q.start(tk);
-        tflow = flow_hash(fnv_range<2>(r, t0), fnv_range<2>(r, t0 + 2), tk == GPK_DEC_TCP ? 4 : 5);
-        st |= GPK_ST_TRANSPORT_FLOW;
-      }
+      const bool fl = clean(q, GPK_DEC_ETHERNET), fn = nk && clean(q, nk), ft = tk && clean(q, tk);
+      uint64_t lflow, nflow, tflow;
+      flow_hashes(r, fl, fl ? q.start(GPK_DEC_ETHERNET) : 0u, fn, fn ? q.start(nk) : 0u, nk == GPK_DEC_IPV6, ft,
+                  ft ? q.start(tk) : 0u, tk == GPK_DEC_TCP ? 4u : 5u, lflow, nflow, tflow);
+      lflow = fl ? lflow : 0;
+      nflow = fn ? nflow : 0;
+      tflow = ft ? tflow : 0;
+      st |= (fl ? GPK_ST_LINK_FLOW : 0u) | (fn ? GPK_ST_NET_FLOW : 0u) |
+            (fn && nk == GPK_DEC_IPV6 ? GPK_ST_NET_IPV6 : 0u) | (ft ? GPK_ST_TRANSPORT_FLOW : 0u);
       if (P.flows) {
         __builtin_nontemporal_store(lflow, P.flows + i);
         __builtin_nontemporal_store(nflow, P.flows + P.n + i);
