@@ -65,6 +65,12 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 #ifndef GPK_BLOB_ROUND
 #define GPK_BLOB_ROUND 128  // dwords: the table blob's LDS share is rounded to this
 #endif
+#ifndef GPK_PB_EARLY
+#define GPK_PB_EARLY 1  // passes of the dense stream issued before DecodeLayers (0: none), 80-VGPR kernels (A/B r04k: C3 -2.4 %)
+#endif
+#ifndef GPK_PB_EARLY7
+#define GPK_PB_EARLY7 0  // ... in the 72-VGPR kernels (A/B r04k: C4 +0.6 %, C1 +2 % with 1)
+#endif
 #ifndef GPK_PB_SDEPTH
 #define GPK_PB_SDEPTH 4  // sparse phase B: 1 KiB wave loads in flight
 #endif
@@ -460,18 +466,88 @@ __device__ __forceinline__ void slot_wait_n(u32x4 (&c)[kGran], int n) {
   }
 }
 
+// The dense stream of one wave: region [R0, R0 + R) (R0 16-byte aligned),
+// D passes in flight in fixed slot registers. Started early (stream_start,
+// before DecodeLayers, from the packet extents) when the wave's packets are
+// packed, so the first D KiB arrive while the headers are parsed.
 template <int D>
-__device__ __forceinline__ uint32_t dense_segment_sums(const KParams& P, uint64_t R0, uint32_t R, bool job,
-                                                       uint64_t s, uint64_t e, uint32_t lane, uint32_t hlds,
-                                                       uint32_t tlds) {
-  static_assert(kGran == 1, "head/tail chunks from the LDS window need 16-byte granules");
+struct Stream {
+  Gran ring[D];
+  uint64_t R0;
+  uint32_t R;
+  bool on;
+};
+
+// Issue passes [d0, d1) of the stream over [R0, R0 + R) into their slots.
+template <int D>
+__device__ __forceinline__ void stream_issue(const KParams& P, Stream<D>& S, uint64_t R0, uint32_t R, uint32_t lane,
+                                             int d0, int d1) {
+  S.R0 = R0;
+  S.R = R;
+  S.on = true;
   // whole 16-byte chunks: the range check zeroes a 16-byte load that
   // crosses the record limit, not just its bytes past it
   const __amdgpu_buffer_rsrc_t rs = rsrc(P.data + R0, (R + 15) & ~15u);
+#pragma unroll
+  for (int d = 0; d < D; d++) {
+    if (d < d0 || d >= d1) continue;
+#pragma unroll
+    for (int k = 0; k < kGran; k++) S.ring[d].c[k] = u32x4{0, 0, 0, 0};
+    slot_load(S.ring[d].c, rs, lane * kGranBytes, d * kPassBytes);
+  }
+}
+
+// Whether the byte ranges [s, e) of the lanes with `job` lie in one compact
+// region (at most 4 x their total + 8 KiB, within +-2 GiB of a wave-uniform
+// base, none over 64 KiB: l_to_words); returns it as R0 / R.
+__device__ __forceinline__ bool dense_region(bool job, uint64_t s, uint64_t e, uint64_t& R0, uint32_t& R) {
+  const uint64_t jobs = __ballot(job);
+  if (!jobs) return false;
+  // relative to a wave-uniform base (the first job lane's chunk), in 32-bit
+  // biased coordinates
+  const uint64_t B = readlane64(s, (uint32_t)__builtin_ctzll(jobs)) & ~15ull;
+  constexpr uint64_t kBias = 0x80000000ull;
+  const uint64_t bs = s + kBias - B, be = e + kBias - B;
+  const bool far = job && (bs >> 32 || be >> 32 || e - s > 65536u);
+  const uint32_t lo = wave_min(job ? (uint32_t)bs : 0xffffffffu);
+  const uint32_t hi = wave_max(job ? (uint32_t)be : 0u);
+  const uint32_t tot = wave_sum(job ? (uint32_t)(e - s) : 0u);
+  const uint32_t lo16 = lo & ~15u;
+  R0 = B + lo16 - kBias;
+  R = hi - lo16;
+  return !__ballot(far) && hi - lo16 <= 4u * tot + 8192u;
+}
+
+// Early start: the packets of the wave (not yet parsed) as the region; the
+// first E passes are issued now (their slot registers stay live through
+// DecodeLayers, so only a few: tools/check_stream_isa.py rejects a build
+// whose register allocation touches them), the rest when phase B begins.
+template <int D, int E>
+__device__ __forceinline__ void stream_start(const KParams& P, Stream<D>& S, bool active, uint64_t off, uint32_t cl,
+                                             uint32_t lane) {
+  uint64_t R0;
+  uint32_t R;
+  S.on = false;
+  if (dense_region(active, off, off + cl, R0, R)) stream_issue(P, S, R0, R, lane, 0, E < D ? E : D);
+}
+
+// All stream loads of the wave have landed (the slot registers are free).
+template <int D>
+__device__ __forceinline__ void stream_drain(Stream<D>& S) {
+#pragma unroll
+  for (int d = 0; d < D; d++) slot_wait<0>(S.ring[d].c);
+}
+
+template <int D>
+__device__ __forceinline__ uint32_t dense_segment_sums(const KParams& P, Stream<D>& S, bool job, uint64_t s,
+                                                       uint64_t e, uint32_t lane, uint32_t hlds, uint32_t tlds) {
+  static_assert(kGran == 1, "head/tail chunks from the LDS window need 16-byte granules");
+  const uint64_t R0 = S.R0;
+  const uint32_t R = S.R;
+  const __amdgpu_buffer_rsrc_t rs = rsrc(P.data + R0, (R + 15) & ~15u);
   const uint32_t rsl = job ? (uint32_t)(s - R0) : 0u, rel = job ? (uint32_t)(e - R0) : 0u;
-  // head / tail chunks, summed before the stream starts (their wait must
-  // not drain the stream): from the LDS header windows when a window holds
-  // them (hlds / tlds = LDS byte address, else ~0), else from memory
+  // head / tail chunks: from the LDS header windows when a window holds them
+  // (hlds / tlds = LDS byte address, else ~0), else from memory
   uint32_t L = 0;
   {
     u32x4 hc = lds_chunk(hlds), tc = lds_chunk(tlds);
@@ -481,17 +557,7 @@ __device__ __forceinline__ uint32_t dense_segment_sums(const KParams& P, uint64_
   }
   const uint32_t np = (R + kPassBytes - 1) / kPassBytes;  // wave-uniform
   const uint32_t vo = lane * kGranBytes;
-  Gran ring[D];
-#pragma unroll
-  for (int d = 0; d < D; d++) {
-#pragma unroll
-    for (int k = 0; k < kGran; k++) ring[d].c[k] = u32x4{0, 0, 0, 0};
-    slot_load(ring[d].c, rs, vo, d * kPassBytes);
-  }
-  // prefix targets: through granule gs-1 (a) and ge-1 (b); -1 = the empty
-  // prefix. Target t sits in pass t >> 6 at lane t & 63. In its pass a lane
-  // pulls lane t's prefix with ds_bpermute; in every other pass it pulls its
-  // own (identity permutation: no bank conflicts), which the select drops.
+  Gran (&ring)[D] = S.ring;
   const int32_t a = (int32_t)(rsl / kGranBytes) - 1, b = (int32_t)(rel / kGranBytes) - 1;
   const int32_t pa = a >> 6, pb = b >> 6;  // -1 never matches
   const int32_t la = (a & 63) << 2, lb = (b & 63) << 2, ll = (int32_t)lane << 2;
@@ -528,8 +594,7 @@ __device__ __forceinline__ uint32_t dense_segment_sums(const KParams& P, uint64_
     pass(d, (int32_t)(p0 + d), false);
   }
   L += xb - xa;
-#pragma unroll
-  for (int d = 0; d < D; d++) slot_wait<0>(ring[d].c);  // the last refills land before the registers are reused
+  stream_drain(S);  // the last refills land before the registers are reused
   return l_to_words(L, (uint32_t)s & 1u);
 }
 
@@ -615,26 +680,33 @@ __device__ __forceinline__ uint32_t sparse_segment_sums(const KParams& P, bool j
   return own;
 }
 
-// Word sums of every job lane's segment [s, e): dense prefix stream when the
-// wave's segments share a compact region, else the per-segment stream.
-template <int D>
-__device__ __forceinline__ uint32_t segment_sums(const KParams& P, bool job, uint64_t s, uint64_t e, uint32_t lane,
-                                                 uint32_t hlds, uint32_t tlds) {
-  const uint64_t jobs = __ballot(job);
-  if (!jobs) return 0;
-  // region relative to a wave-uniform base (the first job lane's chunk), in
-  // 32-bit biased coordinates; lanes too far from it (or with a segment over
-  // 64 KiB) make the wave sparse
-  const uint64_t B = readlane64(s, (uint32_t)__builtin_ctzll(jobs)) & ~15ull;
-  constexpr uint64_t kBias = 0x80000000ull;
-  const uint64_t bs = s + kBias - B, be = e + kBias - B;
-  const bool far = job && (bs >> 32 || be >> 32 || e - s > 65536u);  // far, or too long for l_to_words
-  const uint32_t lo = wave_min(job ? (uint32_t)bs : 0xffffffffu);
-  const uint32_t hi = wave_max(job ? (uint32_t)be : 0u);
-  const uint32_t tot = wave_sum(job ? (uint32_t)(e - s) : 0u);
-  const uint32_t lo16 = lo & ~15u;
-  const bool dense = !__ballot(far) && hi - lo16 <= 4u * tot + 8192u;
-  if (dense) return dense_segment_sums<D>(P, B + lo16 - kBias, hi - lo16, job, s, e, lane, hlds, tlds);
+// Word sums of every job lane's segment [s, e): the dense prefix stream (the
+// one started early, else one over the segments' region when that is
+// compact), else the per-segment stream.
+template <int D, int E>
+__device__ __forceinline__ uint32_t segment_sums(const KParams& P, Stream<D>& S, bool job, uint64_t s, uint64_t e,
+                                                 uint32_t lane, uint32_t hlds, uint32_t tlds) {
+  if (S.on) {
+    if (!__ballot(job)) {  // nothing to sum: the early loads still land before their registers are reused
+      stream_drain(S);
+      return 0;
+    }
+    // The early passes have landed during the parse; waiting for them here
+    // (their registers as operands) puts any register copy the allocator
+    // needs between the early slots and the loop's after the data is in.
+    stream_drain(S);
+    stream_issue(P, S, S.R0, S.R, lane, E < D ? E : D, D);
+    return dense_segment_sums<D>(P, S, job, s, e, lane, hlds, tlds);
+  }
+  // (with the early start on, a wave whose packets are not packed goes to
+  // the per-segment stream: one call site keeps the slot registers in place)
+  uint64_t R0;
+  uint32_t R;
+  if (E == 0 && dense_region(job, s, e, R0, R)) {
+    stream_issue(P, S, R0, R, lane, 0, D);
+    return dense_segment_sums<D>(P, S, job, s, e, lane, hlds, tlds);
+  }
+  if (!__ballot(job)) return 0;
   return sparse_segment_sums(P, job, s, e, lane);
 }
 
@@ -645,6 +717,16 @@ __device__ __forceinline__ void decode_packet(const KParams& P, const TT& T, uin
   uint32_t win = W * 16 - m;
   if (cl < win) win = cl;
   Rd r{P.data + off, slot_dw * 4 + m, win};
+
+  // Phase B's stream over the wave's packets starts now when they are packed:
+  // its first D KiB load while the headers are parsed.
+  constexpr int D = kLayout ? 4 : (O > 6 ? GPK_PB_DEPTH7 : GPK_PB_DEPTH);  // layouts: fewer registers left
+  // early passes: as many as the kernel's register budget carries through
+  // DecodeLayers untouched (tools/check_stream_isa.py)
+  constexpr int E = (kLayout || kKeys) ? 0 : (O > 6 ? GPK_PB_EARLY7 : GPK_PB_EARLY);
+  Stream<D> S;
+  S.on = false;
+  if (kL4 && E > 0 && (P.outputs & GPK_OUT_L4_CSUM)) stream_start<D, E>(P, S, active, off, cl, lane);
 
   // ---- Phase A: DecodeLayers ------------------------------------------------
   Parse q;
@@ -787,8 +869,7 @@ __device__ __forceinline__ void decode_packet(const KParams& P, const TT& T, uin
       tlds = slot_dw * 4 + 16 * (uint32_t)((je >> 4) - c0);
     else if (GPK_PB_LDS_HT && job && lane < 63 && nnch && (noff >> 4) == (je >> 4))
       tlds = (slot_dw + slot_dw_of<W>()) * 4;
-    constexpr int D = kLayout ? 4 : (O > 6 ? GPK_PB_DEPTH7 : GPK_PB_DEPTH);  // layouts: fewer registers left
-    const uint32_t sum = segment_sums<D>(P, job, js, je, lane, hlds, tlds);
+    const uint32_t sum = segment_sums<D, E>(P, S, job, js, je, lane, hlds, tlds);
     if (job) {
       l4c = fold(jinit + sum - jexist);
       const bool udp = (st & GPK_ST_L4_UDP) != 0;
