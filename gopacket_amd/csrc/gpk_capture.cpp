@@ -25,8 +25,11 @@
 // readNameResolutionBlock ngread_nrb.go:63-130, readDecryptionSecretsBlock
 // ngread_dsb.go:17-39; NewReader/readHeader read.go:64-122, ReadPacketData
 // :124-140, readPacketHeader :171-180.
+#include <condition_variable>
 #include <cstdarg>
 #include <cstdio>
+#include <functional>
+#include <mutex>
 #include <cstring>
 #include <cstdlib>
 #include <new>
@@ -907,6 +910,79 @@ struct PktVec {  // growable, uninitialised arrays (malloc: gpk_capindex_free)
   }
 };
 
+// Persistent worker threads for the walk (one set per process, created on
+// first use): a staging slot is walked every few milliseconds, and spawning
+// dozens of threads per slot cost about as much as the walk itself.
+class Pool {
+ public:
+  static Pool& get() {
+    static Pool p;
+    return p;
+  }
+  // f(0) .. f(n-1) on the pool's threads and the caller's; returns when all are done
+  void run(int n, const std::function<void(int)>& f) {
+    if (n <= 0) return;
+    std::unique_lock<std::mutex> lk(mu_);
+    job_ = &f;
+    next_ = 0;
+    total_ = n;
+    left_ = n;
+    gen_++;
+    cv_.notify_all();
+    lk.unlock();
+    work();
+    lk.lock();
+    done_.wait(lk, [&] { return left_ == 0; });
+    job_ = nullptr;
+  }
+  ~Pool() {
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : th_) t.join();
+  }
+
+ private:
+  Pool() {
+    unsigned n = std::thread::hardware_concurrency();
+    n = n < 2 ? 2 : (n > 64 ? 64 : n);
+    for (unsigned k = 0; k + 1 < n; k++) th_.emplace_back([this] { loop(); });
+  }
+  void work() {  // take tasks of the current job until none is left
+    for (;;) {
+      std::unique_lock<std::mutex> lk(mu_);
+      if (!job_ || next_ >= total_) return;
+      const int k = next_++;
+      const std::function<void(int)>* f = job_;
+      lk.unlock();
+      (*f)(k);
+      lk.lock();
+      if (--left_ == 0) done_.notify_all();
+    }
+  }
+  void loop() {
+    uint64_t seen = 0;
+    for (;;) {
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+        if (stop_) return;
+        seen = gen_;
+      }
+      work();
+    }
+  }
+  std::vector<std::thread> th_;
+  std::mutex mu_;
+  std::condition_variable cv_, done_;
+  const std::function<void(int)>* job_ = nullptr;
+  int next_ = 0, total_ = 0, left_ = 0;
+  uint64_t gen_ = 0;
+  bool stop_ = false;
+};
+
 // What ReadPacketData does on a plain EPB at b[p] (ngread.go:497-527, 642-675):
 // block header; 20-byte EPB header; interface known (else an error) and, without
 // WantMixedLinkType, of the first interface's link type (else the block is
@@ -1020,40 +1096,85 @@ extern "C" int gpk_capreader_index_all(gpk_capreader* r, const uint8_t* buf, uin
         const uint64_t ver = state_version(r), span = len - pos, base = pos;
         const int T = threads > 64 ? 64 : threads;
         std::vector<Seg> seg(T);
-        std::vector<std::thread> th;
-        for (int k = 1; k < T; k++)
-          th.emplace_back([&, k] {
-            const uint64_t s0 = base + span * k / T, s1 = k + 1 < T ? base + span * (k + 1) / T : len;
-            const uint64_t to = s1 < s0 + (1u << 20) ? s1 : s0 + (1u << 20);
-            const uint64_t p = find_sync(snap, r->flags, buf, s0, to, len, base);
-            if (p != ~0ull) walk_seg(snap, r->flags, buf, p, s1, len, seg[k]);
-          });
-        // meanwhile the exact walk takes the first segment itself (the reader
-        // state it mutates is not the workers' snapshot)
-        st = seq_walk(r, buf, pos, base + span / T, 0, v, &stop);
-        pos = stop;
+        PktVec tail;  // exact-walk packets between and after the segments
+        auto fail_all = [&](int code) {
+          for (auto& sg : seg) sg.v.release();
+          tail.release();
+          v.release();
+          return code;
+        };
+        // task 0: the exact walk of the first segment (it alone mutates the
+        // reader; the workers use the snapshot); tasks 1..T-1: speculative
+        int st0 = GPK_CAP_MORE;
+        uint64_t stop0 = pos;
+        Pool::get().run(T, [&](int k) {
+          if (k == 0) {
+            st0 = seq_walk(r, buf, pos, base + span / T, 0, v, &stop0);
+            return;
+          }
+          const uint64_t s0 = base + span * k / T, s1 = k + 1 < T ? base + span * (k + 1) / T : len;
+          const uint64_t to = s1 < s0 + (1u << 20) ? s1 : s0 + (1u << 20);
+          const uint64_t p = find_sync(snap, r->flags, buf, s0, to, len, base);
+          if (p != ~0ull) walk_seg(snap, r->flags, buf, p, s1, len, seg[k]);
+        });
+        st = st0;
+        pos = stop0;
+        if (st < 0) return fail_all(st);
         if (st != GPK_CAP_MORE) done = true;
-        for (auto& t : th) t.join();
+        // Stitch in order: the exact walk runs up to each accepted segment's
+        // start (normally nothing is left to walk), the segment's packets
+        // follow. Pieces are copied into the result in parallel afterwards.
+        struct Piece {
+          const PktVec* src;  // nullptr: v itself
+          uint64_t from, n, at;
+        };
+        std::vector<Piece> pieces;
+        uint64_t total = v.n;
+        pieces.push_back({nullptr, 0, v.n, 0});
         for (int k = 1; k < T && !done; k++) {
           Seg& s = seg[k];
-          if (s.sync == ~0ull || s.sync < pos) {
-            s.v.release();
-            continue;
-          }
-          st = seq_walk(r, buf, pos, s.sync, 0, v, &stop);
+          if (s.sync == ~0ull || s.sync < pos) continue;
+          const uint64_t t0 = tail.n;
+          st = seq_walk(r, buf, pos, s.sync, 0, tail, &stop);
+          if (st < 0) return fail_all(st);
           pos = stop;
+          if (tail.n > t0) {
+            pieces.push_back({&tail, t0, tail.n - t0, total});
+            total += tail.n - t0;
+          }
           if (st != GPK_CAP_MORE) {
             done = true;
-          } else if (pos == s.sync && state_version(r) == ver && v.reserve(v.n + s.v.n)) {
-            memcpy(v.off + v.n, s.v.off, s.v.n * 8);
-            memcpy(v.cap + v.n, s.v.cap, s.v.n * 4);
-            memcpy(v.ci + v.n, s.v.ci, s.v.n * sizeof(gpk_capture_info));
-            v.n += s.v.n;
+          } else if (pos == s.sync && state_version(r) == ver) {
+            pieces.push_back({&s.v, 0, s.v.n, total});
+            total += s.v.n;
             pos = s.end;
           }
-          s.v.release();
         }
-        for (auto& s : seg) s.v.release();
+        if (!done) {  // the rest of the slot, exactly
+          const uint64_t t0 = tail.n;
+          st = seq_walk(r, buf, pos, len, eof, tail, &stop);
+          if (st < 0) return fail_all(st);
+          pos = stop;
+          if (tail.n > t0) {
+            pieces.push_back({&tail, t0, tail.n - t0, total});
+            total += tail.n - t0;
+          }
+          done = true;
+        }
+        PktVec out_v;
+        if (!out_v.reserve(total ? total : 1)) return fail_all(GPK_ENOMEM);
+        Pool::get().run((int)pieces.size(), [&](int k) {
+          const Piece& pc = pieces[k];
+          const PktVec& src = pc.src ? *pc.src : v;
+          memcpy(out_v.off + pc.at, src.off + pc.from, pc.n * 8);
+          memcpy(out_v.cap + pc.at, src.cap + pc.from, pc.n * 4);
+          memcpy(out_v.ci + pc.at, src.ci + pc.from, pc.n * sizeof(gpk_capture_info));
+        });
+        out_v.n = total;
+        for (auto& sg : seg) sg.v.release();
+        tail.release();
+        v.release();
+        v = out_v;
       }
     }
     if (!done) {
