@@ -106,7 +106,7 @@ def probe_read(data, nbytes, steps, stream):
     return (nbytes & ~15) / (e0.elapsed_time(e1) / steps * 1e-3) / 1e9
 
 
-def run_config(name, n, steps, warmup, rank, world, ctx, check_sample=2048, probe=False):
+def run_config(name, n, steps, warmup, rank, world, ctx, check_sample=2048, probe=False, full_check=False):
     import torch
     from gopacket_amd import engine, shard, synth
     cfg = CONFIGS[name]
@@ -163,7 +163,11 @@ def run_config(name, n, steps, warmup, rank, world, ctx, check_sample=2048, prob
     parity = None
     if check_sample:
         parity = sample_parity(name, cfg, rec, fl, err, first, n, check_sample)
-    res = dict(n=n, payload_bytes=payload_bytes, wall_s=wall_max, kernel_ms=kernel_ms,
+    full = None
+    if full_check:
+        full, full_s = full_parity(name, cfg, data, off, cap, rec, fl, err, n, host_cores()[0])
+        full = dict(result=full, seconds=round(full_s, 2))
+    res = dict(full_parity=full, n=n, payload_bytes=payload_bytes, wall_s=wall_max, kernel_ms=kernel_ms,
                algo_bytes=payload_bytes + INDEX_BYTES * n, parity=parity, probe_gbs=probe_gbs, strong=strong,
                kernel=kernel, blocks_per_cu=blocks_per_cu)
     del data, off, cap, rec, err, fl
@@ -228,6 +232,48 @@ def sample_parity(name, cfg, rec, fl, err, first, n, k):
         gf = torch.stack([fl[ti], fl[n + ti], fl[2 * n + ti]]).cpu().numpy().view(np.uint64).reshape(-1)
         ok = ok and bool(np.array_equal(gf, ref["flows"]))
     return "%s (%d sampled packets vs oracle)" % ("bit-exact" if ok else "MISMATCH", len(idx))
+
+
+def full_parity(name, cfg, data, off, cap, rec, fl, err, n, threads, chunk=1 << 20):
+    """Every packet of the device batch against the CPU oracle (SURVEY.md §8c
+    at full size): chunks of the batch's own bytes and index are copied back,
+    decoded by oracle/gpk_oracle.c on `threads` host threads, and the records,
+    error arguments and flows compared bit for bit with the device outputs.
+    Returns (summary string, seconds)."""
+    from gopacket_amd import _lib
+    from oracle import oracle as O
+    dec = [{"Ethernet": "ETHERNET", "Dot1Q": "DOT1Q", "IPv4": "IPV4", "IPv6": "IPV6",
+            "IPv6ExtensionSkipper": "IPV6_EXT", "TCP": "TCP", "UDP": "UDP", "Payload": "PAYLOAD"}[d]
+           for d in cfg["decoders"]]
+    p = O.OracleParser(17, dec, outputs=cfg["outputs"])
+    t0 = time.perf_counter()
+    bad, first_bad = 0, None
+    for a in range(0, n, chunk):
+        b = min(n, a + chunk)
+        o = off[a:b].cpu().numpy().astype(np.uint64)
+        c = cap[a:b].cpu().numpy().astype(np.uint32)
+        lo, hi = int(o.min()), int((o + c).max())
+        host = np.empty(hi - lo + 16, np.uint8)
+        host[:hi - lo] = data[lo:hi].cpu().numpy()
+        host[hi - lo:] = 0
+        ref = p.decode(host, o - np.uint64(lo), c, nthreads=threads, layouts=False)
+        got = rec[a * 16:b * 16].cpu().numpy().view(_lib.RECORD_DTYPE)
+        ok = got == ref["records"]
+        ge = err[2 * a:2 * b].cpu().numpy().view(np.uint32).reshape(-1, 2)
+        ok &= (ge == ref["err_args"].reshape(-1, 2)).all(axis=1)
+        if fl is not None:
+            rf = ref["flows"].reshape(3, -1)
+            for k in range(3):
+                ok &= fl[k * n + a:k * n + b].cpu().numpy().view(np.uint64) == rf[k]
+        nb = int((~ok).sum())
+        if nb and first_bad is None:
+            first_bad = a + int(np.argmin(ok))
+        bad += nb
+    secs = time.perf_counter() - t0
+    if bad:
+        return "MISMATCH (%d of %d packets differ from the oracle, first at %d)" % (bad, n, first_bad), secs
+    return "bit-exact (all %d packets vs oracle: records, error arguments%s)" % (
+        n, ", flows" if fl is not None else ""), secs
 
 
 def host_cores():
@@ -715,6 +761,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
+    ap.add_argument("--no-full-parity", action="store_true",
+                    help="skip the every-packet comparison against the oracle (sampled parity only)")
     ap.add_argument("--no-probe", action="store_true", help="skip the streaming-read reference kernel")
     ap.add_argument("--pcie", action="store_true", help="also time the host-buffer path (PCIe-inclusive)")
     ap.add_argument("--c5", type=float, default=10.0, metavar="GIB",
@@ -743,7 +791,8 @@ def main():
     for name in names:
         results[name] = run_config(name, args.packets, args.steps, args.warmup, rank, world, ctx,
                                    check_sample=0 if args.no_parity else 2048,
-                                   probe=not args.no_probe)
+                                   probe=not args.no_probe,
+                                   full_check=world == 1 and not (args.no_parity or args.no_full_parity))
     if rank == 0:
         head = names[0]
         r = results[head]
@@ -768,6 +817,7 @@ def main():
                          "algo_bytes_per_launch": r["algo_bytes"],
                          "probe_read_GBps": r["probe_gbs"] and round(r["probe_gbs"], 1)},
             "parity": r["parity"],
+            "full_parity": r["full_parity"],
             "configs": {},
         }
         for name in names[1:]:
@@ -778,7 +828,7 @@ def main():
             row = {"workload": CONFIGS[name]["workload"],
                    "value": round(pk * args.steps / s["wall_s"] / 1e6, 2), "unit": "Mpkts/s",
                    "kernel": s["kernel"], "blocks_per_cu": s["blocks_per_cu"], "kernel_ms": round(s["kernel_ms"], 4), "achieved_GBps": round(ach, 1),
-                   "frac": round(ach / HBM_PEAK_GBS, 4), "parity": s["parity"],
+                   "frac": round(ach / HBM_PEAK_GBS, 4), "parity": s["parity"], "full_parity": s["full_parity"],
                    "probe_read_GBps": s["probe_gbs"] and round(s["probe_gbs"], 1)}
             if st:
                 row.update(scaling="strong", total_packets=st["total_packets"], byte_balance=st["balance"],

@@ -5,9 +5,9 @@
 // decoders below restate layers/{ethernet,dot1q,ip4,ip6,tcp,udp}.go; their
 // results must be bit-identical to the reference (checked against oracle/).
 //
-// Bytes come from a per-lane LDS window holding the packet's first 80 bytes
-// (five 16-byte chunks, filled by the kernel); positions past the window fall
-// back to global byte loads (deep stacks, long options).
+// Bytes come from a per-lane LDS window holding the packet's first bytes (the
+// 16-byte-aligned run of W chunks, filled by the kernel); positions past the
+// window fall back to global byte loads (deep stacks, long options).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -118,26 +118,17 @@ struct Rd {
   uint32_t win;      // packet bytes present in LDS
 };
 
-// Four LDS bytes from any byte address. gfx950 serves an unaligned
-// ds_read_b32 exactly (tools/probes/lds_unaligned.hip, 64/64 byte offsets on
-// MI355X) but stalls on it (SQ_LDS_UNALIGNED_STALL: ~7 % of C4's and ~9 % of
-// C1's wave cycles, profiles/r04_pmc_occupancy.txt), and packets at arbitrary
-// offsets make most header reads unaligned. So: the two aligned dwords (one
-// ds_read2_b32) and v_alignbyte_b32 (A/B r04n: C1 -3 %, C4 +-0, C2 +1.4 %,
-// whose synthetic packets all start 16-byte aligned). A read may run up to 7
-// bytes past the bytes a caller uses (into the next slot or the table blob;
-// past the allocation the hardware returns zeros); those bytes are never used.
-#ifndef GPK_LDS_ALIGNED
-#define GPK_LDS_ALIGNED 1  // 0: one unaligned ds_read_b32
-#endif
+// Four LDS bytes from any byte address: one ds_read_b32 (gfx950 serves
+// unaligned LDS dword reads exactly: tools/probes/lds_unaligned.hip, 64/64
+// byte offsets on MI355X). A read may run up to 3 bytes past the bytes a
+// caller uses (into the next slot or the table blob; past the allocation the
+// hardware returns zeros); those bytes are never used. Two aligned dwords +
+// v_alignbyte instead, with or without the windows stored dword-rotated so
+// packet byte 0 opens the slot, measured no faster and raised the LDS
+// bank-conflict cycles 2-5x (profiles/r06_ab_lds_reads.txt).
 typedef uint32_t u32_ua __attribute__((aligned(1)));
 __device__ __forceinline__ uint32_t lds32u(uint32_t byte_addr) {
-#if GPK_LDS_ALIGNED
-  const uint32_t q = byte_addr >> 2;
-  return __builtin_amdgcn_alignbyte(gpk_smem[q + 1], gpk_smem[q], byte_addr & 3u);
-#else
   return *reinterpret_cast<const u32_ua*>(reinterpret_cast<const uint8_t*>(gpk_smem) + byte_addr);
-#endif
 }
 // big-endian 16 / 32 bits of the four bytes w = b0 | b1 << 8 | ... (v_perm_b32)
 __device__ __forceinline__ uint32_t be16_of(uint32_t w) { return __builtin_amdgcn_perm(0u, w, 0x0c0c0001u); }

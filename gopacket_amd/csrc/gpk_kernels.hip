@@ -4,9 +4,11 @@
 //
 // One workgroup = 256 packets = 4 waves, one lane per packet.
 //
-//  Phase A (lane per packet): the packet's first 80 bytes (five 16-byte
-//    aligned chunks) are loaded into the lane's LDS slot; the lane runs
-//    DecodeLayers (gpk_device.h) out of LDS, computes the IPv4 header checksum
+//  Phase A (lane per packet): the 16-byte-aligned run of W chunks holding
+//    the packet's first bytes (W = 6: 96 bytes; 4 for header-only parsers)
+//    is loaded into the lane's LDS slot; the lane runs DecodeLayers
+//    (gpk_device.h: a straight-line common case, else the general state
+//    machine) out of LDS, computes the IPv4 header checksum
 //    (ip4.go:323-332), the three Flow.FastHash values (flows.go:167-174) and,
 //    for the TCP/UDP checksum (tcpip.go:54-69), the pseudo-header sum and the
 //    byte range [s, e) of the segment.
@@ -884,10 +886,11 @@ __device__ __forceinline__ void decode_packet(const KParams& P, const TT& T, uin
 // (after the header-window slots) and every NextLayerType lookup is an LDS
 // read; otherwise they are read from the global DevTables. Either way the
 // only vector-memory traffic of the decode is the packet bytes themselves.
-// W: header-window chunks. The 5-chunk default holds Ethernet + two tags +
-// IPv6 + TCP; parsers with no Dot1Q/IPv6/TCP decoder and no L4 checksum (C2)
-// run a 4-chunk window whose smaller LDS slot and 64-VGPR budget give 8 waves
-// per SIMD (A/B: C2 -8.6 %, C4 and C3 no gain or worse with 4 chunks).
+// W: header-window chunks. The 6-chunk default holds Ethernet + two tags +
+// IPv6 + TCP with timestamps at any packet alignment; parsers with no
+// Dot1Q/IPv6/TCP decoder and no L4 checksum (C2) run a 4-chunk window whose
+// smaller LDS slot and 64-VGPR budget give 8 waves per SIMD (A/B: C2 -8.6 %,
+// C4 and C3 no gain or worse with 4 chunks).
 // O: waves per SIMD the register budget is cut for. Batches of small packets
 // (mean < 1 KiB) are issue-bound in the header phase and run O = 7 (72 VGPRs;
 // with the table blob sized to the parser, 7 blocks fit a CU's LDS); big
