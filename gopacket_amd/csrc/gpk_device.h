@@ -66,6 +66,7 @@ struct KParams {
   // GPK_GROUP_DEFRAG; per packet 10 key words, a 64-bit hash and a reason code
   int32_t key_kind;
   uint32_t small_headers;   // no Dot1Q / IPv6 / IPv6-extension / TCP decoder: a 4-chunk window suffices
+  uint32_t mid_headers;     // no IPv6 / IPv6-extension decoder: the small-packet kernel's 5-chunk window suffices
   uint32_t big_packets;     // batch bytes / packets >= 1 KiB: launch choice only (occupancy)
   uint32_t* keys;
   uint64_t* khash;

@@ -397,9 +397,13 @@ static int upload(gpk_ctx* c, const gpk_parser* p, gpk::KParams& P, int* slot) {
   P.fast = fast_flags(p);
   // headers that fit the 4-chunk window: no decoder that adds tags, IPv6, extension headers or TCP options
   P.small_headers = 1;
+  // headers that fit the 5-chunk dword-aligned window (>= 77 bytes): no IPv6 decoder (Ethernet + two tags +
+  // IPv4 + TCP with timestamps is 74 bytes)
+  P.mid_headers = 1;
   for (int t2 = 0; t2 < GPK_MAX_LAYER_TYPE; t2++) {
     const int kd = p->tab.dispatch[t2];
     if (kd == GPK_DEC_DOT1Q || kd == GPK_DEC_IPV6 || kd == GPK_DEC_IPV6_EXT || kd == GPK_DEC_TCP) P.small_headers = 0;
+    if (kd == GPK_DEC_IPV6 || kd == GPK_DEC_IPV6_EXT) P.mid_headers = 0;
   }
   return GPK_OK;
 }
@@ -450,6 +454,7 @@ static int make_params(gpk_ctx* c, const gpk_parser* p, const gpk_batch* b, cons
   P.ignore_unsupported = p->ignore_unsupported;
   P.key_kind = 0;
   P.small_headers = 0;
+  P.mid_headers = 0;
   P.keys = nullptr;
   P.khash = nullptr;
   P.kcode = nullptr;

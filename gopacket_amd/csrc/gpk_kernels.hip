@@ -48,6 +48,9 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 #ifndef GPK_W4_WAVES
 #define GPK_W4_WAVES 8  // 4-chunk window kernel: 64 VGPRs
 #endif
+#ifndef GPK_MID_W5
+#define GPK_MID_W5 1  // small-packet kernels of parsers without IPv6: dword-aligned 5-chunk window
+#endif
 #ifndef GPK_PB_GRAN
 #define GPK_PB_GRAN 1  // dense phase B: 16-byte chunks per lane per pass (A/B r03: 1 KiB passes, whole
                        // lines per load instruction, beat 2 KiB passes of two half-coalesced loads by 20 %)
@@ -313,20 +316,34 @@ __device__ __forceinline__ Idx load_index(const KParams& P, uint64_t i) {
   return Idx{P.offsets[j], P.caplens[j]};
 }
 
-template <int W>
+// AL: the window's alignment. 16: the run of 16-byte-aligned chunks holding
+// the packet's first bytes (window = 16W - (off & 15) bytes, 16W - 15 at
+// worst); 4: W 16-byte loads from the packet's own dword, off & ~3 (a
+// dword-aligned global_load_dwordx4; window >= 16W - 3 bytes, so one chunk
+// fewer covers the same headers and the LDS slot shrinks by 16 bytes).
+template <int W, int AL>
 __device__ __forceinline__ uint32_t win_chunks(const Idx& x, bool active) {
-  const uint32_t m = (uint32_t)(x.off & 15);
+  const uint32_t m = (uint32_t)(x.off & (AL - 1));
   uint32_t win = W * 16 - m;
   if (x.cl < win) win = x.cl;
   return active ? (m + win + 15) >> 4 : 0;
 }
 
-template <int W>
+typedef u32x4 u32x4_a4 __attribute__((aligned(4)));
+template <int W, int AL>
 __device__ __forceinline__ void load_window(const KParams& P, const Idx& x, uint32_t nchunk, WinT<W>& w) {
-  const uint8_t* src = nchunk ? P.data + (x.off & ~15ull) : reinterpret_cast<const uint8_t*>(P.tab);
+  const uint8_t* src = nchunk ? P.data + (x.off & ~(uint64_t)(AL - 1)) : reinterpret_cast<const uint8_t*>(P.tab);
   const uint32_t last = nchunk ? nchunk - 1 : 0;
 #pragma unroll
-  for (int k = 0; k < W; k++) w.v[k] = ld16(src + 16 * ((uint32_t)k < last ? (uint32_t)k : last));
+  for (int k = 0; k < W; k++) {
+    const uint8_t* p = src + 16 * ((uint32_t)k < last ? (uint32_t)k : last);
+    if (AL == 16) {
+      w.v[k] = ld16(p);
+    } else {
+      const u32x4 v = *reinterpret_cast<const u32x4_a4*>(p);
+      w.v[k] = make_uint4(v.x, v.y, v.z, v.w);
+    }
+  }
 }
 
 template <int W>
@@ -712,10 +729,10 @@ __device__ __forceinline__ uint32_t segment_sums(const KParams& P, Stream<D>& S,
   return sparse_segment_sums(P, job, s, e, lane);
 }
 
-template <bool kL4, bool kLayout, class TT, bool kKeys, int W, int O>
+template <bool kL4, bool kLayout, class TT, bool kKeys, int W, int O, int AL>
 __device__ __forceinline__ void decode_packet(const KParams& P, const TT& T, uint64_t i, bool active, uint64_t off,
                                               uint32_t cl, uint32_t slot_dw, uint32_t lane) {
-  const uint32_t m = (uint32_t)(off & 15);
+  const uint32_t m = (uint32_t)(off & (AL - 1));
   uint32_t win = W * 16 - m;
   if (cl < win) win = cl;
   Rd r{P.data + off, slot_dw * 4 + m, win};
@@ -866,11 +883,21 @@ __device__ __forceinline__ void decode_packet(const KParams& P, const TT& T, uin
     const uint64_t noff = (uint64_t)noff_hi << 32 | noff_lo;
     const uint64_t c0 = off >> 4;
     uint32_t hlds = ~0u, tlds = ~0u;
-    if (GPK_PB_LDS_HT && job && (js >> 4) - c0 < nch) hlds = slot_dw * 4 + 16 * (uint32_t)((js >> 4) - c0);
-    if (GPK_PB_LDS_HT && job && (je >> 4) - c0 < nch)
-      tlds = slot_dw * 4 + 16 * (uint32_t)((je >> 4) - c0);
-    else if (GPK_PB_LDS_HT && job && lane < 63 && nnch && (noff >> 4) == (je >> 4))
-      tlds = (slot_dw + slot_dw_of<W>()) * 4;
+    if (AL == 16) {
+      if (GPK_PB_LDS_HT && job && (js >> 4) - c0 < nch) hlds = slot_dw * 4 + 16 * (uint32_t)((js >> 4) - c0);
+      if (GPK_PB_LDS_HT && job && (je >> 4) - c0 < nch)
+        tlds = slot_dw * 4 + 16 * (uint32_t)((je >> 4) - c0);
+      else if (GPK_PB_LDS_HT && job && lane < 63 && nnch && (noff >> 4) == (je >> 4))
+        tlds = (slot_dw + slot_dw_of<W>()) * 4;
+    } else {
+      // the window holds batch bytes [off & ~3, +16 nch): a head/tail chunk
+      // (16-byte aligned in the batch, dword-aligned in the slot) is taken
+      // from it when the bytes before s / e that it contributes are there
+      const uint64_t wb = off & ~3ull;
+      const uint32_t hb = (uint32_t)((js & ~15ull) - wb), tb = (uint32_t)((je & ~15ull) - wb);
+      if (GPK_PB_LDS_HT && job && hb < 16 * nch && hb + (uint32_t)(js & 15) <= 16 * nch) hlds = slot_dw * 4 + hb;
+      if (GPK_PB_LDS_HT && job && tb < 16 * nch && tb + (uint32_t)(je & 15) <= 16 * nch) tlds = slot_dw * 4 + tb;
+    }
     const uint32_t sum = segment_sums<D, E>(P, S, job, js, je, lane, hlds, tlds);
     if (job) {
       l4c = fold(jinit + sum - jexist);
@@ -895,7 +922,8 @@ __device__ __forceinline__ void decode_packet(const KParams& P, const TT& T, uin
 // (mean < 1 KiB) are issue-bound in the header phase and run O = 7 (72 VGPRs;
 // with the table blob sized to the parser, 7 blocks fit a CU's LDS); big
 // packets keep O = 6.
-template <bool kL4, bool kLayout, bool kCompact, bool kKeys = false, int W = kWinChunks, int O = GPK_WAVES_PER_EU>
+template <bool kL4, bool kLayout, bool kCompact, bool kKeys = false, int W = kWinChunks, int O = GPK_WAVES_PER_EU,
+          int AL = 16>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W == 4 ? GPK_W4_WAVES : O, 8))) void decode_kernel(
     KParams P) {
   const uint32_t tid = threadIdx.x;
@@ -906,9 +934,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W == 4 ?
   // flight together: two dependent memory round trips per packet.
   const uint64_t i0 = (uint64_t)blockIdx.x * kBlock + tid;
   const Idx c0 = load_index(P, i0);
-  const uint32_t n0 = win_chunks<W>(c0, i0 < P.n);
+  const uint32_t n0 = win_chunks<W, AL>(c0, i0 < P.n);
   WinT<W> w0;
-  load_window(P, c0, n0, w0);
+  load_window<W, AL>(P, c0, n0, w0);
   if (kCompact) {  // the table blob (<= kCtDwords): clamped indices, duplicate writes of equal values
     static_assert(kCtDwords <= 3 * kBlock, "three blob words per thread");
     const uint32_t last = P.cg.words - 1;
@@ -921,9 +949,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W == 4 ?
   }
   store_window(slot_dw, w0);
   if (kCompact)
-    decode_packet<kL4, kLayout, LTab, kKeys, W, O>(P, LTab{P.cg, base}, i0, i0 < P.n, c0.off, c0.cl, slot_dw, tid & 63);
+    decode_packet<kL4, kLayout, LTab, kKeys, W, O, AL>(P, LTab{P.cg, base}, i0, i0 < P.n, c0.off, c0.cl, slot_dw, tid & 63);
   else
-    decode_packet<kL4, kLayout, GTab, kKeys, W, O>(P, GTab{P.tab}, i0, i0 < P.n, c0.off, c0.cl, slot_dw, tid & 63);
+    decode_packet<kL4, kLayout, GTab, kKeys, W, O, AL>(P, GTab{P.tab}, i0, i0 < P.n, c0.off, c0.cl, slot_dw, tid & 63);
 }
 
 // Full decoded list of one packet (lists longer than the 16 inline codes).
@@ -944,17 +972,17 @@ namespace {
 // Launch one specialisation on `stream`, or (occ != nullptr) report how many of
 // its blocks fit a CU with this launch's LDS size instead.
 template <bool kL4, bool kLayout, bool kCompact, bool kKeys = false, int W = gpk::kWinChunks,
-          int O = GPK_WAVES_PER_EU>
+          int O = GPK_WAVES_PER_EU, int AL = 16>
 hipError_t launch(const gpk::KParams* P, hipStream_t stream, int* occ) {
   using namespace gpk;
   constexpr int slot_lds = kBlock * slot_dw_of<W>() * 4;
   // the table blob takes only the words this parser's tables use
   const int lds = kCompact ? slot_lds + (int)((P->cg.words + GPK_BLOB_ROUND - 1) & ~(GPK_BLOB_ROUND - 1u)) * 4 : slot_lds;
-  if (occ) return hipOccupancyMaxActiveBlocksPerMultiprocessor(occ, decode_kernel<kL4, kLayout, kCompact, kKeys, W, O>,
+  if (occ) return hipOccupancyMaxActiveBlocksPerMultiprocessor(occ, decode_kernel<kL4, kLayout, kCompact, kKeys, W, O, AL>,
                                                               kBlock, lds);
   const uint64_t grid = (P->n + kBlock - 1) / kBlock;
   if (grid > 0xffffffffull) return hipErrorInvalidValue;
-  hipLaunchKernelGGL((decode_kernel<kL4, kLayout, kCompact, kKeys, W, O>), dim3((unsigned)grid), dim3(kBlock), lds,
+  hipLaunchKernelGGL((decode_kernel<kL4, kLayout, kCompact, kKeys, W, O, AL>), dim3((unsigned)grid), dim3(kBlock), lds,
                      stream, *P);
   return hipGetLastError();
 }
@@ -962,16 +990,20 @@ hipError_t launch(const gpk::KParams* P, hipStream_t stream, int* occ) {
 // The specialisation a launch uses (gpk_launch_decode, gpk_launch_name).
 struct Sel {
   bool l4, layout, compact, keys;
-  int W, O;
+  int W, O, AL;
 };
 Sel select(const gpk::KParams* P, int with_l4, int with_layout) {
-  Sel s{with_l4 != 0, with_layout != 0, P->ctab != nullptr, P->key_kind != 0, gpk::kWinChunks, GPK_WAVES_PER_EU};
+  Sel s{with_l4 != 0, with_layout != 0, P->ctab != nullptr, P->key_kind != 0, gpk::kWinChunks, GPK_WAVES_PER_EU, 16};
   if (s.keys) {  // fused grouping keys: no layouts (gpk_decode_group_batch)
     s.layout = false;
   } else if (!s.l4 && !s.layout && P->small_headers) {
     s.W = 4;
   } else if (!s.layout && !P->big_packets) {
     s.O = GPK_SMALL_WAVES;
+    if (GPK_MID_W5 && P->mid_headers) {  // a dword-aligned 5-chunk window: 7 blocks per CU (LDS)
+      s.W = 5;
+      s.AL = 4;
+    }
   }
   return s;
 }
@@ -984,11 +1016,13 @@ hipError_t launch_sel(const gpk::KParams* P, const Sel& s, hipStream_t stream, i
   if (s.W == 4) return launch<false, false, kCompact, false, 4>(P, stream, occ);
   if (s.l4 && s.layout) return launch<true, true, kCompact>(P, stream, occ);
   if (s.l4)
-    return s.O != GPK_WAVES_PER_EU ? launch<true, false, kCompact, false, W, GPK_SMALL_WAVES>(P, stream, occ)
-                                   : launch<true, false, kCompact>(P, stream, occ);
+    return s.O == GPK_WAVES_PER_EU ? launch<true, false, kCompact>(P, stream, occ)
+           : s.AL == 4             ? launch<true, false, kCompact, false, 5, GPK_SMALL_WAVES, 4>(P, stream, occ)
+                                   : launch<true, false, kCompact, false, W, GPK_SMALL_WAVES>(P, stream, occ);
   if (s.layout) return launch<false, true, kCompact>(P, stream, occ);
-  return s.O != GPK_WAVES_PER_EU ? launch<false, false, kCompact, false, W, GPK_SMALL_WAVES>(P, stream, occ)
-                                 : launch<false, false, kCompact>(P, stream, occ);
+  return s.O == GPK_WAVES_PER_EU ? launch<false, false, kCompact>(P, stream, occ)
+         : s.AL == 4             ? launch<false, false, kCompact, false, 5, GPK_SMALL_WAVES, 4>(P, stream, occ)
+                                 : launch<false, false, kCompact, false, W, GPK_SMALL_WAVES>(P, stream, occ);
 }
 
 }  // namespace
@@ -1009,9 +1043,9 @@ extern "C" hipError_t gpk_launch_occupancy(const gpk::KParams* P, int with_l4, i
 // Name of the kernel specialisation gpk_launch_decode would launch.
 extern "C" int gpk_launch_describe(const gpk::KParams* P, int with_l4, int with_layout, char* buf, size_t cap) {
   const Sel s = select(P, with_l4, with_layout);
-  return snprintf(buf, cap, "gpk::decode_kernel<%s,%s,%s,%s,%d,%d>", s.l4 ? "true" : "false",
+  return snprintf(buf, cap, "gpk::decode_kernel<%s,%s,%s,%s,%d,%d,%d>", s.l4 ? "true" : "false",
                   s.layout ? "true" : "false", s.compact ? "true" : "false", s.keys ? "true" : "false", s.W,
-                  s.W == 4 ? 6 : s.O);
+                  s.W == 4 ? 6 : s.O, s.AL);
 }
 
 extern "C" hipError_t gpk_launch_list(const gpk::KParams* P, uint64_t index, int64_t* out, uint32_t cap,

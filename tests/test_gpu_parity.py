@@ -43,6 +43,11 @@ def test_fuzz(gpu_ctx, cfg_name, align):
     packets = pktutil.fuzz_packets(zlib.crc32(cfg_name.encode()) % 1000 + align, 40000)
     dev, ref = run_both(gpu_ctx, CONFIGS[cfg_name], packets, align=align, pad=align // 2)
     assert_same(dev, ref, cfg_name)
+    # the same packets through the kernels without layout output (the small-packet
+    # specialisations: dword-aligned 5-chunk window for parsers without IPv6, else 6 chunks)
+    data, off, cap = pktutil.pack(packets, align=align, pad=align // 2)
+    dev2 = gpu_ctx.decode_host(device_parser(CONFIGS[cfg_name]), data, off, cap, layouts=False)
+    assert_same(dev2, ref, cfg_name + " (no layouts)")
     err = dev["records"]["status"] & 0x7F
     if cfg_name != "first_unregistered":  # that one fails every packet with UnsupportedLayerType(LLC)
         assert len(np.unique(err)) > 5  # the fuzzer reaches many error sites
