@@ -50,6 +50,7 @@ struct KParams {
   const uint64_t* offsets;
   const uint32_t* caplens;
   uint64_t n;
+  uint64_t data_end;        // readable bytes of data: gpk_batch.data_bytes rounded up to 16 (0 = unknown)
   gpk_record* records;
   uint32_t* err_args;
   uint64_t* flows;

@@ -441,6 +441,7 @@ static int make_params(gpk_ctx* c, const gpk_parser* p, const gpk_batch* b, cons
   P.caplens = b->caplens;
   P.n = b->n;
   P.big_packets = b->n && b->data_bytes / b->n >= 1024;
+  P.data_end = (b->data_bytes + 15) & ~15ull;
   P.records = o ? o->records : nullptr;
   P.err_args = o ? o->err_args : nullptr;
   P.flows = o && (p->outputs & GPK_OUT_FLOWS) ? o->flows : nullptr;

@@ -294,6 +294,7 @@ __device__ __forceinline__ u32x4 bload(__amdgpu_buffer_rsrc_t rs, uint32_t voff,
 template <int W>
 struct WinT {
   uint4 v[W];
+  uint32_t x;  // AL = 4: the window's 4W+1-th dword (the slot's odd dword)
 };
 // LDS dwords per lane for a window of W chunks (odd: see kSlotDw)
 template <int W>
@@ -318,21 +319,36 @@ __device__ __forceinline__ Idx load_index(const KParams& P, uint64_t i) {
 
 // AL: the window's alignment. 16: the run of 16-byte-aligned chunks holding
 // the packet's first bytes (window = 16W - (off & 15) bytes, 16W - 15 at
-// worst); 4: W 16-byte loads from the packet's own dword, off & ~3 (a
-// dword-aligned global_load_dwordx4; window >= 16W - 3 bytes, so one chunk
-// fewer covers the same headers and the LDS slot shrinks by 16 bytes).
+// worst; the slot's odd dword is padding). 4: W 16-byte loads and one dword
+// from the packet's own dword, off & ~3 (dword-aligned global_load_dwordx4;
+// window = 16W + 4 - (off & 3) >= 16W + 1 bytes, so one chunk fewer covers
+// the same headers and the slot shrinks by 16 bytes). A dword-aligned
+// 16-byte load can reach into the 16-byte granule after the packet's last
+// byte; a lane whose loads would pass the batch's readable end
+// (P.data_end, from gpk_batch.data_bytes) takes the aligned run instead.
+struct WinGeo {
+  uint64_t wb;   // window base: batch offset of LDS slot byte 0 (off - m)
+  uint32_t m;    // packet byte 0 at slot byte m
+  uint32_t win;  // packet bytes in the window
+  uint32_t nch;  // 16-byte loads that hold window bytes (0: inactive lane)
+};
 template <int W, int AL>
-__device__ __forceinline__ uint32_t win_chunks(const Idx& x, bool active) {
-  const uint32_t m = (uint32_t)(x.off & (AL - 1));
-  uint32_t win = W * 16 - m;
-  if (x.cl < win) win = x.cl;
-  return active ? (m + win + 15) >> 4 : 0;
+__device__ __forceinline__ WinGeo win_geo(const KParams& P, const Idx& x, bool active) {
+  uint32_t m = (uint32_t)(x.off & (AL - 1)), cap = AL == 4 ? W * 16 + 4 : W * 16;
+  uint32_t win = x.cl < cap - m ? x.cl : cap - m;
+  if (AL == 4 && (x.off & ~3ull) + 16ull * ((m + win + 15) >> 4) > P.data_end) {
+    m = (uint32_t)(x.off & 15);
+    cap = W * 16;
+    win = x.cl < cap - m ? x.cl : cap - m;
+  }
+  return WinGeo{x.off - m, m, win, active ? (m + win + 15) >> 4 : 0u};
 }
 
 typedef u32x4 u32x4_a4 __attribute__((aligned(4)));
 template <int W, int AL>
-__device__ __forceinline__ void load_window(const KParams& P, const Idx& x, uint32_t nchunk, WinT<W>& w) {
-  const uint8_t* src = nchunk ? P.data + (x.off & ~(uint64_t)(AL - 1)) : reinterpret_cast<const uint8_t*>(P.tab);
+__device__ __forceinline__ void load_window(const KParams& P, const WinGeo& g, WinT<W>& w) {
+  const uint32_t nchunk = g.nch;
+  const uint8_t* src = nchunk ? P.data + g.wb : reinterpret_cast<const uint8_t*>(P.tab);
   const uint32_t last = nchunk ? nchunk - 1 : 0;
 #pragma unroll
   for (int k = 0; k < W; k++) {
@@ -344,9 +360,12 @@ __device__ __forceinline__ void load_window(const KParams& P, const Idx& x, uint
       w.v[k] = make_uint4(v.x, v.y, v.z, v.w);
     }
   }
+  // the odd dword: bytes [16W, 16W + 4) of the window when it reaches them,
+  // else a dword of the last chunk (valid memory, never used)
+  if (AL == 4) w.x = *reinterpret_cast<const uint32_t*>(src + (nchunk > W ? 16u * W : 16u * last));
 }
 
-template <int W>
+template <int W, int AL>
 __device__ __forceinline__ void store_window(uint32_t slot_dw, const WinT<W>& w) {
 #pragma unroll
   for (int k = 0; k < W; k++) {
@@ -355,6 +374,7 @@ __device__ __forceinline__ void store_window(uint32_t slot_dw, const WinT<W>& w)
     gpk_smem[slot_dw + 4 * k + 2] = w.v[k].z;
     gpk_smem[slot_dw + 4 * k + 3] = w.v[k].w;
   }
+  if (AL == 4) gpk_smem[slot_dw + 4 * W] = w.x;
 }
 
 // The grouping key of gpk_flows.hip's key_kernel, derived here from the parse
@@ -731,10 +751,8 @@ __device__ __forceinline__ uint32_t segment_sums(const KParams& P, Stream<D>& S,
 
 template <bool kL4, bool kLayout, class TT, bool kKeys, int W, int O, int AL>
 __device__ __forceinline__ void decode_packet(const KParams& P, const TT& T, uint64_t i, bool active, uint64_t off,
-                                              uint32_t cl, uint32_t slot_dw, uint32_t lane) {
-  const uint32_t m = (uint32_t)(off & (AL - 1));
-  uint32_t win = W * 16 - m;
-  if (cl < win) win = cl;
+                                              uint32_t cl, const WinGeo& g, uint32_t slot_dw, uint32_t lane) {
+  const uint32_t m = g.m, win = g.win;
   Rd r{P.data + off, slot_dw * 4 + m, win};
 
   // Phase B's stream over the wave's packets starts now when they are packed:
@@ -890,13 +908,14 @@ __device__ __forceinline__ void decode_packet(const KParams& P, const TT& T, uin
       else if (GPK_PB_LDS_HT && job && lane < 63 && nnch && (noff >> 4) == (je >> 4))
         tlds = (slot_dw + slot_dw_of<W>()) * 4;
     } else {
-      // the window holds batch bytes [off & ~3, +16 nch): a head/tail chunk
+      // the window holds batch bytes [wb, wb + m + win): a head/tail chunk
       // (16-byte aligned in the batch, dword-aligned in the slot) is taken
       // from it when the bytes before s / e that it contributes are there
-      const uint64_t wb = off & ~3ull;
+      const uint64_t wb = g.wb;
+      const uint32_t vb = m + win;
       const uint32_t hb = (uint32_t)((js & ~15ull) - wb), tb = (uint32_t)((je & ~15ull) - wb);
-      if (GPK_PB_LDS_HT && job && hb < 16 * nch && hb + (uint32_t)(js & 15) <= 16 * nch) hlds = slot_dw * 4 + hb;
-      if (GPK_PB_LDS_HT && job && tb < 16 * nch && tb + (uint32_t)(je & 15) <= 16 * nch) tlds = slot_dw * 4 + tb;
+      if (GPK_PB_LDS_HT && job && hb < vb && hb + (uint32_t)(js & 15) <= vb) hlds = slot_dw * 4 + hb;
+      if (GPK_PB_LDS_HT && job && tb < vb && tb + (uint32_t)(je & 15) <= vb) tlds = slot_dw * 4 + tb;
     }
     const uint32_t sum = segment_sums<D, E>(P, S, job, js, je, lane, hlds, tlds);
     if (job) {
@@ -934,9 +953,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W == 4 ?
   // flight together: two dependent memory round trips per packet.
   const uint64_t i0 = (uint64_t)blockIdx.x * kBlock + tid;
   const Idx c0 = load_index(P, i0);
-  const uint32_t n0 = win_chunks<W, AL>(c0, i0 < P.n);
+  const WinGeo g0 = win_geo<W, AL>(P, c0, i0 < P.n);
   WinT<W> w0;
-  load_window<W, AL>(P, c0, n0, w0);
+  load_window<W, AL>(P, g0, w0);
   if (kCompact) {  // the table blob (<= kCtDwords): clamped indices, duplicate writes of equal values
     static_assert(kCtDwords <= 3 * kBlock, "three blob words per thread");
     const uint32_t last = P.cg.words - 1;
@@ -947,11 +966,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W == 4 ?
     }
     __syncthreads();
   }
-  store_window(slot_dw, w0);
+  store_window<W, AL>(slot_dw, w0);
   if (kCompact)
-    decode_packet<kL4, kLayout, LTab, kKeys, W, O, AL>(P, LTab{P.cg, base}, i0, i0 < P.n, c0.off, c0.cl, slot_dw, tid & 63);
+    decode_packet<kL4, kLayout, LTab, kKeys, W, O, AL>(P, LTab{P.cg, base}, i0, i0 < P.n, c0.off, c0.cl, g0, slot_dw,
+                                                       tid & 63);
   else
-    decode_packet<kL4, kLayout, GTab, kKeys, W, O, AL>(P, GTab{P.tab}, i0, i0 < P.n, c0.off, c0.cl, slot_dw, tid & 63);
+    decode_packet<kL4, kLayout, GTab, kKeys, W, O, AL>(P, GTab{P.tab}, i0, i0 < P.n, c0.off, c0.cl, g0, slot_dw,
+                                                       tid & 63);
 }
 
 // Full decoded list of one packet (lists longer than the 16 inline codes).
@@ -1000,7 +1021,7 @@ Sel select(const gpk::KParams* P, int with_l4, int with_layout) {
     s.W = 4;
   } else if (!s.layout && !P->big_packets) {
     s.O = GPK_SMALL_WAVES;
-    if (GPK_MID_W5 && P->mid_headers) {  // a dword-aligned 5-chunk window: 7 blocks per CU (LDS)
+    if (GPK_MID_W5 && P->mid_headers && P->data_end) {  // a dword-aligned 5-chunk window: 7 blocks per CU (LDS)
       s.W = 5;
       s.AL = 4;
     }

@@ -247,9 +247,14 @@ int gpk_ctx_set_table_mode(gpk_ctx* ctx, int mode);
  * the first and the last byte of the packets of one group of 64 consecutive
  * packets (a wave), so data must be one allocation covering all packets.
  * data_bytes: the size of data in bytes (gpk_decode_batch_host copies that
- * many). gpk_decode_batch uses it only as a hint of the mean packet size
- * (data_bytes / n selects a kernel variant; 0 = unknown): pass the summed
- * capture lengths (or the packed buffer size) for best results. */
+ * many); 0 = unknown. gpk_decode_batch uses it as a hint of the mean packet
+ * size (data_bytes / n selects a kernel variant) and as the readable end of
+ * data for the small-packet kernel, which loads header words at dword rather
+ * than 16-byte alignment only below data + data_bytes rounded up to 16 (a
+ * packet whose header window would reach past it, and every packet when
+ * data_bytes is 0, uses 16-byte-aligned loads). Pass the packed buffer size
+ * (or at least the summed capture lengths) for best results; never more than
+ * the readable bytes of data. */
 typedef struct gpk_batch {
   const uint8_t* data;
   const uint64_t* offsets;
