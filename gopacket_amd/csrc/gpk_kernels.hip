@@ -577,9 +577,14 @@ __device__ __forceinline__ void stream_drain(Stream<D>& S) {
   for (int d = 0; d < D; d++) slot_wait<0>(S.ring[d].c);
 }
 
+// tafter: tlds holds the bytes of the granule of e from e on (the next
+// packet's first bytes, in the next lane's window; the bytes before e in that
+// chunk are not the granule's): the segment then takes P(ge) minus them
+// instead of P(ge - 1) plus the bytes before e.
 template <int D>
 __device__ __forceinline__ uint32_t dense_segment_sums(const KParams& P, Stream<D>& S, bool job, uint64_t s,
-                                                       uint64_t e, uint32_t lane, uint32_t hlds, uint32_t tlds) {
+                                                       uint64_t e, uint32_t lane, uint32_t hlds, uint32_t tlds,
+                                                       bool tafter) {
   static_assert(kGran == 1, "head/tail chunks from the LDS window need 16-byte granules");
   const uint64_t R0 = S.R0;
   const uint32_t R = S.R;
@@ -588,16 +593,17 @@ __device__ __forceinline__ uint32_t dense_segment_sums(const KParams& P, Stream<
   // head / tail chunks: from the LDS header windows when a window holds them
   // (hlds / tlds = LDS byte address, else ~0), else from memory
   uint32_t L = 0;
+  const bool ta = tafter && rel < R;  // the granule of e is streamed: P(ge) exists
   {
     u32x4 hc = lds_chunk(hlds), tc = lds_chunk(tlds);
     if (hlds == ~0u) hc = __builtin_amdgcn_raw_buffer_load_b128(rs, rsl & ~15u, 0, 0);
-    if (tlds == ~0u) tc = __builtin_amdgcn_raw_buffer_load_b128(rs, rel & ~15u, 0, 0);
-    L = chunk_l_below(tc, rel & 15u, 0u) - chunk_l_below(hc, rsl & 15u, 0u);
+    if (tlds == ~0u || (tafter && !ta)) tc = __builtin_amdgcn_raw_buffer_load_b128(rs, rel & ~15u, 0, 0);
+    L = chunk_l_below(tc, rel & 15u, 0u) - (ta ? chunk_l(tc, 0u) : 0u) - chunk_l_below(hc, rsl & 15u, 0u);
   }
   const uint32_t np = (R + kPassBytes - 1) / kPassBytes;  // wave-uniform
   const uint32_t vo = lane * kGranBytes;
   Gran (&ring)[D] = S.ring;
-  const int32_t a = (int32_t)(rsl / kGranBytes) - 1, b = (int32_t)(rel / kGranBytes) - 1;
+  const int32_t a = (int32_t)(rsl / kGranBytes) - 1, b = (int32_t)(rel / kGranBytes) - (ta ? 0 : 1);
   const int32_t pa = a >> 6, pb = b >> 6;  // -1 never matches
   const int32_t la = (a & 63) << 2, lb = (b & 63) << 2, ll = (int32_t)lane << 2;
   uint32_t xa = 0, xb = 0, c = 0;
@@ -724,7 +730,7 @@ __device__ __forceinline__ uint32_t sparse_segment_sums(const KParams& P, bool j
 // compact), else the per-segment stream.
 template <int D, int E>
 __device__ __forceinline__ uint32_t segment_sums(const KParams& P, Stream<D>& S, bool job, uint64_t s, uint64_t e,
-                                                 uint32_t lane, uint32_t hlds, uint32_t tlds) {
+                                                 uint32_t lane, uint32_t hlds, uint32_t tlds, bool tafter) {
   if (S.on) {
     if (!__ballot(job)) {  // nothing to sum: the early loads still land before their registers are reused
       stream_drain(S);
@@ -735,7 +741,7 @@ __device__ __forceinline__ uint32_t segment_sums(const KParams& P, Stream<D>& S,
     // needs between the early slots and the loop's after the data is in.
     stream_drain(S);
     stream_issue(P, S, S.R0, S.R, lane, E < D ? E : D, D);
-    return dense_segment_sums<D>(P, S, job, s, e, lane, hlds, tlds);
+    return dense_segment_sums<D>(P, S, job, s, e, lane, hlds, tlds, tafter);
   }
   // (with the early start on, a wave whose packets are not packed goes to
   // the per-segment stream: one call site keeps the slot registers in place)
@@ -743,7 +749,7 @@ __device__ __forceinline__ uint32_t segment_sums(const KParams& P, Stream<D>& S,
   uint32_t R;
   if (E == 0 && dense_region(job, s, e, R0, R)) {
     stream_issue(P, S, R0, R, lane, 0, D);
-    return dense_segment_sums<D>(P, S, job, s, e, lane, hlds, tlds);
+    return dense_segment_sums<D>(P, S, job, s, e, lane, hlds, tlds, tafter);
   }
   if (!__ballot(job)) return 0;
   return sparse_segment_sums(P, job, s, e, lane);
@@ -901,6 +907,7 @@ __device__ __forceinline__ void decode_packet(const KParams& P, const TT& T, uin
     const uint64_t noff = (uint64_t)noff_hi << 32 | noff_lo;
     const uint64_t c0 = off >> 4;
     uint32_t hlds = ~0u, tlds = ~0u;
+    bool tafter = false;
     if (AL == 16) {
       if (GPK_PB_LDS_HT && job && (js >> 4) - c0 < nch) hlds = slot_dw * 4 + 16 * (uint32_t)((js >> 4) - c0);
       if (GPK_PB_LDS_HT && job && (je >> 4) - c0 < nch)
@@ -915,9 +922,17 @@ __device__ __forceinline__ void decode_packet(const KParams& P, const TT& T, uin
       const uint32_t vb = m + win;
       const uint32_t hb = (uint32_t)((js & ~15ull) - wb), tb = (uint32_t)((je & ~15ull) - wb);
       if (GPK_PB_LDS_HT && job && hb < vb && hb + (uint32_t)(js & 15) <= vb) hlds = slot_dw * 4 + hb;
-      if (GPK_PB_LDS_HT && job && tb < vb && tb + (uint32_t)(je & 15) <= vb) tlds = slot_dw * 4 + tb;
+      const uint32_t nm = (uint32_t)__shfl_down((int)m, 1);
+      if (GPK_PB_LDS_HT && job && tb < vb && tb + (uint32_t)(je & 15) <= vb) {
+        tlds = slot_dw * 4 + tb;
+      } else if (GPK_PB_LDS_HT && job && lane < 63 && nnch && noff == je) {
+        // the next packet starts at e: its window (packet byte 0 at slot byte
+        // nm) holds the granule's bytes from e on, at a dword-aligned address
+        tlds = (slot_dw + slot_dw_of<W>()) * 4 + nm - (uint32_t)(je & 15);
+        tafter = true;
+      }
     }
-    const uint32_t sum = segment_sums<D, E>(P, S, job, js, je, lane, hlds, tlds);
+    const uint32_t sum = segment_sums<D, E>(P, S, job, js, je, lane, hlds, tlds, tafter);
     if (job) {
       l4c = fold(jinit + sum - jexist);
       const bool udp = (st & GPK_ST_L4_UDP) != 0;
