@@ -278,10 +278,17 @@ def full_parity(name, cfg, data, off, cap, rec, fl, err, n, threads, chunk=1 << 
 
 def host_cores():
     """(threads used, nproc, CPU share, CPU model). The GPU box gives a
-    process a share of the host (its affinity mask / OMP_NUM_THREADS, 16 cores
-    per GPU on the driver's boxes) while nproc counts the whole machine; the
+    process a share of the host (a cgroup CPU quota, cpu.max, and
+    OMP_NUM_THREADS: 16 cores per GPU on the driver's boxes, with every CPU of
+    the machine in the affinity mask) while nproc counts the whole machine; the
     parallel CPU baseline runs one thread per core of the share."""
     share = len(os.sched_getaffinity(0))
+    try:  # a cgroup v2 CPU quota ("quota period"): the box's share of a larger machine
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max" and int(p) > 0:
+            share = min(share, -(-int(q) // int(p)))
+    except (OSError, ValueError):
+        pass
     nproc = os.cpu_count() or share
     omp = os.environ.get("OMP_NUM_THREADS", "")
     threads = min(share, int(omp)) if omp.isdigit() and int(omp) > 0 else share

@@ -35,6 +35,7 @@
 #include <new>
 #include <string>
 #include <thread>
+#include <sched.h>
 #include <vector>
 
 #include "../../include/gpk_capture.h"
@@ -910,9 +911,53 @@ struct PktVec {  // growable, uninitialised arrays (malloc: gpk_capindex_free)
   }
 };
 
+// CPUs this process may actually run on at once: the affinity mask, a cgroup
+// CPU quota (v2 cpu.max, v1 cfs_quota_us / cfs_period_us) and OMP_NUM_THREADS
+// when set. A GPU box gives a process a quota of a few cores of a large
+// machine whose every CPU is in its mask: threads beyond the quota exhaust it
+// and are then all throttled until the next scheduler period.
+unsigned usable_cpus() {
+  unsigned n = std::thread::hardware_concurrency();
+  cpu_set_t set;
+  if (sched_getaffinity(0, sizeof(set), &set) == 0) {
+    const int c = CPU_COUNT(&set);
+    if (c > 0 && (unsigned)c < n) n = (unsigned)c;
+  }
+  auto quota = [](const char* qf, const char* pf) -> long {  // ceil(quota / period), 0 = none
+    long q = 0, p = 0;
+    if (FILE* f = fopen(qf, "r")) {
+      char buf[64] = {0};
+      if (fgets(buf, sizeof(buf), f)) {
+        if (!pf) {  // v2: "quota period" or "max period"
+          if (sscanf(buf, "%ld %ld", &q, &p) != 2) q = 0;
+        } else {
+          q = strtol(buf, nullptr, 10);
+        }
+      }
+      fclose(f);
+    }
+    if (pf) {
+      if (FILE* f = fopen(pf, "r")) {
+        if (fscanf(f, "%ld", &p) != 1) p = 0;
+        fclose(f);
+      }
+    }
+    return q > 0 && p > 0 ? (q + p - 1) / p : 0;
+  };
+  long c = quota("/sys/fs/cgroup/cpu.max", nullptr);
+  if (!c) c = quota("/sys/fs/cgroup/cpu/cpu.cfs_quota_us", "/sys/fs/cgroup/cpu/cpu.cfs_period_us");
+  if (c > 0 && (unsigned long)c < n) n = (unsigned)c;
+  if (const char* e = getenv("OMP_NUM_THREADS")) {
+    const long o = strtol(e, nullptr, 10);
+    if (o > 0 && (unsigned long)o < n) n = (unsigned)o;
+  }
+  return n ? n : 1;
+}
+
 // Persistent worker threads for the walk (one set per process, created on
-// first use): a staging slot is walked every few milliseconds, and spawning
-// dozens of threads per slot cost about as much as the walk itself.
+// first use, one per usable CPU): a staging slot is walked every few
+// milliseconds, and spawning dozens of threads per slot cost about as much as
+// the walk itself.
 class Pool {
  public:
   static Pool& get() {
@@ -946,7 +991,7 @@ class Pool {
 
  private:
   Pool() {
-    unsigned n = std::thread::hardware_concurrency();
+    unsigned n = usable_cpus();
     n = n < 2 ? 2 : (n > 64 ? 64 : n);
     for (unsigned k = 0; k + 1 < n; k++) th_.emplace_back([this] { loop(); });
   }
