@@ -502,10 +502,14 @@ def c5_replay(ctx, gib=10.0, reps=2, threads=16, cpu_threads=16):
     ok = (st["packets"] == n and st["error"] == "EOF" and len(idx) == len(sample)
           and np.array_equal(got, ref["records"]) and np.array_equal(gfl, ref["flows"]))
     w = st["wall_s"]
+    w0 = runs[0]["wall_s"]
     return dict(workload="C5: pcapng replay of the C4 IMIX mix, end to end incl. HtoD/DtoH",
                 packets=st["packets"], file_bytes=st["file_bytes"], value=round(st["packets"] / w / 1e6, 2),
                 unit="Mpkts/s", GBps=round(st["file_bytes"] / w / 1e9, 2), wall_s=round(w, 4),
                 runs_wall_s=[round(r["wall_s"], 4) for r in runs],
+                first_call=dict(value=round(st["packets"] / w0 / 1e6, 2), wall_s=round(w0, 4),
+                                note="includes allocating and pinning the staging buffers, which the context "
+                                     "keeps for later calls (the best run reuses them)"),
                 breakdown_s=dict(read=round(st["read_s"], 4), index=round(st["index_s"], 4),
                                  gpu_copy_decode=round(st["gpu_s"], 4), kernel=round(st["kernel_s"], 4),
                                  deliver=round(st["deliver_s"], 4)),

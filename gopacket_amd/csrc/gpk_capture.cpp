@@ -39,6 +39,7 @@
 #include <vector>
 
 #include "../../include/gpk_capture.h"
+#include "gpk_walk.h"
 
 namespace {
 
@@ -1118,6 +1119,29 @@ uint64_t state_version(const gpk_capreader* r) {  // anything plain_epb depends 
 }
 
 }  // namespace
+
+// The reader state the device walk needs (gpk_walk.h): the same inputs as
+// plain_epb, taken where the host walk would take its workers' snapshot.
+bool gpk_capreader_walk_state(const gpk_capreader* r, gpk::WalkState* out) {
+  if (!r || !out || r->format != GPK_CAP_PCAPNG || !r->opened || r->open_failed) return false;
+  const NgState& st = r->st;
+  if (st.ifaces.size() > (size_t)gpk::kWalkMaxIf) return false;
+  memset(out, 0, sizeof(*out));
+  out->be = st.be;
+  out->mixed = (r->flags & GPK_NG_WANT_MIXED_LINKTYPE) != 0;
+  out->nif = (uint32_t)st.ifaces.size();
+  for (size_t i = 0; i < st.ifaces.size(); i++) {
+    const Iface& it = st.ifaces[i];
+    gpk::WalkIface& w = out->ifc[i];
+    w.second_mask = it.second_mask;
+    w.scale_up = it.scale_up;
+    w.scale_down = it.scale_down;
+    w.tsoff = it.tsoff;
+    w.link_type = it.link_type;
+    w.plain = it.second_mask != 0 && (out->mixed || it.link_type == st.link_type);
+  }
+  return true;
+}
 
 extern "C" int gpk_capreader_index_all(gpk_capreader* r, const uint8_t* buf, uint64_t len, int eof, int threads,
                                        gpk_capindex* out, uint64_t* consumed) {

@@ -84,7 +84,30 @@ struct gpk_ctx {
   size_t dbuf_bytes = 0;
   hipStream_t stream = nullptr;
   std::mutex mu;
+  // gpk_replay_file's staging buffers, kept for the next call (gpk_walk.h)
+  void* replay_cache = nullptr;
+  void (*replay_cache_free)(void*) = nullptr;
 };
+
+void* gpk_ctx_replay_take(gpk_ctx* c) {
+  std::lock_guard<std::mutex> g(c->mu);
+  void* p = c->replay_cache;
+  c->replay_cache = nullptr;
+  return p;
+}
+
+void gpk_ctx_replay_put(gpk_ctx* c, void* p, void (*deleter)(void*)) {
+  void* old = nullptr;
+  void (*old_free)(void*) = nullptr;
+  {
+    std::lock_guard<std::mutex> g(c->mu);
+    old = c->replay_cache;
+    old_free = c->replay_cache_free;
+    c->replay_cache = p;
+    c->replay_cache_free = deleter;
+  }
+  if (old && old_free) old_free(old);
+}
 
 // Every table change takes a new process-wide id, so a context never mistakes
 // a new parser that reuses a freed parser's address for the one it uploaded.
@@ -242,6 +265,7 @@ int gpk_ctx_destroy(gpk_ctx* c) {
   if (c->stream) (void)hipStreamDestroy(c->stream);
   free_slots(c);
   if (c->dbuf) (void)hipFree(c->dbuf);
+  if (c->replay_cache && c->replay_cache_free) c->replay_cache_free(c->replay_cache);
   delete c;
   return GPK_OK;
 }

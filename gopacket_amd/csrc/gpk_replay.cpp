@@ -19,7 +19,12 @@
 //     and the CUs work on different slots at once;
 //   * the next slot is read while the current one is walked and the previous
 //     ones are on the device; the unfinished record at a slot's end is
-//     carried into the head of the next slot (a reserved carry region).
+//     carried into the head of the next slot (a reserved carry region);
+//   * the record walk itself runs on the device once the reader has read the
+//     section header and interfaces (gpk_walk.h): the slot goes to HBM first,
+//     a segmented walk indexes its plain Enhanced Packet Blocks in place, and
+//     the host's exact reader takes over only where a block is not plain, so
+//     the host CPUs are left to the file reads.
 // Results are delivered in packet order through the callback.
 #include <hip/hip_runtime.h>
 #include <fcntl.h>
@@ -38,6 +43,7 @@
 #include <vector>
 
 #include "../../include/gpk_capture.h"
+#include "gpk_walk.h"
 
 namespace {
 
@@ -97,8 +103,15 @@ struct Src {  // the capture byte stream: plain file (parallel pread) or gzip (z
 struct Slot {
   uint8_t* host = nullptr;  // [carry region | fresh bytes | 16 B slack], pinned
   uint8_t* dev = nullptr;
+  // device record walk (gpk_walk.h): per-segment results, and the slot's
+  // packet index on the device (offsets relative to dev)
+  gpk::WalkSegs d_seg{}, h_seg{};
+  uint64_t* d_off = nullptr;
+  uint32_t* d_cap = nullptr;
+  gpk_capture_info* d_ci = nullptr;
   hipStream_t stream = nullptr;
   hipEvent_t h2d = nullptr;  // the slot's HtoD finished: host buffer reusable
+  hipError_t h2d_err = hipSuccess;  // the read thread's HtoD of the fresh bytes (device walk)
   bool h2d_pending = false;
   std::future<uint64_t> fill;  // async read of the fresh bytes
   bool fill_pending = false;
@@ -145,6 +158,7 @@ struct Pipeline {
     if (hipEventElapsedTime(&ms, B.e0, B.done) == hipSuccess) st->gpu_s += ms * 1e-3;
     if (hipEventElapsedTime(&kms, B.k0, B.k1) == hipSuccess) st->kernel_s += kms * 1e-3;
     double t = now_s();
+    for (uint64_t i = 0; i < B.n; i++) st->packet_bytes += B.h_cap[i];
     if (cb) cb(user, B.first, B.n, B.h_rec, B.h_err, B.h_flow, B.h_ci, B.h_cap);
     st->deliver_s += now_s() - t;
     free_bats.push_back(b);
@@ -165,6 +179,11 @@ struct Pipeline {
       if (s.stream) (void)hipStreamSynchronize(s.stream);
       if (s.host) (void)hipHostFree(s.host);
       if (s.dev) (void)hipFree(s.dev);
+      for (void* p : {(void*)s.d_seg.sync, (void*)s.d_seg.end, (void*)s.d_seg.count, (void*)s.d_seg.base,
+                      (void*)s.d_off, (void*)s.d_cap, (void*)s.d_ci})
+        if (p) (void)hipFree(p);
+      for (void* p : {(void*)s.h_seg.sync, (void*)s.h_seg.end, (void*)s.h_seg.count, (void*)s.h_seg.base})
+        if (p) (void)hipHostFree(p);
       if (s.h2d) (void)hipEventDestroy(s.h2d);
       if (s.stream) (void)hipStreamDestroy(s.stream);
     }
@@ -179,6 +198,68 @@ struct Pipeline {
     }
   }
 };
+
+constexpr uint32_t kMaxSeg = 16384;  // device-walk segments per slot
+
+#define ALLOC_OK(call, what) \
+  do {                       \
+    if ((call) != hipSuccess) return std::string(what) + ": " + hipGetErrorString(hipGetLastError()); \
+  } while (0)
+
+std::string alloc_slot(Slot& s, uint64_t C, uint64_t R, bool dev_walk, uint64_t max_pk) {
+  ALLOC_OK(hipHostMalloc((void**)&s.host, C + R + 16, hipHostMallocDefault), "hipHostMalloc slot");
+  memset(s.host + C + R, 0, 16);
+  ALLOC_OK(hipMalloc((void**)&s.dev, C + R + 16), "hipMalloc slot");
+  ALLOC_OK(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking), "hipStreamCreate");
+  ALLOC_OK(hipEventCreateWithFlags(&s.h2d, hipEventDisableTiming), "hipEventCreate");
+  if (!dev_walk) return "";
+  ALLOC_OK(hipMalloc((void**)&s.d_seg.sync, kMaxSeg * 8), "hipMalloc walk");
+  ALLOC_OK(hipMalloc((void**)&s.d_seg.end, kMaxSeg * 8), "hipMalloc walk");
+  ALLOC_OK(hipMalloc((void**)&s.d_seg.count, kMaxSeg * 4), "hipMalloc walk");
+  ALLOC_OK(hipMalloc((void**)&s.d_seg.base, kMaxSeg * 8), "hipMalloc walk");
+  ALLOC_OK(hipHostMalloc((void**)&s.h_seg.sync, kMaxSeg * 8, 0), "hipHostMalloc walk");
+  ALLOC_OK(hipHostMalloc((void**)&s.h_seg.end, kMaxSeg * 8, 0), "hipHostMalloc walk");
+  ALLOC_OK(hipHostMalloc((void**)&s.h_seg.count, kMaxSeg * 4, 0), "hipHostMalloc walk");
+  ALLOC_OK(hipHostMalloc((void**)&s.h_seg.base, kMaxSeg * 8, 0), "hipHostMalloc walk");
+  ALLOC_OK(hipMalloc((void**)&s.d_off, max_pk * 8), "hipMalloc index");
+  ALLOC_OK(hipMalloc((void**)&s.d_cap, max_pk * 4), "hipMalloc index");
+  ALLOC_OK(hipMalloc((void**)&s.d_ci, max_pk * sizeof(gpk_capture_info)), "hipMalloc index");
+  return "";
+}
+
+std::string alloc_bat(Bat& B, uint64_t P) {
+  ALLOC_OK(hipHostMalloc((void**)&B.h_off, P * 8, 0), "hipHostMalloc");
+  ALLOC_OK(hipHostMalloc((void**)&B.h_cap, P * 4, 0), "hipHostMalloc");
+  ALLOC_OK(hipHostMalloc((void**)&B.h_ci, P * sizeof(gpk_capture_info), 0), "hipHostMalloc");
+  ALLOC_OK(hipHostMalloc((void**)&B.h_rec, P * sizeof(gpk_record), 0), "hipHostMalloc");
+  ALLOC_OK(hipHostMalloc((void**)&B.h_err, P * 8, 0), "hipHostMalloc");
+  ALLOC_OK(hipHostMalloc((void**)&B.h_flow, P * 24, 0), "hipHostMalloc");
+  ALLOC_OK(hipMalloc((void**)&B.d_off, P * 8), "hipMalloc");
+  ALLOC_OK(hipMalloc((void**)&B.d_cap, P * 4), "hipMalloc");
+  ALLOC_OK(hipMalloc((void**)&B.d_rec, P * sizeof(gpk_record)), "hipMalloc");
+  ALLOC_OK(hipMalloc((void**)&B.d_err, P * 8), "hipMalloc");
+  ALLOC_OK(hipMalloc((void**)&B.d_flow, P * 24), "hipMalloc");
+  ALLOC_OK(hipEventCreate(&B.e0), "hipEventCreate");
+  ALLOC_OK(hipEventCreate(&B.k0), "hipEventCreate");
+  ALLOC_OK(hipEventCreate(&B.k1), "hipEventCreate");
+  ALLOC_OK(hipEventCreate(&B.done), "hipEventCreate");
+  return "";
+}
+
+// The buffers of a finished call, left in the context for the next one.
+struct Cached {
+  uint64_t C, R, P;
+  bool dev_walk;
+  std::vector<Slot> slots;
+  std::vector<Bat> bats;
+};
+void free_cached(void* p) {
+  Cached* c = (Cached*)p;
+  Pipeline pl;  // its destructor frees what it holds
+  pl.slots = std::move(c->slots);
+  pl.bats = std::move(c->bats);
+  delete c;
+}
 
 }  // namespace
 
@@ -242,38 +323,54 @@ extern "C" int gpk_replay_file(gpk_ctx* ctx, const gpk_parser* parser, const cha
   }
 
   // ---- buffers ---------------------------------------------------------------
+  // (kept in the context between calls: the pinned staging slots are ~GBs and
+  // allocating them costs as much as replaying a 10 GB file)
   const uint64_t R = opt.slot_bytes, C = opt.slot_bytes;  // fresh bytes, carry region
   Pipeline pl;
   pl.cb = cb;
   pl.user = user;
   pl.st = stats;
   pl.P = opt.batch_pkts;
-  pl.slots.resize(opt.slots);
-  pl.bats.resize(2 * opt.slots);
-  bool good = true;
-  for (auto& s : pl.slots) {
-    good = good && pl.ok(hipHostMalloc((void**)&s.host, C + R + 16, hipHostMallocDefault), "hipHostMalloc slot") &&
-           pl.ok(hipMalloc((void**)&s.dev, C + R + 16), "hipMalloc slot") &&
-           pl.ok(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking), "hipStreamCreate") &&
-           pl.ok(hipEventCreateWithFlags(&s.h2d, hipEventDisableTiming), "hipEventCreate");
-    if (good) memset(s.host + C + R, 0, 16);
-  }
   const uint64_t P = pl.P;
-  for (size_t i = 0; good && i < pl.bats.size(); i++) {
-    Bat& B = pl.bats[i];
-    good = pl.ok(hipHostMalloc((void**)&B.h_off, P * 8, 0), "hipHostMalloc") &&
-           pl.ok(hipHostMalloc((void**)&B.h_cap, P * 4, 0), "hipHostMalloc") &&
-           pl.ok(hipHostMalloc((void**)&B.h_ci, P * sizeof(gpk_capture_info), 0), "hipHostMalloc") &&
-           pl.ok(hipHostMalloc((void**)&B.h_rec, P * sizeof(gpk_record), 0), "hipHostMalloc") &&
-           pl.ok(hipHostMalloc((void**)&B.h_err, P * 8, 0), "hipHostMalloc") &&
-           pl.ok(hipHostMalloc((void**)&B.h_flow, P * 24, 0), "hipHostMalloc") &&
-           pl.ok(hipMalloc((void**)&B.d_off, P * 8), "hipMalloc") && pl.ok(hipMalloc((void**)&B.d_cap, P * 4), "hipMalloc") &&
-           pl.ok(hipMalloc((void**)&B.d_rec, P * sizeof(gpk_record)), "hipMalloc") &&
-           pl.ok(hipMalloc((void**)&B.d_err, P * 8), "hipMalloc") && pl.ok(hipMalloc((void**)&B.d_flow, P * 24), "hipMalloc") &&
-           pl.ok(hipEventCreate(&B.e0), "hipEventCreate") && pl.ok(hipEventCreate(&B.k0), "hipEventCreate") &&
-           pl.ok(hipEventCreate(&B.k1), "hipEventCreate") && pl.ok(hipEventCreate(&B.done), "hipEventCreate");
-    pl.free_bats.push_back((int)i);
+  // device record walk buffers (pcapng only; GPK_REPLAY_HOST_WALK=1 keeps the walk on the host)
+  const char* hw = getenv("GPK_REPLAY_HOST_WALK");
+  const bool dev_walk = format == GPK_CAP_PCAPNG && !(hw && hw[0] == '1');
+  const uint64_t max_pk = (C + R) / 32 + 1;  // a block is at least 32 bytes
+  bool good = true;
+  Cached* cached = (Cached*)gpk_ctx_replay_take(ctx);
+  if (cached && cached->C == C && cached->R == R && cached->P == P && cached->dev_walk == dev_walk &&
+      cached->slots.size() == (size_t)opt.slots) {
+    pl.slots = std::move(cached->slots);
+    pl.bats = std::move(cached->bats);
+    delete cached;
+    for (auto& s : pl.slots) s.fill_pending = s.h2d_pending = false;
+  } else {
+    if (cached) free_cached(cached);
+    pl.slots.resize(opt.slots);
+    pl.bats.resize(2 * opt.slots);
+    // every slot and batch allocated on its own thread (pinning GBs is the slow part)
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    std::vector<std::future<std::string>> jobs;
+    for (auto& s : pl.slots)
+      jobs.push_back(std::async(std::launch::async, [&, dev, sp = &s] {
+        (void)hipSetDevice(dev);
+        return alloc_slot(*sp, C, R, dev_walk, max_pk);
+      }));
+    for (auto& b : pl.bats)
+      jobs.push_back(std::async(std::launch::async, [&, dev, bp = &b] {
+        (void)hipSetDevice(dev);
+        return alloc_bat(*bp, P);
+      }));
+    for (auto& jb : jobs) {
+      const std::string e = jb.get();
+      if (!e.empty()) {
+        good = false;
+        if (pl.herr.empty()) pl.herr = e;
+      }
+    }
   }
+  for (size_t i = 0; i < pl.bats.size(); i++) pl.free_bats.push_back((int)i);
   if (!good) {
     gpk_capreader_destroy(rd);
     if (src.gz) gzclose(src.gz);
@@ -282,16 +379,30 @@ extern "C" int gpk_replay_file(gpk_ctx* ctx, const gpk_parser* parser, const cha
     return GPK_ENOMEM;
   }
 
+  // With the device walk the device copy of a slot mirrors its host layout
+  // ([carry region | fresh bytes]), so the fresh bytes go to HBM from the
+  // read thread as soon as they are read (on the slot's stream, after
+  // everything earlier that reads the slot), overlapping the previous slot's
+  // walk and decode; only the short carry is copied later.
+  int dev = 0;
+  (void)hipGetDevice(&dev);
   auto start_fill = [&](Slot& s) {
-    s.fill = std::async(std::launch::async, [&src, &s, C, R, stats] {
+    s.h2d_err = hipSuccess;
+    s.fill = std::async(std::launch::async, [&src, &s, C, R, stats, dev, dev_walk] {
       double t = now_s();
       uint64_t k = src.read(s.host + C, R);
       stats->read_s += now_s() - t;
+      if (dev_walk && k) {
+        (void)hipSetDevice(dev);
+        s.h2d_err = hipMemcpyAsync(s.dev + C, s.host + C, k, hipMemcpyHostToDevice, s.stream);
+      }
       return k;
     });
     s.fill_pending = true;
   };
 
+  const double t_loop = now_s();
+  const char* trace = getenv("GPK_REPLAY_TRACE");
   // ---- the loop --------------------------------------------------------------
   const uint8_t* carry = nullptr;
   uint64_t carry_len = 0, packet_index = 0;
@@ -321,32 +432,102 @@ extern "C" int gpk_replay_file(gpk_ctx* ctx, const gpk_parser* parser, const cha
       }
       if (good) start_fill(N);
     }
-    // walk the records of [start, start+len) (parallel, gpk_capreader_index_all)
-    gpk_capindex xi;
-    uint64_t used = 0;
+    // walk the records of [start, start+len): on the device once the reader
+    // is open (gpk_walk.h), the rest (and everything before) on the host
+    // (parallel, gpk_capreader_index_all)
+    gpk_capindex xi{};
+    uint64_t used = 0, G = 0;  // G: packets indexed on the device (the slot's first G)
     double t_ix = now_s();
     // the walk is a dependent load per record: more chains than cores hide DRAM latency
     const int walk_threads = std::min(64, 4 * opt.read_threads);
-    int st = gpk_capreader_index_all(rd, S.host + start, len, eof ? 1 : 0, walk_threads, &xi, &used);
+    gpk::WalkState ws;
+    const bool dwalk = dev_walk;  // device index (S.d_*), slot layout mirrored on the device
+    const bool on_dev = dev_walk && gpk_capreader_walk_state(rd, &ws);  // ... and the walk runs there
+    // positions relative to the 16-byte-aligned base the kernels get
+    const uint64_t base_off = start & ~15ull, p0 = start & 15, L = p0 + len;
+    int st = GPK_CAP_MORE;
+    if (dwalk) {
+      // the carry next to the fresh bytes the read thread has sent
+      good = pl.ok(S.h2d_err, "HtoD slot");
+      if (good && carry_len)
+        good = pl.ok(hipMemcpyAsync(S.dev + start, S.host + start, carry_len, hipMemcpyHostToDevice, S.stream),
+                     "HtoD carry");
+      good = good && pl.ok(hipEventRecord(S.h2d, S.stream), "hipEventRecord");
+      S.h2d_pending = true;
+      uint64_t pos = p0;
+      if (good && on_dev) {
+        const uint64_t seg = std::max<uint64_t>(4096, ((L + kMaxSeg - 1) / kMaxSeg + 3) & ~3ull);
+        const uint32_t nseg = (uint32_t)((L + seg - 1) / seg);
+        good = pl.ok(gpk_walk_segments(S.dev + base_off, p0, L, seg, nseg, ws, S.d_seg, S.stream), "walk kernel") &&
+               pl.ok(hipMemcpyAsync(S.h_seg.sync, S.d_seg.sync, nseg * 8ull, hipMemcpyDeviceToHost, S.stream),
+                     "DtoH walk") &&
+               pl.ok(hipMemcpyAsync(S.h_seg.end, S.d_seg.end, nseg * 8ull, hipMemcpyDeviceToHost, S.stream), "DtoH walk") &&
+               pl.ok(hipMemcpyAsync(S.h_seg.count, S.d_seg.count, nseg * 4ull, hipMemcpyDeviceToHost, S.stream),
+                     "DtoH walk") &&
+               pl.ok(hipStreamSynchronize(S.stream), "hipStreamSynchronize");
+        // accept segments while each starts where the previous one's chain
+        // ended (segment 0 starts where the reader stands); stop after a
+        // chain that ended inside its segment (a block that is not plain)
+        bool go = good;
+        for (uint32_t k = 0; k < nseg; k++) {
+          const uint64_t s1 = std::min<uint64_t>(L, (uint64_t)(k + 1) * seg);
+          if (go && S.h_seg.sync[k] == pos) {
+            S.h_seg.base[k] = G;
+            G += S.h_seg.count[k];
+            pos = S.h_seg.end[k];
+            go = pos >= s1;
+          } else {
+            S.h_seg.base[k] = ~0ull;
+            go = false;
+          }
+        }
+        if (good && G)
+          good = pl.ok(hipMemcpyAsync(S.d_seg.base, S.h_seg.base, nseg * 8ull, hipMemcpyHostToDevice, S.stream),
+                       "HtoD walk") &&
+                 pl.ok(gpk_walk_emit(S.dev + base_off, L, nseg, ws, S.d_seg, S.d_off, S.d_cap, S.d_ci, S.stream),
+                       "emit kernel");
+      }
+      if (good) {
+        // the exact reader from the first block the device walk did not take
+        st = gpk_capreader_index_all(rd, S.host + base_off + pos, L - pos, eof ? 1 : 0, walk_threads, &xi, &used);
+        used += pos - p0;
+        if (st >= 0 && xi.n) {
+          for (uint64_t i = 0; i < xi.n; i++) xi.offsets[i] += pos;
+          good = pl.ok(hipMemcpyAsync(S.d_off + G, xi.offsets, xi.n * 8, hipMemcpyHostToDevice, S.stream), "HtoD index") &&
+                 pl.ok(hipMemcpyAsync(S.d_cap + G, xi.caplens, xi.n * 4, hipMemcpyHostToDevice, S.stream), "HtoD index") &&
+                 pl.ok(hipMemcpyAsync(S.d_ci + G, xi.ci, xi.n * sizeof(gpk_capture_info), hipMemcpyHostToDevice,
+                                      S.stream), "HtoD index") &&
+                 pl.ok(hipStreamSynchronize(S.stream), "hipStreamSynchronize");  // xi is freed below
+        }
+      }
+    } else {
+      st = gpk_capreader_index_all(rd, S.host + start, len, eof ? 1 : 0, walk_threads, &xi, &used);
+    }
     stats->index_s += now_s() - t_ix;
     if (st < 0) {
       rc = st;
       finished = true;
       break;
     }
-    const uint64_t pos = start + used;
-    bool copied = false;
-    for (uint64_t first = 0; first < xi.n && good;) {  // batches of up to P packets
-      const uint64_t n = std::min<uint64_t>(P, xi.n - first);
+    if (!good) {
+      gpk_capindex_free(&xi);
+      break;
+    }
+    const uint64_t pos = start + used, total = G + xi.n;
+    bool copied = dwalk;
+    for (uint64_t first = 0; first < total && good;) {  // batches of up to P packets
+      const uint64_t n = std::min<uint64_t>(P, total - first);
       const int b = pl.acquire();
       if (b < 0) {
         good = false;
         break;
       }
       Bat& B = pl.bats[b];
-      memcpy(B.h_off, xi.offsets + first, n * 8);  // relative to the slot's device copy (start)
-      memcpy(B.h_cap, xi.caplens + first, n * 4);
-      memcpy(B.h_ci, xi.ci + first, n * sizeof(gpk_capture_info));
+      if (!dwalk) {
+        memcpy(B.h_off, xi.offsets + first, n * 8);  // relative to the slot's device copy (start)
+        memcpy(B.h_cap, xi.caplens + first, n * 4);
+        memcpy(B.h_ci, xi.ci + first, n * sizeof(gpk_capture_info));
+      }
       if (!copied) {  // the whole slot, once, before its first kernel
         good = pl.ok(hipMemcpyAsync(S.dev, S.host + start, len + 16, hipMemcpyHostToDevice, S.stream), "HtoD slot") &&
                pl.ok(hipEventRecord(S.h2d, S.stream), "hipEventRecord");
@@ -355,17 +536,22 @@ extern "C" int gpk_replay_file(gpk_ctx* ctx, const gpk_parser* parser, const cha
       }
       B.first = packet_index;
       B.n = n;
-      good = good && pl.ok(hipEventRecord(B.e0, S.stream), "hipEventRecord") &&
-             pl.ok(hipMemcpyAsync(B.d_off, B.h_off, n * 8, hipMemcpyHostToDevice, S.stream), "HtoD offsets") &&
-             pl.ok(hipMemcpyAsync(B.d_cap, B.h_cap, n * 4, hipMemcpyHostToDevice, S.stream), "HtoD caplens") &&
-             pl.ok(hipMemsetAsync(B.d_err, 0, n * 8, S.stream), "hipMemsetAsync") &&
+      good = good && pl.ok(hipEventRecord(B.e0, S.stream), "hipEventRecord");
+      if (!dwalk)
+        good = good &&
+               pl.ok(hipMemcpyAsync(B.d_off, B.h_off, n * 8, hipMemcpyHostToDevice, S.stream), "HtoD offsets") &&
+               pl.ok(hipMemcpyAsync(B.d_cap, B.h_cap, n * 4, hipMemcpyHostToDevice, S.stream), "HtoD caplens");
+      good = good && pl.ok(hipMemsetAsync(B.d_err, 0, n * 8, S.stream), "hipMemsetAsync") &&
              pl.ok(hipEventRecord(B.k0, S.stream), "hipEventRecord");
       if (!good) {
         pl.free_bats.push_back(b);
         break;
       }
-      // data_bytes: the batch's span in the slot as the mean-packet-size hint (gpk.h)
-      gpk_batch db{S.dev, B.d_off, B.d_cap, n, n ? B.h_off[n - 1] + B.h_cap[n - 1] - B.h_off[0] : 0};
+      // data_bytes: the batch's span in the slot as the mean-packet-size hint;
+      // with the device index, the slot's bytes (gpk.h)
+      gpk_batch db{dwalk ? S.dev + base_off : S.dev, dwalk ? S.d_off + first : B.d_off,
+                   dwalk ? S.d_cap + first : B.d_cap, n,
+                   dwalk ? L : (n ? B.h_off[n - 1] + B.h_cap[n - 1] - B.h_off[0] : 0)};
       gpk_results dr{B.d_rec, B.d_err, B.d_flow, nullptr};
       int drc = gpk_decode_batch(ctx, parser, &db, &dr, S.stream);
       if (drc) {
@@ -378,12 +564,16 @@ extern "C" int gpk_replay_file(gpk_ctx* ctx, const gpk_parser* parser, const cha
       good = pl.ok(hipEventRecord(B.k1, S.stream), "hipEventRecord") &&
              pl.ok(hipMemcpyAsync(B.h_rec, B.d_rec, n * sizeof(gpk_record), hipMemcpyDeviceToHost, S.stream), "DtoH") &&
              pl.ok(hipMemcpyAsync(B.h_err, B.d_err, n * 8, hipMemcpyDeviceToHost, S.stream), "DtoH") &&
-             pl.ok(hipMemcpyAsync(B.h_flow, B.d_flow, n * 24, hipMemcpyDeviceToHost, S.stream), "DtoH") &&
-             pl.ok(hipEventRecord(B.done, S.stream), "hipEventRecord");
+             pl.ok(hipMemcpyAsync(B.h_flow, B.d_flow, n * 24, hipMemcpyDeviceToHost, S.stream), "DtoH");
+      if (dwalk)
+        good = good &&
+               pl.ok(hipMemcpyAsync(B.h_cap, S.d_cap + first, n * 4, hipMemcpyDeviceToHost, S.stream), "DtoH caplens") &&
+               pl.ok(hipMemcpyAsync(B.h_ci, S.d_ci + first, n * sizeof(gpk_capture_info), hipMemcpyDeviceToHost,
+                                    S.stream), "DtoH capture info");
+      good = good && pl.ok(hipEventRecord(B.done, S.stream), "hipEventRecord");
       pl.inflight.push_back(b);
       packet_index += n;
       stats->batches++;
-      for (uint64_t i = 0; i < n; i++) stats->packet_bytes += B.h_cap[i];
       first += n;
     }
     gpk_capindex_free(&xi);
@@ -410,6 +600,9 @@ extern "C" int gpk_replay_file(gpk_ctx* ctx, const gpk_parser* parser, const cha
     }
   stats->packets = packet_index;
   stats->wall_s = now_s() - t_start;
+  if (trace && trace[0] == '1')
+    fprintf(stderr, "gpk_replay: setup %.4f s, loop %.4f s, %llu slots\n", t_loop - t_start, now_s() - t_loop,
+            (unsigned long long)stats->slots);
   gpk_capreader_destroy(rd);
   if (src.gz) gzclose(src.gz);
   close(src.fd);
@@ -417,5 +610,8 @@ extern "C" int gpk_replay_file(gpk_ctx* ctx, const gpk_parser* parser, const cha
     snprintf(stats->error, sizeof(stats->error), "%s", pl.herr.c_str());
     return rc ? rc : GPK_EHIP;
   }
+  for (auto& s : pl.slots) good = good && pl.ok(hipStreamSynchronize(s.stream), "hipStreamSynchronize");
+  if (good)  // idle buffers for the next call
+    gpk_ctx_replay_put(ctx, new Cached{C, R, P, dev_walk, std::move(pl.slots), std::move(pl.bats)}, free_cached);
   return rc;
 }

@@ -85,3 +85,48 @@ def test_replay_mixed_blocks(gpu_ctx, tmp_path):
     path.write_bytes(raw)
     st = check(gpu_ctx, str(path), raw, slot_bytes=4096, slots=2, batch_pkts=3)
     assert st["error"] == "EOF"
+
+
+def walk_capture(bo="<"):
+    """Plain EPBs over three interfaces with different timestamp resolutions
+    (if_tsresol 6, 9 and 2^-10), payloads that hold fake EPB chains at 4-byte
+    aligned positions, and a few blocks the device walk must leave to the host
+    (an EPB with options, a name record, an interface statistics block)."""
+    import struct
+    rng = np.random.default_rng(5)
+    fake = b"".join(pcapgen.epb(bytes(rng.integers(0, 256, 40, dtype=np.uint8)), bo=bo) for _ in range(5))
+    raw = pcapgen.shb(bo) + pcapgen.idb(1, 0, bo) + pcapgen.idb(1, 0, bo, pcapgen.opt(9, b"\x09", bo) + pcapgen.end_opt(bo)) \
+        + pcapgen.idb(1, 0, bo, pcapgen.opt(9, b"\x8a", bo) + pcapgen.end_opt(bo))
+    from gopacket_amd import synth
+    blocks = []
+    for i in range(12000):
+        p = synth.packet(4, i)
+        if i % 97 == 5:
+            p = p[:14] + fake + p[14:]  # a plausible block chain inside the packet bytes
+        ts = int(rng.integers(0, 1 << 62))
+        if i == 4000:
+            blocks.append(pcapgen.epb(p, iface=i % 3, ts=ts, bo=bo, options=pcapgen.opt(1, b"note", bo) + pcapgen.end_opt(bo)))
+        elif i == 7000:
+            blocks.append(pcapgen.nrb([(1, b"\x0a\x00\x00\x01x\x00")], bo=bo))
+        elif i == 9000:
+            blocks.append(pcapgen.isb(1, ts, bo=bo))
+        else:
+            blocks.append(pcapgen.epb(p, iface=i % 3, ts=ts, length=len(p) + (i % 5), bo=bo))
+    return raw + b"".join(blocks)
+
+
+@pytest.mark.parametrize("bo", ["<", ">"])
+def test_replay_device_walk(gpu_ctx, tmp_path, bo):
+    """The device record walk (gpk_walk.hip) against the reader oracle, and the
+    same file with the walk kept on the host (GPK_REPLAY_HOST_WALK=1)."""
+    raw = walk_capture(bo)
+    path = tmp_path / "walk.pcapng"
+    path.write_bytes(raw)
+    for slot in (1 << 16, 1 << 20):
+        st = check(gpu_ctx, str(path), raw, slot_bytes=slot, slots=3, batch_pkts=5000)
+        assert st["error"] == "EOF"
+    os.environ["GPK_REPLAY_HOST_WALK"] = "1"
+    try:
+        check(gpu_ctx, str(path), raw, slot_bytes=1 << 16, slots=3, batch_pkts=5000)
+    finally:
+        del os.environ["GPK_REPLAY_HOST_WALK"]
