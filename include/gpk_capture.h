@@ -156,7 +156,7 @@ typedef struct gpk_replay_stats {
   uint64_t packets, packet_bytes, file_bytes, stream_bytes, batches, slots;
   double wall_s;         /* open .. last result delivered                        */
   double read_s;         /* file -> pinned staging (read threads, busy time)     */
-  double index_s;        /* record walk (gpk_capreader_index)                    */
+  double index_s;        /* record walk: device walk + host reader, and the waits for them */
   double gpu_s;          /* HtoD + decode + DtoH, summed over batches            */
   double kernel_s;       /* decode kernels alone                                 */
   double deliver_s;      /* result callback                                      */
@@ -170,6 +170,12 @@ typedef void (*gpk_replay_cb)(void* user, uint64_t first_packet, uint64_t n, con
                               const uint32_t* err_args, const uint64_t* flows, const gpk_capture_info* ci,
                               const uint32_t* caplens);
 
+/* Replay a whole capture file through HBM. For pcapng the record walk runs
+ * on the device once the section header and interfaces are read (plain
+ * Enhanced Packet Blocks; the host reader takes every other block, same
+ * results either way; GPK_REPLAY_HOST_WALK=1 in the environment keeps it on
+ * the host). The pinned staging slots and device buffers stay with ctx for
+ * the next call with the same sizes (gpk_ctx_destroy frees them). */
 int gpk_replay_file(gpk_ctx* ctx, const gpk_parser* p, const char* path, const gpk_replay_opts* opts,
                     gpk_replay_cb cb, void* user, gpk_replay_stats* stats);
 
