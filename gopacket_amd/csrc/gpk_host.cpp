@@ -69,10 +69,12 @@ struct TabSlot {
   gpk::CompactGeom cg{};
   uint64_t version = 0;       // parser table version held, 0 = empty
   uint64_t last_use = 0;      // LRU tick
-  std::vector<std::pair<hipStream_t, hipEvent_t>> uses;  // last launch reading this copy, per stream
+  // completes after every launch that read this copy so far: recorded on the
+  // context's own stream, which waits for each launch's stream (note_launch),
+  // so it never refers to a caller's stream that may be destroyed meanwhile
+  hipEvent_t done = nullptr;
 };
 constexpr int kTabSlots = 8;
-constexpr size_t kMaxStreamsPerSlot = 16;
 
 struct gpk_ctx {
   int device = 0;
@@ -233,8 +235,8 @@ int gpk_parser_set_udp_port(gpk_parser* p, uint32_t v, int32_t lt) {
 // ---- context -----------------------------------------------------------------
 static void free_slots(gpk_ctx* c) {
   for (TabSlot& t : c->slots) {
-    for (auto& u : t.uses) (void)hipEventDestroy(u.second);
-    t.uses.clear();
+    if (t.done) (void)hipEventDestroy(t.done);
+    t.done = nullptr;
     if (t.dtab) (void)hipFree(t.dtab);
     if (t.dctab) (void)hipFree(t.dctab);
     t.dtab = nullptr;
@@ -379,11 +381,7 @@ static uint32_t fast_flags(const gpk_parser* p) {
 
 // Wait until no launch reads slot t any more (it is about to be rewritten).
 static int drain_slot(TabSlot& t) {
-  for (auto& u : t.uses) {
-    HIPCHK(hipEventSynchronize(u.second));
-    (void)hipEventDestroy(u.second);
-  }
-  t.uses.clear();
+  if (t.done) HIPCHK(hipEventSynchronize(t.done));
   return GPK_OK;
 }
 
@@ -433,21 +431,22 @@ static int upload(gpk_ctx* c, const gpk_parser* p, gpk::KParams& P, int* slot) {
 }
 
 // A launch on stream s reads slot k: record that, so the slot is rewritten
-// only after it completes.
+// only after it completes. The context's stream waits for s at this point
+// (a transient event, released at once) and the slot's event is recorded
+// after that wait: it completes once every launch so far that read the slot
+// has, whatever happens to s afterwards.
 static int note_launch(gpk_ctx* c, int k, hipStream_t s) {
   TabSlot& t = c->slots[k];
-  hipEvent_t ev = nullptr;
-  for (auto& u : t.uses)
-    if (u.first == s) ev = u.second;
-  if (!ev) {
-    if (t.uses.size() >= kMaxStreamsPerSlot) {
-      int rc = drain_slot(t);
-      if (rc) return rc;
-    }
+  if (s != c->stream) {
+    hipEvent_t ev = nullptr;
     HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-    t.uses.emplace_back(s, ev);
+    hipError_t e = hipEventRecord(ev, s);
+    if (e == hipSuccess) e = hipStreamWaitEvent(c->stream, ev, 0);
+    (void)hipEventDestroy(ev);
+    HIPCHK(e);
   }
-  HIPCHK(hipEventRecord(ev, s));
+  if (!t.done) HIPCHK(hipEventCreateWithFlags(&t.done, hipEventDisableTiming));
+  HIPCHK(hipEventRecord(t.done, c->stream));
   return GPK_OK;
 }
 
