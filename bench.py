@@ -147,6 +147,15 @@ def run_config(name, n, steps, warmup, rank, world, ctx, check_sample=2048, prob
 
     for _ in range(warmup):
         step()
+    # and at least ~50 ms of launches: a short kernel (C1: 0.3 ms) right after
+    # its batch was generated runs ~20 % slower for its first ~10 ms of launches
+    # (clock ramp), which 3 steps do not cover (tools/c1_diag.py)
+    torch.cuda.synchronize()
+    tw = time.perf_counter()
+    while time.perf_counter() - tw < 0.05:
+        for _ in range(4):
+            step()
+        torch.cuda.synchronize()
     barrier(world)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
