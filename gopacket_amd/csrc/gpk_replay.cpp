@@ -199,7 +199,7 @@ struct Pipeline {
   }
 };
 
-constexpr uint32_t kMaxSeg = 16384;  // device-walk segments per slot
+constexpr uint32_t kMaxSeg = 65536;  // device-walk segments per slot (>= 4 KiB each)
 
 #define ALLOC_OK(call, what) \
   do {                       \

@@ -1,7 +1,7 @@
 // gpk_walk.hip — the pcapng record walk of a staging slot, on the device
 // (gpk_walk.h has the scheme). One thread per segment: the walk is a chain of
 // dependent 32-byte header reads, so the parallelism is across segments, and
-// a slot of 256 MiB in 16 KiB segments is 16 Ki independent chains.
+// a slot of 256 MiB in 4 KiB segments is 64 Ki independent chains.
 #include "gpk_walk.h"
 
 namespace gpk {
