@@ -52,7 +52,7 @@ EXPORTS = (
     "gpk_parser_create", "gpk_parser_destroy", "gpk_parser_add_decoder", "gpk_parser_set_options",
     "gpk_parser_set_outputs", "gpk_parser_decoder_for", "gpk_parser_set_ethertype",
     "gpk_parser_set_ipprotocol", "gpk_parser_set_tcp_port", "gpk_parser_set_udp_port", "gpk_ctx_create",
-    "gpk_ctx_destroy", "gpk_ctx_set_table_mode", "gpk_decode_batch", "gpk_decode_kernel_name", "gpk_decode_occupancy", "gpk_decode_batch_host",
+    "gpk_ctx_destroy", "gpk_ctx_set_table_mode", "gpk_decode_batch", "gpk_decode_kernel_name", "gpk_decode_occupancy", "gpk_diag_set_buffer", "gpk_decode_batch_host",
     "gpk_decoded_list",
     "gpk_decoded_list_host", "gpk_host_alloc", "gpk_host_free", "gpk_format_error", "gpk_layer_type_name", "gpk_code_layer_type", "gpk_strerror",
     "gpk_last_hip_error", "gpk_abi_version",
@@ -212,6 +212,7 @@ def lib():
         "gpk_decode_batch_host": ([vp, vp, P(Batch), P(Results)], c_int),
         "gpk_decode_kernel_name": ([vp, vp, P(Batch), c_int, ctypes.c_char_p, ctypes.c_size_t], c_int),
         "gpk_decode_occupancy": ([vp, vp, P(Batch), c_int, P(c_int)], c_int),
+        "gpk_diag_set_buffer": ([vp], c_int),
         "gpk_decoded_list": ([vp, vp, P(Batch), u64, P(i64), u32, P(u32)], c_int),
         "gpk_decoded_list_host": ([vp, vp, ctypes.c_char_p, u32, P(i64), u32, P(u32)], c_int),
         "gpk_host_alloc": ([P(vp), ctypes.c_size_t], c_int),

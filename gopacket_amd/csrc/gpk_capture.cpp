@@ -965,9 +965,13 @@ class Pool {
     static Pool p;
     return p;
   }
-  // f(0) .. f(n-1) on the pool's threads and the caller's; returns when all are done
+  // f(0) .. f(n-1) on the pool's threads and the caller's; returns when all are done.
+  // The pool is process-wide and holds one job at a time: callers on other
+  // threads (two replays, two readers, ctypes calls that release the GIL)
+  // queue here until the running job has finished; f must not call run().
   void run(int n, const std::function<void(int)>& f) {
     if (n <= 0) return;
+    std::lock_guard<std::mutex> one_job(run_mu_);
     std::unique_lock<std::mutex> lk(mu_);
     job_ = &f;
     next_ = 0;
@@ -1021,6 +1025,7 @@ class Pool {
     }
   }
   std::vector<std::thread> th_;
+  std::mutex run_mu_;  // held for a whole job
   std::mutex mu_;
   std::condition_variable cv_, done_;
   const std::function<void(int)>* job_ = nullptr;

@@ -72,6 +72,7 @@ struct KParams {
   uint32_t* keys;
   uint64_t* khash;
   int32_t* kcode;
+  uint64_t* diag;           // GPK_DIAG_TIMES builds only: 8 u64 per wave (gpk_diag_set_buffer)
 };
 
 // Straight-line common-case parse (fast_parser below). Each bit says the
@@ -748,6 +749,9 @@ __device__ __forceinline__ Outcome run_parser(const KParams& P, const TT& T, con
 #ifndef GPK_FAST
 #define GPK_FAST 1
 #endif
+#ifndef GPK_FAST_TCP_NEED
+#define GPK_FAST_TCP_NEED 20
+#endif
 // TCP options of the straight-line path (tcp.go:336-549 for well-formed
 // option lists without MPTCP): EOL ends the list, NOP, TLVs of length >= 2
 // inside the header. False sends the packet to the general decoder.
@@ -824,7 +828,11 @@ __device__ __forceinline__ bool fast_parser(const KParams& P, const TT& T, const
   int32_t h;
   uint32_t poff, plen;
   if (proto == 6 && (F & GPK_FAST_TCP)) {  // tcp.go:291-551
-    if (len < 20 || off + 20 > W) return false;
+    // the header's first GPK_FAST_TCP_NEED bytes must be in the window: every
+    // field an output reads (ports, data offset, flags; the checksum at 16-17
+    // goes through the mixed reader) lies there, the urgent pointer (18-19) is
+    // never read
+    if (len < 20 || off + GPK_FAST_TCP_NEED > W) return false;
     const uint32_t ds = (rd8(rl, off + 12) >> 4) * 4;
     if (ds < 20 || ds > len) return false;
     // options: the block NOP, NOP, Timestamps (kind 8, length 10) is well

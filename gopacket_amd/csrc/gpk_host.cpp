@@ -450,6 +450,9 @@ static int note_launch(gpk_ctx* c, int k, hipStream_t s) {
   return GPK_OK;
 }
 
+// Diagnostic builds (GPK_DIAG_TIMES) write per-wave timestamps here.
+static std::atomic<uint64_t*> g_diag{nullptr};
+
 static int make_params(gpk_ctx* c, const gpk_parser* p, const gpk_batch* b, const gpk_results* o,
                        gpk::KParams& P) {
   if (!c || !p || !b) return GPK_EINVAL;
@@ -482,6 +485,12 @@ static int make_params(gpk_ctx* c, const gpk_parser* p, const gpk_batch* b, cons
   P.keys = nullptr;
   P.khash = nullptr;
   P.kcode = nullptr;
+  P.diag = g_diag.load();
+  return GPK_OK;
+}
+
+int gpk_diag_set_buffer(void* buf) {
+  g_diag.store(static_cast<uint64_t*>(buf));
   return GPK_OK;
 }
 

@@ -51,6 +51,9 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 #ifndef GPK_MID_W5
 #define GPK_MID_W5 1  // small-packet kernels of parsers without IPv6: dword-aligned 5-chunk window
 #endif
+#ifndef GPK_MID_IP6
+#define GPK_MID_IP6 0  // ... for parsers with IPv6 too
+#endif
 #ifndef GPK_PB_GRAN
 #define GPK_PB_GRAN 1  // dense phase B: 16-byte chunks per lane per pass (A/B r03: 1 KiB passes, whole
                        // lines per load instruction, beat 2 KiB passes of two half-coalesced loads by 20 %)
@@ -81,6 +84,15 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 #endif
 #ifndef GPK_DIAG_NOPARSE
 #define GPK_DIAG_NOPARSE 0  // timing only: skip DecodeLayers (fixed layout)
+#endif
+#ifndef GPK_PERSIST
+#define GPK_PERSIST 0  // persistent waves for the 6-chunk L4 kernels: next tile's windows by LDS-DMA during phase B
+#endif
+#ifndef GPK_PERS_DO
+#define GPK_PERS_DO 7  // ... its phase-B depth as decode_packet's O (7: GPK_PB_DEPTH7 passes, 6: GPK_PB_DEPTH)
+#endif
+#ifndef GPK_DIAG_TIMES
+#define GPK_DIAG_TIMES 0  // diagnostic builds: per-wave phase timestamps into KParams.diag (tools/wave_times.py)
 #endif
 #ifndef GPK_PB_NULL
 #define GPK_PB_NULL 0  // timing only: phase-B stream loads read nothing (zero-record descriptors)
@@ -523,7 +535,6 @@ __device__ __forceinline__ void stream_issue(const KParams& P, Stream<D>& S, uin
                                              int d0, int d1) {
   S.R0 = R0;
   S.R = R;
-  S.on = true;
   // whole 16-byte chunks: the range check zeroes a 16-byte load that
   // crosses the record limit, not just its bytes past it
   const __amdgpu_buffer_rsrc_t rs = rsrc(P.data + R0, (R + 15) & ~15u);
@@ -561,13 +572,21 @@ __device__ __forceinline__ bool dense_region(bool job, uint64_t s, uint64_t e, u
 // first E passes are issued now (their slot registers stay live through
 // DecodeLayers, so only a few: tools/check_stream_isa.py rejects a build
 // whose register allocation touches them), the rest when phase B begins.
+// The passes are issued on every path, over an empty region (range-checked
+// zeros, no memory access) when the wave's packets are not packed, and
+// segment_sums drains them first on every path: no later branch has to know
+// whether they were issued.
 template <int D, int E>
 __device__ __forceinline__ void stream_start(const KParams& P, Stream<D>& S, bool active, uint64_t off, uint32_t cl,
                                              uint32_t lane) {
   uint64_t R0;
   uint32_t R;
-  S.on = false;
-  if (dense_region(active, off, off + cl, R0, R)) stream_issue(P, S, R0, R, lane, 0, E < D ? E : D);
+  S.on = dense_region(active, off, off + cl, R0, R);
+  if (!S.on) {
+    R0 = 0;
+    R = 0;
+  }
+  stream_issue(P, S, R0, R, lane, 0, E < D ? E : D);
 }
 
 // All stream loads of the wave have landed (the slot registers are free).
@@ -581,25 +600,29 @@ __device__ __forceinline__ void stream_drain(Stream<D>& S) {
 // packet's first bytes, in the next lane's window; the bytes before e in that
 // chunk are not the granule's): the segment then takes P(ge) minus them
 // instead of P(ge - 1) plus the bytes before e.
+// The head / tail part of a dense segment sum (issued before the stream: the
+// head and tail chunks come from the LDS header windows when a window holds
+// them, hlds / tlds = LDS byte address, else ~0, else from memory). Returns the
+// correction L; ta: the granule of e is streamed and P(ge) is taken.
+__device__ __forceinline__ uint32_t dense_head_tail(const KParams& P, uint64_t R0, uint32_t R, bool job, uint64_t s,
+                                                    uint64_t e, uint32_t hlds, uint32_t tlds, bool tafter, bool& ta) {
+  static_assert(kGran == 1, "head/tail chunks from the LDS window need 16-byte granules");
+  const __amdgpu_buffer_rsrc_t rs = rsrc(P.data + R0, (R + 15) & ~15u);
+  const uint32_t rsl = job ? (uint32_t)(s - R0) : 0u, rel = job ? (uint32_t)(e - R0) : 0u;
+  ta = tafter && rel < R;  // the granule of e is streamed: P(ge) exists
+  u32x4 hc = lds_chunk(hlds), tc = lds_chunk(tlds);
+  if (hlds == ~0u) hc = __builtin_amdgcn_raw_buffer_load_b128(rs, rsl & ~15u, 0, 0);
+  if (tlds == ~0u || (tafter && !ta)) tc = __builtin_amdgcn_raw_buffer_load_b128(rs, rel & ~15u, 0, 0);
+  return chunk_l_below(tc, rel & 15u, 0u) - (ta ? chunk_l(tc, 0u) : 0u) - chunk_l_below(hc, rsl & 15u, 0u);
+}
+
 template <int D>
 __device__ __forceinline__ uint32_t dense_segment_sums(const KParams& P, Stream<D>& S, bool job, uint64_t s,
-                                                       uint64_t e, uint32_t lane, uint32_t hlds, uint32_t tlds,
-                                                       bool tafter) {
-  static_assert(kGran == 1, "head/tail chunks from the LDS window need 16-byte granules");
+                                                       uint64_t e, uint32_t lane, uint32_t L, bool ta) {
   const uint64_t R0 = S.R0;
   const uint32_t R = S.R;
   const __amdgpu_buffer_rsrc_t rs = rsrc(P.data + R0, (R + 15) & ~15u);
   const uint32_t rsl = job ? (uint32_t)(s - R0) : 0u, rel = job ? (uint32_t)(e - R0) : 0u;
-  // head / tail chunks: from the LDS header windows when a window holds them
-  // (hlds / tlds = LDS byte address, else ~0), else from memory
-  uint32_t L = 0;
-  const bool ta = tafter && rel < R;  // the granule of e is streamed: P(ge) exists
-  {
-    u32x4 hc = lds_chunk(hlds), tc = lds_chunk(tlds);
-    if (hlds == ~0u) hc = __builtin_amdgcn_raw_buffer_load_b128(rs, rsl & ~15u, 0, 0);
-    if (tlds == ~0u || (tafter && !ta)) tc = __builtin_amdgcn_raw_buffer_load_b128(rs, rel & ~15u, 0, 0);
-    L = chunk_l_below(tc, rel & 15u, 0u) - (ta ? chunk_l(tc, 0u) : 0u) - chunk_l_below(hc, rsl & 15u, 0u);
-  }
   const uint32_t np = (R + kPassBytes - 1) / kPassBytes;  // wave-uniform
   const uint32_t vo = lane * kGranBytes;
   Gran (&ring)[D] = S.ring;
@@ -725,39 +748,64 @@ __device__ __forceinline__ uint32_t sparse_segment_sums(const KParams& P, bool j
   return own;
 }
 
+// What a caller runs once per wave between its last read of the LDS header
+// windows and phase B's stream (the persistent kernel issues the next tile's
+// window loads there), and where those loads must have landed (wait).
+struct NoHook {
+  __device__ __forceinline__ void operator()() const {}
+  __device__ __forceinline__ void wait() const {}
+};
+
 // Word sums of every job lane's segment [s, e): the dense prefix stream (the
 // one started early, else one over the segments' region when that is
-// compact), else the per-segment stream.
-template <int D, int E>
+// compact), else the per-segment stream. hook() runs once on every path,
+// after the head / tail chunks have been read and before the stream's loads.
+template <int D, int E, class Hook>
 __device__ __forceinline__ uint32_t segment_sums(const KParams& P, Stream<D>& S, bool job, uint64_t s, uint64_t e,
-                                                 uint32_t lane, uint32_t hlds, uint32_t tlds, bool tafter) {
-  if (S.on) {
-    if (!__ballot(job)) {  // nothing to sum: the early loads still land before their registers are reused
-      stream_drain(S);
+                                                 uint32_t lane, uint32_t hlds, uint32_t tlds, bool tafter,
+                                                 const Hook& hook) {
+  bool ta = false;
+  // The early passes (E > 0: issued on every path) have landed during the
+  // parse; waiting for them here (their registers as operands) puts any
+  // register copy the allocator needs between the early slots and the loop's
+  // after the data is in.
+  if (E > 0) stream_drain(S);
+  if (E > 0 && S.on) {
+    if (!__ballot(job)) {  // nothing to sum
+      hook();
+      hook.wait();
       return 0;
     }
-    // The early passes have landed during the parse; waiting for them here
-    // (their registers as operands) puts any register copy the allocator
-    // needs between the early slots and the loop's after the data is in.
-    stream_drain(S);
+    const uint32_t L = dense_head_tail(P, S.R0, S.R, job, s, e, hlds, tlds, tafter, ta);
+    hook();  // landed by the stream's first waits (its loads are older than the stream's)
     stream_issue(P, S, S.R0, S.R, lane, E < D ? E : D, D);
-    return dense_segment_sums<D>(P, S, job, s, e, lane, hlds, tlds, tafter);
+    return dense_segment_sums<D>(P, S, job, s, e, lane, L, ta);
   }
   // (with the early start on, a wave whose packets are not packed goes to
   // the per-segment stream: one call site keeps the slot registers in place)
   uint64_t R0;
   uint32_t R;
   if (E == 0 && dense_region(job, s, e, R0, R)) {
+    const uint32_t L = dense_head_tail(P, R0, R, job, s, e, hlds, tlds, tafter, ta);
+    hook();
     stream_issue(P, S, R0, R, lane, 0, D);
-    return dense_segment_sums<D>(P, S, job, s, e, lane, hlds, tlds, tafter);
+    return dense_segment_sums<D>(P, S, job, s, e, lane, L, ta);
   }
-  if (!__ballot(job)) return 0;
-  return sparse_segment_sums(P, job, s, e, lane);
+  hook();
+  if (!__ballot(job)) {
+    hook.wait();
+    return 0;
+  }
+  const uint32_t r = sparse_segment_sums(P, job, s, e, lane);
+  hook.wait();
+  return r;
 }
 
-template <bool kL4, bool kLayout, class TT, bool kKeys, int W, int O, int AL>
+template <bool kL4, bool kLayout, class TT, bool kKeys, int W, int O, int AL, int kSlotStride = W * 4 + 1,
+          int kEarly = -1, class Hook = NoHook>
 __device__ __forceinline__ void decode_packet(const KParams& P, const TT& T, uint64_t i, bool active, uint64_t off,
-                                              uint32_t cl, const WinGeo& g, uint32_t slot_dw, uint32_t lane) {
+                                              uint32_t cl, const WinGeo& g, uint32_t slot_dw, uint32_t lane,
+                                              uint64_t* dt, const Hook& hook = Hook()) {
   const uint32_t m = g.m, win = g.win;
   Rd r{P.data + off, slot_dw * 4 + m, win};
 
@@ -766,10 +814,10 @@ __device__ __forceinline__ void decode_packet(const KParams& P, const TT& T, uin
   constexpr int D = kLayout ? 4 : (O > 6 ? GPK_PB_DEPTH7 : GPK_PB_DEPTH);  // layouts: fewer registers left
   // early passes: as many as the kernel's register budget carries through
   // DecodeLayers untouched (tools/check_stream_isa.py)
-  constexpr int E = (kLayout || kKeys) ? 0 : (O > 6 ? GPK_PB_EARLY7 : GPK_PB_EARLY);
+  constexpr int E = kEarly >= 0 ? kEarly : ((kLayout || kKeys) ? 0 : (O > 6 ? GPK_PB_EARLY7 : GPK_PB_EARLY));
   Stream<D> S;
   S.on = false;
-  if (kL4 && E > 0 && (P.outputs & GPK_OUT_L4_CSUM)) stream_start<D, E>(P, S, active, off, cl, lane);
+  if (kL4 && E > 0) stream_start<D, E>(P, S, active && (P.outputs & GPK_OUT_L4_CSUM), off, cl, lane);
 
   // ---- Phase A: DecodeLayers ------------------------------------------------
   Parse q;
@@ -897,6 +945,9 @@ __device__ __forceinline__ void decode_packet(const KParams& P, const TT& T, uin
   const uint32_t lay_lo = (uint32_t)q.layers, lay_hi = (uint32_t)(q.layers >> 32);
 
   // ---- Phase B: segment sums ---------------------------------------------
+#if GPK_DIAG_TIMES
+  dt[3] = __builtin_amdgcn_s_memrealtime();
+#endif
   if (kL4) {
     // the segment's first and last chunk in an LDS header window: its own,
     // or (the segment ending where the next packet starts) the next lane's
@@ -913,7 +964,7 @@ __device__ __forceinline__ void decode_packet(const KParams& P, const TT& T, uin
       if (GPK_PB_LDS_HT && job && (je >> 4) - c0 < nch)
         tlds = slot_dw * 4 + 16 * (uint32_t)((je >> 4) - c0);
       else if (GPK_PB_LDS_HT && job && lane < 63 && nnch && (noff >> 4) == (je >> 4))
-        tlds = (slot_dw + slot_dw_of<W>()) * 4;
+        tlds = (slot_dw + kSlotStride) * 4;
     } else {
       // the window holds batch bytes [wb, wb + m + win): a head/tail chunk
       // (16-byte aligned in the batch, dword-aligned in the slot) is taken
@@ -928,16 +979,23 @@ __device__ __forceinline__ void decode_packet(const KParams& P, const TT& T, uin
       } else if (GPK_PB_LDS_HT && job && lane < 63 && nnch && noff == je) {
         // the next packet starts at e: its window (packet byte 0 at slot byte
         // nm) holds the granule's bytes from e on, at a dword-aligned address
-        tlds = (slot_dw + slot_dw_of<W>()) * 4 + nm - (uint32_t)(je & 15);
+        tlds = (slot_dw + kSlotStride) * 4 + nm - (uint32_t)(je & 15);
         tafter = true;
       }
     }
-    const uint32_t sum = segment_sums<D, E>(P, S, job, js, je, lane, hlds, tlds, tafter);
+    const uint32_t sum = segment_sums<D, E>(P, S, job, js, je, lane, hlds, tlds, tafter, hook);
+#if GPK_DIAG_TIMES
+    dt[4] = __builtin_amdgcn_s_memrealtime();
+    dt[7] = (uint64_t)(S.on ? S.R : 0u) | (uint64_t)__popcll(__ballot(job)) << 32;
+#endif
     if (job) {
       l4c = fold(jinit + sum - jexist);
       const bool udp = (st & GPK_ST_L4_UDP) != 0;
       if (l4c == jexist || (udp && jexist == 0)) st |= GPK_ST_L4_VALID;
     }
+  } else {
+    hook();
+    hook.wait();
   }
   if (active)  // written once, never read back here: non-temporal
     __builtin_nontemporal_store(u32x4{lay_lo, lay_hi, st, ip4c | (l4c << 16)}, reinterpret_cast<u32x4*>(P.records) + i);
@@ -967,7 +1025,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W == 4 ?
   // Every packet's index, then its header window and the table blob are in
   // flight together: two dependent memory round trips per packet.
   const uint64_t i0 = (uint64_t)blockIdx.x * kBlock + tid;
+  uint64_t dt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#if GPK_DIAG_TIMES
+  dt[0] = __builtin_amdgcn_s_memrealtime();
+#endif
   const Idx c0 = load_index(P, i0);
+#if GPK_DIAG_TIMES
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  dt[1] = __builtin_amdgcn_s_memrealtime();
+#endif
   const WinGeo g0 = win_geo<W, AL>(P, c0, i0 < P.n);
   WinT<W> w0;
   load_window<W, AL>(P, g0, w0);
@@ -982,12 +1048,153 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W == 4 ?
     __syncthreads();
   }
   store_window<W, AL>(slot_dw, w0);
+#if GPK_DIAG_TIMES
+  dt[2] = __builtin_amdgcn_s_memrealtime();
+#endif
   if (kCompact)
     decode_packet<kL4, kLayout, LTab, kKeys, W, O, AL>(P, LTab{P.cg, base}, i0, i0 < P.n, c0.off, c0.cl, g0, slot_dw,
-                                                       tid & 63);
+                                                       tid & 63, dt);
   else
     decode_packet<kL4, kLayout, GTab, kKeys, W, O, AL>(P, GTab{P.tab}, i0, i0 < P.n, c0.off, c0.cl, g0, slot_dw,
-                                                       tid & 63);
+                                                       tid & 63, dt);
+#if GPK_DIAG_TIMES
+  // timestamps (100 MHz realtime counter, one clock for all XCDs), HW_ID | XCC_ID << 32, the
+  // phase-B region bytes | job lanes << 32
+  dt[5] = __builtin_amdgcn_s_memrealtime();
+  dt[6] = (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 4) | (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32;
+  if (P.diag && (tid & 63) < 8) {
+    uint64_t v = dt[0];
+#pragma unroll
+    for (int k = 1; k < 8; k++) v = (tid & 7) == (uint32_t)k ? dt[k] : v;
+    P.diag[((uint64_t)blockIdx.x * kWaves + tid / 64) * 8 + (tid & 7)] = v;
+  }
+#endif
+}
+
+// ---- persistent waves ------------------------------------------------------
+// A wave decodes 64-packet tiles t, t + S, t + 2S, ... (S = the waves of the
+// grid, which is sized to be resident at once, so the tiles active across the
+// chip stay one contiguous window of the batch). No wave ends between tiles:
+// the per-wave start-up of the one-tile kernel (dispatch, index round trip,
+// header-window round trip, the block's LDS held until its last wave ends;
+// tools/wave_times.py) is paid once. The next tile's index is loaded at the
+// top of each tile and its header windows go straight into this wave's LDS
+// slots by LDS-DMA (no VGPRs) once phase B no longer reads them, so they land
+// while the current tile's segments stream.
+
+// 16 bytes per lane into LDS: lane l's bytes land at LDS byte `lds` + 16 l
+// (wave-uniform destination, per-lane source; tools/probes/lds_dma.hip).
+__device__ __forceinline__ void dma16(uint64_t src, uint32_t lds) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(src), "s"(lds)
+               : "memory");
+}
+
+// The W-chunk header windows of a tile's 64 packets into the wave's slots
+// (slot q at byte 16 W q of `region`, no padding dword: one LDS-DMA
+// instruction writes 1 KiB contiguously). Instruction k's lane l carries
+// cell 64 k + l = chunk c of packet q (q = cell / W), so every lane fetches
+// packet q's window base and chunk count from lane q (ds_bpermute). Chunks
+// past a packet's window re-read its last chunk, a packet with none the
+// parser's table copy, as load_window does.
+template <int W>
+struct WinDma {
+  const uint8_t* data;
+  const void* tab;
+  Idx x;         // the next tile's index entry of this lane
+  bool active;   // ... is a packet of the batch
+  bool more;     // wave-uniform: there is a next tile
+  uint32_t region, lane;
+  __device__ __forceinline__ void operator()() const {
+    if (!more) return;
+    const uint32_t m = (uint32_t)(x.off & 15), win = x.cl < 16u * W - m ? x.cl : 16u * W - m;
+    const uint32_t nch = active ? (m + win + 15) >> 4 : 0u;
+    const uint64_t src = nch ? (uint64_t)(uintptr_t)(data + (x.off - m)) : (uint64_t)(uintptr_t)tab;
+    const uint32_t last = nch ? nch - 1 : 0u;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of the old windows are done
+#pragma unroll
+    for (int k = 0; k < W; k++) {
+      const uint32_t e = 64u * k + lane, q = e / W, c = e - q * W;
+      const int qa = (int)(q << 2);
+      const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute(qa, (int)(uint32_t)src);
+      const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute(qa, (int)(uint32_t)(src >> 32));
+      const uint32_t lq = (uint32_t)__builtin_amdgcn_ds_bpermute(qa, (int)last);
+      dma16(((uint64_t)hi << 32 | lo) + 16u * (c < lq ? c : lq), region + 1024u * k);
+    }
+  }
+  // the windows have landed (paths whose own waits do not cover them)
+  __device__ __forceinline__ void wait() const {
+    if (more) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+};
+
+template <bool kL4, bool kCompact, int W, int O>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(O, 8))) void decode_pers_kernel(KParams Pv) {
+  const KParams& P0 = Pv;
+  constexpr int kStride = 4 * W;  // LDS dwords per lane
+  const uint32_t tid = threadIdx.x, lane0 = tid & 63;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const uint32_t base = kBlock * kStride;
+  if (kCompact) {  // the table blob, once per block
+    static_assert(kCtDwords <= 3 * kBlock, "three blob words per thread");
+    const uint32_t last = P0.cg.words - 1;
+#pragma unroll
+    for (uint32_t k = 0; k < 3; k++) {
+      const uint32_t j = tid + k * kBlock < last ? tid + k * kBlock : last;
+      gpk_smem[base + j] = P0.ctab[j];
+    }
+    __syncthreads();
+  }
+  const uint64_t ntiles = (P0.n + 63) >> 6;
+  const uint64_t stride = (uint64_t)gridDim.x * kWaves;
+  uint64_t t = (uint64_t)blockIdx.x * kWaves + wave;
+  if (t >= ntiles) return;
+  const uint32_t region =
+      __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)gpk_smem + wave * (64u * kStride * 4u));
+  Idx cur = load_index(P0, t * 64 + lane0);
+  {
+    const WinDma<W> h{P0.data, P0.tab, cur, t * 64 + lane0 < P0.n, true, region, lane0};
+    h();
+    h.wait();
+  }
+  for (;;) {
+    const KParams& P = Pv;
+    // lane-derived values re-formed per tile as well (hoisted, they are spilled)
+    uint32_t lane = lane0;
+    asm volatile("" : "+v"(lane));
+    const uint32_t slot_dw = (wave * 64u + lane) * kStride;
+    const uint64_t tn = t + stride;
+    const bool more = tn < ntiles;
+    const uint64_t i = t * 64 + lane, in = (more ? tn : t) * 64 + lane;
+    uint64_t dt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#if GPK_DIAG_TIMES
+    dt[0] = dt[1] = dt[2] = __builtin_amdgcn_s_memrealtime();
+#endif
+    const Idx nxt = load_index(P, in);
+    const WinGeo g = win_geo<W, 16>(P, cur, i < P.n);
+    const WinDma<W> h{P.data, P.tab, nxt, in < P.n, more, region, lane};
+    if (kCompact)
+      decode_packet<kL4, false, LTab, false, W, GPK_PERS_DO, 16, kStride, 0, WinDma<W>>(P, LTab{P.cg, base}, i, i < P.n, cur.off,
+                                                                             cur.cl, g, slot_dw, lane, dt, h);
+    else
+      decode_packet<kL4, false, GTab, false, W, GPK_PERS_DO, 16, kStride, 0, WinDma<W>>(P, GTab{P.tab}, i, i < P.n, cur.off,
+                                                                             cur.cl, g, slot_dw, lane, dt, h);
+#if GPK_DIAG_TIMES
+    dt[5] = __builtin_amdgcn_s_memrealtime();
+    dt[6] = (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 4) | (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32;
+    if (P.diag && lane < 8) {
+      uint64_t v = dt[0];
+#pragma unroll
+      for (int k = 1; k < 8; k++) v = lane == (uint32_t)k ? dt[k] : v;
+      P.diag[t * 8 + lane] = v;
+    }
+#endif
+    if (!more) break;
+    t = tn;
+    cur = nxt;
+  }
 }
 
 // Full decoded list of one packet (lists longer than the 16 inline codes).
@@ -1023,30 +1230,59 @@ hipError_t launch(const gpk::KParams* P, hipStream_t stream, int* occ) {
   return hipGetLastError();
 }
 
+// Persistent kernel: as many blocks as are resident at once (LDS, registers).
+template <bool kL4, bool kCompact, int W, int O>
+hipError_t launch_pers(const gpk::KParams* P, hipStream_t stream, int* occ) {
+  using namespace gpk;
+  constexpr int slot_lds = kBlock * 4 * W * 4;
+  const int lds = kCompact ? slot_lds + (int)((P->cg.words + GPK_BLOB_ROUND - 1) & ~(GPK_BLOB_ROUND - 1u)) * 4 : slot_lds;
+  int per_cu = 0;
+  hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, decode_pers_kernel<kL4, kCompact, W, O>, kBlock, lds);
+  if (e != hipSuccess) return e;
+  if (occ) {
+    *occ = per_cu;
+    return hipSuccess;
+  }
+  int dev = 0, cus = 0;
+  if ((e = hipGetDevice(&dev)) != hipSuccess) return e;
+  if ((e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess) return e;
+  const uint64_t tiles = (P->n + 63) / 64, want = (tiles + kWaves - 1) / kWaves;
+  const uint64_t resident = (uint64_t)(per_cu > 0 ? per_cu : 1) * (uint64_t)(cus > 0 ? cus : 1);
+  const unsigned grid = (unsigned)(want < resident ? want : resident);
+  hipLaunchKernelGGL((decode_pers_kernel<kL4, kCompact, W, O>), dim3(grid), dim3(kBlock), lds, stream, *P);
+  return hipGetLastError();
+}
+
 // The specialisation a launch uses (gpk_launch_decode, gpk_launch_name).
 struct Sel {
   bool l4, layout, compact, keys;
   int W, O, AL;
+  bool pers;
 };
 Sel select(const gpk::KParams* P, int with_l4, int with_layout) {
-  Sel s{with_l4 != 0, with_layout != 0, P->ctab != nullptr, P->key_kind != 0, gpk::kWinChunks, GPK_WAVES_PER_EU, 16};
+  Sel s{with_l4 != 0, with_layout != 0, P->ctab != nullptr, P->key_kind != 0, gpk::kWinChunks, GPK_WAVES_PER_EU, 16,
+        false};
   if (s.keys) {  // fused grouping keys: no layouts (gpk_decode_group_batch)
     s.layout = false;
   } else if (!s.l4 && !s.layout && P->small_headers) {
     s.W = 4;
   } else if (!s.layout && !P->big_packets) {
     s.O = GPK_SMALL_WAVES;
-    if (GPK_MID_W5 && P->mid_headers && P->data_end) {  // a dword-aligned 5-chunk window: 7 blocks per CU (LDS)
+    if (GPK_MID_W5 && (P->mid_headers || GPK_MID_IP6) && P->data_end) {  // a dword-aligned 5-chunk window: 7 blocks per CU (LDS)
       s.W = 5;
       s.AL = 4;
     }
   }
+  // persistent waves: the 6-chunk, 16-byte-aligned L4 kernels (C3, C4)
+  s.pers = GPK_PERSIST && s.l4 && !s.layout && !s.keys && s.W == gpk::kWinChunks && s.AL == 16;
+  if (s.pers) s.O = GPK_WAVES_PER_EU;  // 6 blocks per CU by LDS: the 80-VGPR budget costs no occupancy
   return s;
 }
 
 template <bool kCompact>
 hipError_t launch_sel(const gpk::KParams* P, const Sel& s, hipStream_t stream, int* occ) {
   constexpr int W = gpk::kWinChunks;
+  if (s.pers) return launch_pers<true, kCompact, W, GPK_WAVES_PER_EU>(P, stream, occ);
   if (s.keys)
     return s.l4 ? launch<true, false, kCompact, true>(P, stream, occ) : launch<false, false, kCompact, true>(P, stream, occ);
   if (s.W == 4) return launch<false, false, kCompact, false, 4>(P, stream, occ);
@@ -1079,6 +1315,8 @@ extern "C" hipError_t gpk_launch_occupancy(const gpk::KParams* P, int with_l4, i
 // Name of the kernel specialisation gpk_launch_decode would launch.
 extern "C" int gpk_launch_describe(const gpk::KParams* P, int with_l4, int with_layout, char* buf, size_t cap) {
   const Sel s = select(P, with_l4, with_layout);
+  if (s.pers)
+    return snprintf(buf, cap, "gpk::decode_pers_kernel<true,%s,%d,%d>", s.compact ? "true" : "false", s.W, s.O);
   return snprintf(buf, cap, "gpk::decode_kernel<%s,%s,%s,%s,%d,%d,%d>", s.l4 ? "true" : "false",
                   s.layout ? "true" : "false", s.compact ? "true" : "false", s.keys ? "true" : "false", s.W,
                   s.W == 4 ? 6 : s.O, s.AL);

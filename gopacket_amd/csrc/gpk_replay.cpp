@@ -109,6 +109,7 @@ struct Slot {
   uint64_t* d_off = nullptr;
   uint32_t* d_cap = nullptr;
   gpk_capture_info* d_ci = nullptr;
+  uint64_t idx_cap = 0;  // entries of d_off / d_cap / d_ci
   hipStream_t stream = nullptr;
   hipEvent_t h2d = nullptr;  // the slot's HtoD finished: host buffer reusable
   hipError_t h2d_err = hipSuccess;  // the read thread's HtoD of the fresh bytes (device walk)
@@ -224,6 +225,38 @@ std::string alloc_slot(Slot& s, uint64_t C, uint64_t R, bool dev_walk, uint64_t 
   ALLOC_OK(hipMalloc((void**)&s.d_off, max_pk * 8), "hipMalloc index");
   ALLOC_OK(hipMalloc((void**)&s.d_cap, max_pk * 4), "hipMalloc index");
   ALLOC_OK(hipMalloc((void**)&s.d_ci, max_pk * sizeof(gpk_capture_info)), "hipMalloc index");
+  s.idx_cap = max_pk;
+  return "";
+}
+
+// The slot's device index must hold `need` entries, of which the first `keep`
+// (the device walk's packets, written on the slot's stream) are kept. The
+// first size assumes the device walk's blocks (plain EPBs, >= 32 bytes); the
+// host reader's packets that follow can be smaller records (Simple Packet
+// Blocks of 16 bytes, ngread.go:515-530), so a slot full of them grows it.
+std::string grow_index(Slot& s, uint64_t keep, uint64_t need) {
+  if (need <= s.idx_cap) return "";
+  const uint64_t cap = std::max<uint64_t>(need, 2 * s.idx_cap);
+  uint64_t* o = nullptr;
+  uint32_t* c = nullptr;
+  gpk_capture_info* ci = nullptr;
+  ALLOC_OK(hipMalloc((void**)&o, cap * 8), "hipMalloc index");
+  ALLOC_OK(hipMalloc((void**)&c, cap * 4), "hipMalloc index");
+  ALLOC_OK(hipMalloc((void**)&ci, cap * sizeof(gpk_capture_info)), "hipMalloc index");
+  if (keep) {
+    ALLOC_OK(hipMemcpyAsync(o, s.d_off, keep * 8, hipMemcpyDeviceToDevice, s.stream), "DtoD index");
+    ALLOC_OK(hipMemcpyAsync(c, s.d_cap, keep * 4, hipMemcpyDeviceToDevice, s.stream), "DtoD index");
+    ALLOC_OK(hipMemcpyAsync(ci, s.d_ci, keep * sizeof(gpk_capture_info), hipMemcpyDeviceToDevice, s.stream),
+             "DtoD index");
+  }
+  ALLOC_OK(hipStreamSynchronize(s.stream), "hipStreamSynchronize");
+  (void)hipFree(s.d_off);
+  (void)hipFree(s.d_cap);
+  (void)hipFree(s.d_ci);
+  s.d_off = o;
+  s.d_cap = c;
+  s.d_ci = ci;
+  s.idx_cap = cap;
   return "";
 }
 
@@ -493,7 +526,12 @@ extern "C" int gpk_replay_file(gpk_ctx* ctx, const gpk_parser* parser, const cha
         used += pos - p0;
         if (st >= 0 && xi.n) {
           for (uint64_t i = 0; i < xi.n; i++) xi.offsets[i] += pos;
-          good = pl.ok(hipMemcpyAsync(S.d_off + G, xi.offsets, xi.n * 8, hipMemcpyHostToDevice, S.stream), "HtoD index") &&
+          const std::string ge = grow_index(S, G, G + xi.n);
+          if (!ge.empty()) {
+            good = false;
+            if (pl.herr.empty()) pl.herr = ge;
+          }
+          good = good && pl.ok(hipMemcpyAsync(S.d_off + G, xi.offsets, xi.n * 8, hipMemcpyHostToDevice, S.stream), "HtoD index") &&
                  pl.ok(hipMemcpyAsync(S.d_cap + G, xi.caplens, xi.n * 4, hipMemcpyHostToDevice, S.stream), "HtoD index") &&
                  pl.ok(hipMemcpyAsync(S.d_ci + G, xi.ci, xi.n * sizeof(gpk_capture_info), hipMemcpyHostToDevice,
                                       S.stream), "HtoD index") &&

@@ -289,6 +289,11 @@ int gpk_decode_kernel_name(gpk_ctx* ctx, const gpk_parser* p, const gpk_batch* b
 int gpk_decode_occupancy(gpk_ctx* ctx, const gpk_parser* p, const gpk_batch* batch, int with_layouts,
                          int* blocks_per_cu);
 
+/* Diagnostic: device buffer (8 u64 per 64-packet wave, or NULL) that libraries
+ * built with GPK_DIAG_TIMES fill with per-wave phase timestamps on every
+ * decode launch (tools/wave_times.py). Ignored by the default build. */
+int gpk_diag_set_buffer(void* buf);
+
 /* Host-memory variant: batch and results live in host memory (ideally pinned
  * via gpk_host_alloc). Copies HtoD, decodes, copies DtoH; synchronous. */
 int gpk_decode_batch_host(gpk_ctx* ctx, const gpk_parser* p, const gpk_batch* host_batch,

@@ -397,3 +397,32 @@ def pcapgen_payload(block):
     """The packet bytes of a little-endian plain EPB built by pcapgen.epb."""
     cl = int.from_bytes(block[20:24], "little")
     return block[28:28 + cl]
+
+
+@pytest.mark.timeout(300)
+def test_parallel_walk_concurrent_callers():
+    """The walk's worker pool is process-wide: two readers indexing at once on
+    two threads (ctypes releases the GIL) must each get their own sequential
+    result (the pool held one job and a second caller overwrote it)."""
+    import threading
+    head, blocks, _ = big_capture(n=40000, seed=5)
+    a = head + b"".join(blocks)
+    b = head + b"".join(blocks[::-1][:30000])
+    want = {k: index_all_events(d, 0, 8) for k, d in (("a", a), ("b", b))}
+    got, errs = {}, []
+
+    def go(k, d):
+        try:
+            for r in range(4):
+                got[(k, r)] = index_all_events(d, 0, 8)
+        except Exception as e:  # surfaced below
+            errs.append(e)
+
+    th = [threading.Thread(target=go, args=(k, d)) for k, d in (("a", a), ("b", b))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errs, errs
+    for (k, r), ev in got.items():
+        assert ev == want[k], (k, r)

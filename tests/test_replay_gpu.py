@@ -130,3 +130,22 @@ def test_replay_device_walk(gpu_ctx, tmp_path, bo):
         check(gpu_ctx, str(path), raw, slot_bytes=1 << 16, slots=3, batch_pkts=5000)
     finally:
         del os.environ["GPK_REPLAY_HOST_WALK"]
+
+
+def test_replay_small_records_grow_device_index(gpu_ctx, tmp_path):
+    """Simple Packet Blocks of 16 bytes (zero-length packets, ngread.go:515-530)
+    are walked by the host reader and appended to the slot's device index,
+    which was sized for the device walk's >= 32-byte blocks: a slot full of
+    them must grow the index, both after device-walked EPBs (the
+    walked entries are kept) and on their own."""
+    from gopacket_amd import synth
+    raw = pcapgen.shb() + pcapgen.idb(1, 0)
+    for r in range(4):
+        raw += b"".join(pcapgen.epb(synth.packet(4, 100 * r + i)[:60], ts=i) for i in range(40))
+        raw += b"".join(pcapgen.spb(b"") for _ in range(1500))
+        raw += b"".join(pcapgen.spb(synth.packet(4, i)[:20]) for i in range(300))
+    path = tmp_path / "spb.pcapng"
+    path.write_bytes(raw)
+    for slot in (4096, 1 << 14):
+        st = check(gpu_ctx, str(path), raw, slot_bytes=slot, slots=2, batch_pkts=777)
+        assert st["error"] == "EOF"
