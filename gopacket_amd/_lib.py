@@ -109,7 +109,7 @@ class PumpStats(ctypes.Structure):
     _fields_ = [("packets", ctypes.c_uint64), ("packet_bytes", ctypes.c_uint64), ("batches", ctypes.c_uint64),
                 ("ring_bytes_copied", ctypes.c_uint64), ("waits", ctypes.c_uint64), ("wall_s", ctypes.c_double),
                 ("index_s", ctypes.c_double), ("gpu_s", ctypes.c_double), ("kernel_s", ctypes.c_double),
-                ("status", ctypes.c_int), ("error", ctypes.c_char * 160)]
+                ("status", ctypes.c_int), ("error", ctypes.c_char * 160), ("kernel", ctypes.c_char * 96)]
 
 
 PUMP_CB = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p,
@@ -147,7 +147,7 @@ class ReplayStats(ctypes.Structure):
                 ("stream_bytes", ctypes.c_uint64), ("batches", ctypes.c_uint64), ("slots", ctypes.c_uint64),
                 ("wall_s", ctypes.c_double), ("read_s", ctypes.c_double), ("index_s", ctypes.c_double),
                 ("gpu_s", ctypes.c_double), ("kernel_s", ctypes.c_double), ("deliver_s", ctypes.c_double),
-                ("reader_status", ctypes.c_int), ("error", ctypes.c_char * 160)]
+                ("reader_status", ctypes.c_int), ("error", ctypes.c_char * 160), ("kernel", ctypes.c_char * 96)]
 
 
 REPLAY_CB = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p,
@@ -267,6 +267,8 @@ def lib():
         "gpk_bpf_select": ([vp, P(Batch), vp, vp, vp, vp, vp, vp], c_int),
     }
     for name, (args, res) in sig.items():
+        if _VARIANT and not hasattr(L, name):
+            continue  # a kernel variant library: the decode ABI only (gpk_kernels.hip + gpk_host.cpp)
         f = getattr(L, name)
         f.argtypes = args
         f.restype = res
@@ -310,6 +312,9 @@ def synth_lib():
         S.gpk_probe_read.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int,
                                      ctypes.c_void_p]
         S.gpk_probe_read.restype = ctypes.c_int
+        S.gpk_probe_reread.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int, ctypes.c_void_p,
+                                       ctypes.c_void_p]
+        S.gpk_probe_reread.restype = ctypes.c_int
         S.gpk_synth_tpacket_v3.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int,
                                            ctypes.c_uint64, ctypes.c_int32, ctypes.c_uint32, ctypes.c_void_p]
         S.gpk_synth_tpacket_v3.restype = ctypes.c_uint64

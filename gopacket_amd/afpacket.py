@@ -254,6 +254,7 @@ class TPacket:
                                                                 _lib.lib().gpk_last_hip_error().decode()))
         stats = {k: getattr(st, k) for k, _ in _lib.PumpStats._fields_}
         stats["error"] = st.error.decode(errors="replace")
+        stats["kernel"] = st.kernel.decode(errors="replace")
         res = None
         if collect:
             if parts:

@@ -45,6 +45,9 @@
 
 #include "../../include/gpk_afpacket.h"
 
+extern "C" int gpk_decode_batch_ex(gpk_ctx* c, const gpk_parser* p, const gpk_batch* b, const gpk_results* o,
+                                   void* stream, uint64_t packet_bytes, char* kname, size_t kcap);
+
 namespace {
 
 constexpr uint32_t kStatusUser = 1;        // TP_STATUS_USER
@@ -1203,11 +1206,14 @@ extern "C" int gpk_tpacket_pump(gpk_ctx* ctx, const gpk_parser* parser, gpk_tpac
     if (!good) break;
     gpk_tpacket_release_seq(t, &b.rel_seq);
     b.h2d_pending = true;
-    // data_bytes: the batch's span as the mean-packet-size hint (gpk.h)
-    const uint64_t span = n ? b.h_off[n - 1] + b.h_cap[n - 1] - std::min(b.h_off[0], b.h_off[n - 1]) : 0;
-    gpk_batch db{dev, b.d_off, b.d_cap, n, span};
+    // data_bytes: the readable end of the mirror (ring, side regions, slack);
+    // the mean-size hint apart: the batch's capture lengths
+    uint64_t pk_bytes = 0;
+    for (uint64_t i = 0; i < n; i++) pk_bytes += b.h_cap[i];
+    gpk_batch db{dev, b.d_off, b.d_cap, n, ring_bytes + NB * side_cap + 64};
     gpk_results dr{b.d_rec, b.d_err, b.d_flow, nullptr};
-    int drc = gpk_decode_batch(ctx, parser, &db, &dr, b.stream);
+    int drc = gpk_decode_batch_ex(ctx, parser, &db, &dr, b.stream, pk_bytes ? pk_bytes : 1, st->kernel,
+                                  sizeof(st->kernel));
     if (drc) {
       rc = drc;
       good = false;

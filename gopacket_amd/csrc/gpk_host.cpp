@@ -453,8 +453,10 @@ static int note_launch(gpk_ctx* c, int k, hipStream_t s) {
 // Diagnostic builds (GPK_DIAG_TIMES) write per-wave timestamps here.
 static std::atomic<uint64_t*> g_diag{nullptr};
 
+// packet_bytes: the batch's packet bytes (summed capture lengths, or an
+// estimate) for the mean-size hint; 0 = data_bytes, as gpk.h documents.
 static int make_params(gpk_ctx* c, const gpk_parser* p, const gpk_batch* b, const gpk_results* o,
-                       gpk::KParams& P) {
+                       gpk::KParams& P, uint64_t packet_bytes = 0) {
   if (!c || !p || !b) return GPK_EINVAL;
   if (b->n && (!b->data || !b->offsets || !b->caplens)) return GPK_EINVAL;
   // 16-byte chunk reads never leave the 16-byte granule of a valid byte only
@@ -466,7 +468,7 @@ static int make_params(gpk_ctx* c, const gpk_parser* p, const gpk_batch* b, cons
   P.offsets = b->offsets;
   P.caplens = b->caplens;
   P.n = b->n;
-  P.big_packets = b->n && b->data_bytes / b->n >= 1024;
+  P.big_packets = b->n && (packet_bytes ? packet_bytes : b->data_bytes) / b->n >= 1024;
   P.data_end = (b->data_bytes + 15) & ~15ull;
   P.records = o ? o->records : nullptr;
   P.err_args = o ? o->err_args : nullptr;
@@ -486,6 +488,7 @@ static int make_params(gpk_ctx* c, const gpk_parser* p, const gpk_batch* b, cons
   P.khash = nullptr;
   P.kcode = nullptr;
   P.diag = g_diag.load();
+  P.tiles_per_wave = 0;
   return GPK_OK;
 }
 
@@ -505,6 +508,30 @@ int gpk_decode_batch(gpk_ctx* c, const gpk_parser* p, const gpk_batch* b, const 
   int slot = 0;
   rc = upload(c, p, P, &slot);
   if (rc) return rc;
+  HIPCHK(gpk_launch_decode(&P, (p->outputs & GPK_OUT_L4_CSUM) != 0, o->layouts != nullptr, s));
+  return note_launch(c, slot, s);
+}
+
+// gpk_decode_batch for the library's own pipelines (gpk_replay_file,
+// gpk_tpacket_pump), which know the batch's packet bytes apart from the
+// readable end of data: data_bytes is the readable end only, packet_bytes the
+// mean-size hint; the name of the kernel launched goes to kname when given.
+// Library-internal, not part of the C ABI.
+extern "C" __attribute__((visibility("hidden"))) int gpk_decode_batch_ex(gpk_ctx* c, const gpk_parser* p,
+                                                                         const gpk_batch* b, const gpk_results* o,
+                                                                         void* stream, uint64_t packet_bytes,
+                                                                         char* kname, size_t kcap) {
+  if (!o) return GPK_EINVAL;
+  gpk::KParams P;
+  int rc = make_params(c, p, b, o, P, packet_bytes);
+  if (rc) return rc;
+  hipStream_t s = (hipStream_t)stream;
+  std::lock_guard<std::mutex> g(c->mu);
+  HIPCHK(hipSetDevice(c->device));
+  int slot = 0;
+  rc = upload(c, p, P, &slot);
+  if (rc) return rc;
+  if (kname && kcap) gpk_launch_describe(&P, (p->outputs & GPK_OUT_L4_CSUM) != 0, o->layouts != nullptr, kname, kcap);
   HIPCHK(gpk_launch_decode(&P, (p->outputs & GPK_OUT_L4_CSUM) != 0, o->layouts != nullptr, s));
   return note_launch(c, slot, s);
 }

@@ -32,6 +32,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <cstdlib>
 
 #include "gpk_device.h"
 
@@ -87,6 +88,12 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 #endif
 #ifndef GPK_PERSIST
 #define GPK_PERSIST 0  // persistent waves for the 6-chunk L4 kernels: next tile's windows by LDS-DMA during phase B
+#endif
+#ifndef GPK_PERS_TILES
+#define GPK_PERS_TILES 4  // ... consecutive tiles per wave (0: one resident grid, all tiles); env GPK_PERS_TILES overrides
+#endif
+#ifndef GPK_PERS_DMA
+#define GPK_PERS_DMA 1  // ... 0 (diagnostic): each tile's windows loaded at its top through VGPRs, no prefetch
 #endif
 #ifndef GPK_PERS_DO
 #define GPK_PERS_DO 7  // ... its phase-B depth as decode_packet's O (7: GPK_PB_DEPTH7 passes, 6: GPK_PB_DEPTH)
@@ -754,6 +761,7 @@ __device__ __forceinline__ uint32_t sparse_segment_sums(const KParams& P, bool j
 struct NoHook {
   __device__ __forceinline__ void operator()() const {}
   __device__ __forceinline__ void wait() const {}
+  __device__ __forceinline__ void consume() const {}
 };
 
 // Word sums of every job lane's segment [s, e): the dense prefix stream (the
@@ -843,6 +851,7 @@ __device__ __forceinline__ void decode_packet(const KParams& P, const TT& T, uin
   if (active && P.fast) done = fast_parser(P, T, r, cl, q, s);
   if (active && !done) s = run_parser<false>(P, T, r, cl, q);
 #endif
+  hook.consume();
 
   uint32_t st = (s.err & GPK_ST_ERR_MASK) | (s.trunc ? GPK_ST_TRUNCATED : 0u) |
                 ((q.nlayers > GPK_ST_NLAYERS_MASK ? GPK_ST_NLAYERS_MASK : q.nlayers) << GPK_ST_NLAYERS_SHIFT);
@@ -1108,7 +1117,7 @@ struct WinDma {
   bool more;     // wave-uniform: there is a next tile
   uint32_t region, lane;
   __device__ __forceinline__ void operator()() const {
-    if (!more) return;
+    if (!more || !GPK_PERS_DMA) return;
     const uint32_t m = (uint32_t)(x.off & 15), win = x.cl < 16u * W - m ? x.cl : 16u * W - m;
     const uint32_t nch = active ? (m + win + 15) >> 4 : 0u;
     const uint64_t src = nch ? (uint64_t)(uintptr_t)(data + (x.off - m)) : (uint64_t)(uintptr_t)tab;
@@ -1126,8 +1135,13 @@ struct WinDma {
   }
   // the windows have landed (paths whose own waits do not cover them)
   __device__ __forceinline__ void wait() const {
-    if (more) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (more && GPK_PERS_DMA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
+  // The next index is waited for here, on every path (after the parse: it was
+  // loaded at the top of the tile, and no store of this tile is in flight yet).
+  // Otherwise the copy into the loop's registers at the back edge waits for it
+  // with vmcnt(0), i.e. for this tile's record and flow stores too.
+  __device__ __forceinline__ void consume() const { asm volatile("" ::"v"(x.off), "v"(x.cl)); }
 };
 
 template <bool kL4, bool kCompact, int W, int O>
@@ -1147,14 +1161,16 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(O, 8))) 
     }
     __syncthreads();
   }
+  // a wave decodes tiles [first, end): P.tiles_per_wave consecutive tiles
   const uint64_t ntiles = (P0.n + 63) >> 6;
-  const uint64_t stride = (uint64_t)gridDim.x * kWaves;
-  uint64_t t = (uint64_t)blockIdx.x * kWaves + wave;
-  if (t >= ntiles) return;
+  const uint64_t first = ((uint64_t)blockIdx.x * kWaves + wave) * P0.tiles_per_wave;
+  if (first >= ntiles) return;
+  const uint64_t end = first + P0.tiles_per_wave < ntiles ? first + P0.tiles_per_wave : ntiles;
+  uint64_t t = first;
   const uint32_t region =
       __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)gpk_smem + wave * (64u * kStride * 4u));
   Idx cur = load_index(P0, t * 64 + lane0);
-  {
+  if (GPK_PERS_DMA) {
     const WinDma<W> h{P0.data, P0.tab, cur, t * 64 + lane0 < P0.n, true, region, lane0};
     h();
     h.wait();
@@ -1165,8 +1181,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(O, 8))) 
     uint32_t lane = lane0;
     asm volatile("" : "+v"(lane));
     const uint32_t slot_dw = (wave * 64u + lane) * kStride;
-    const uint64_t tn = t + stride;
-    const bool more = tn < ntiles;
+    const uint64_t tn = t + 1;
+    const bool more = tn < end;
     const uint64_t i = t * 64 + lane, in = (more ? tn : t) * 64 + lane;
     uint64_t dt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #if GPK_DIAG_TIMES
@@ -1174,6 +1190,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(O, 8))) 
 #endif
     const Idx nxt = load_index(P, in);
     const WinGeo g = win_geo<W, 16>(P, cur, i < P.n);
+    if (!GPK_PERS_DMA) {
+      WinT<W> w;
+      load_window<W, 16>(P, g, w);
+      store_window<W, 16>(slot_dw, w);
+#if GPK_DIAG_TIMES
+      dt[2] = __builtin_amdgcn_s_memrealtime();
+#endif
+    }
     const WinDma<W> h{P.data, P.tab, nxt, in < P.n, more, region, lane};
     if (kCompact)
       decode_packet<kL4, false, LTab, false, W, GPK_PERS_DO, 16, kStride, 0, WinDma<W>>(P, LTab{P.cg, base}, i, i < P.n, cur.off,
@@ -1246,10 +1270,22 @@ hipError_t launch_pers(const gpk::KParams* P, hipStream_t stream, int* occ) {
   int dev = 0, cus = 0;
   if ((e = hipGetDevice(&dev)) != hipSuccess) return e;
   if ((e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess) return e;
-  const uint64_t tiles = (P->n + 63) / 64, want = (tiles + kWaves - 1) / kWaves;
-  const uint64_t resident = (uint64_t)(per_cu > 0 ? per_cu : 1) * (uint64_t)(cus > 0 ? cus : 1);
-  const unsigned grid = (unsigned)(want < resident ? want : resident);
-  hipLaunchKernelGGL((decode_pers_kernel<kL4, kCompact, W, O>), dim3(grid), dim3(kBlock), lds, stream, *P);
+  // tiles per wave: all of a wave's share when the grid is one resident wave of
+  // blocks (GPK_PERS_TILES=0), else that many consecutive tiles per wave with
+  // the hardware's dispatcher balancing the blocks
+  const uint64_t tiles = (P->n + 63) / 64;
+  const uint64_t resident = (uint64_t)(per_cu > 0 ? per_cu : 1) * (uint64_t)(cus > 0 ? cus : 1) * kWaves;
+  static const long env_t = [] {
+    const char* e = getenv("GPK_PERS_TILES");
+    return e ? strtol(e, nullptr, 10) : (long)GPK_PERS_TILES;
+  }();
+  uint64_t T = env_t > 0 ? (uint64_t)env_t : (tiles + resident - 1) / resident;
+  if (T < 1) T = 1;
+  KParams Q = *P;
+  Q.tiles_per_wave = (uint32_t)T;
+  const uint64_t grid = (tiles + T * kWaves - 1) / (T * kWaves);
+  if (grid > 0xffffffffull) return hipErrorInvalidValue;
+  hipLaunchKernelGGL((decode_pers_kernel<kL4, kCompact, W, O>), dim3((unsigned)grid), dim3(kBlock), lds, stream, Q);
   return hipGetLastError();
 }
 

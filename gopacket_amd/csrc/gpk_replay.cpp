@@ -45,6 +45,9 @@
 #include "../../include/gpk_capture.h"
 #include "gpk_walk.h"
 
+extern "C" int gpk_decode_batch_ex(gpk_ctx* c, const gpk_parser* p, const gpk_batch* b, const gpk_results* o,
+                                   void* stream, uint64_t packet_bytes, char* kname, size_t kcap);
+
 namespace {
 
 double now_s() {
@@ -585,13 +588,21 @@ extern "C" int gpk_replay_file(gpk_ctx* ctx, const gpk_parser* parser, const cha
         pl.free_bats.push_back(b);
         break;
       }
-      // data_bytes: the batch's span in the slot as the mean-packet-size hint;
-      // with the device index, the slot's bytes (gpk.h)
+      // data_bytes: the readable end of data (the device slot and its 16-byte
+      // slack, measured from the base the kernels get); the mean-size hint
+      // apart: the batch's capture lengths (host index), or its share of the
+      // slot's bytes (device index: the capture lengths stay on the device)
+      uint64_t pk_bytes = 0;
+      if (dwalk) {
+        pk_bytes = total ? (uint64_t)((double)L * (double)n / (double)total) : 0;
+      } else {
+        for (uint64_t i = 0; i < n; i++) pk_bytes += B.h_cap[i];
+      }
       gpk_batch db{dwalk ? S.dev + base_off : S.dev, dwalk ? S.d_off + first : B.d_off,
-                   dwalk ? S.d_cap + first : B.d_cap, n,
-                   dwalk ? L : (n ? B.h_off[n - 1] + B.h_cap[n - 1] - B.h_off[0] : 0)};
+                   dwalk ? S.d_cap + first : B.d_cap, n, dwalk ? C + R + 16 - base_off : len + 16};
       gpk_results dr{B.d_rec, B.d_err, B.d_flow, nullptr};
-      int drc = gpk_decode_batch(ctx, parser, &db, &dr, S.stream);
+      int drc = gpk_decode_batch_ex(ctx, parser, &db, &dr, S.stream, pk_bytes ? pk_bytes : 1, stats->kernel,
+                                    sizeof(stats->kernel));
       if (drc) {
         rc = drc;
         finished = true;

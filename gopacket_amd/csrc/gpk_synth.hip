@@ -111,6 +111,69 @@ __global__ __launch_bounds__(256) void probe_read_kernel(const uint8_t* data, ui
   if (acc == 0x9e3779b9u) out[0] = acc;  // keep the loads live; practically never stores
 }
 
+// Re-read probe (the traffic question): one wave per region of
+// 64 "packets" of pkt bytes, the decode kernel's access pattern without its
+// work. mode 0: the region streamed once (1 KiB per pass, 16 B per lane,
+// non-temporal, 8 passes in flight); mode 1: first each lane's 6-chunk
+// header window at its packet (temporal, as the decode kernel loads it), then
+// the same stream, so the window's lines are fetched twice; mode 2: the
+// header windows alone. If the second fetch of a window line costs DRAM
+// bandwidth, mode 1 takes about mode 0 + the re-fetched share; if it is served
+// on chip (L2 / Infinity Cache), mode 1 takes about mode 0. mode 3: the
+// header windows, then a stream that skips the granules they hold (what a
+// phase B taking those granules from the LDS windows would fetch).
+__global__ __launch_bounds__(256) void probe_reread_kernel(const uint8_t* data, uint64_t nbytes, uint32_t pkt,
+                                                           int mode, uint32_t* out) {
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t wave = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const uint64_t R = 64ull * pkt, base = wave * R;
+  if (base + R > nbytes) return;
+  uint32_t acc = 0;
+  if (mode >= 1) {  // 1, 2, 3
+    const uint8_t* h = data + ((base + (uint64_t)lane * pkt) & ~15ull);
+    u32x4 w[6];
+#pragma unroll
+    for (int k = 0; k < 6; k++) w[k] = *reinterpret_cast<const u32x4*>(h + 16 * k);
+#pragma unroll
+    for (int k = 0; k < 6; k++) acc = __builtin_amdgcn_udot4(w[k].x ^ w[k].y ^ w[k].z ^ w[k].w, 0x01010101u, acc, false);
+  }
+  if (mode <= 1 || mode == 3) {
+    const u32x4* v = reinterpret_cast<const u32x4*>(data + base);
+    const uint32_t nv = (uint32_t)(R / 16);
+    // mode 3: the stream skips the 16-byte granules a header window holds
+    // (range-checked loads out of range: zeros, no memory access)
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)(data + base), 0, (int)R, 0x00020000);
+    const uint32_t inv = (uint32_t)((0x100000000ull + pkt - 1) / pkt);  // exact quotient below 2^17 bytes
+    auto covered = [&](uint32_t g) {
+      const uint32_t q = __umulhi(16u * g, inv);
+      const uint32_t s0 = (q * pkt) & ~15u, s1 = q ? (((q - 1) * pkt) & ~15u) : 0xffffffffu;
+      return 16u * g - s0 < 96u || (q && 16u * g - s1 < 96u);
+    };
+    uint32_t k = lane;
+    for (; k + 7 * 64 < nv; k += 8 * 64) {
+      u32x4 a[8];
+      if (mode == 3) {
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+          const uint32_t g = k + 64 * j;
+          a[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, covered(g) ? 0x7ffffff0u : 16u * g, 0, 2);
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; j++) a[j] = __builtin_nontemporal_load(v + k + 64 * j);
+      }
+#pragma unroll
+      for (int j = 0; j < 8; j++) acc = __builtin_amdgcn_udot4(a[j].x ^ a[j].y ^ a[j].z ^ a[j].w, 0x01010101u, acc, false);
+    }
+    for (; k < nv; k += 64) {
+      const u32x4 a = __builtin_nontemporal_load(v + k);
+      acc = __builtin_amdgcn_udot4(a.x ^ a.y ^ a.z ^ a.w, 0x01010101u, acc, false);
+    }
+  }
+  if (acc == 0x9e3779b9u) out[0] = acc;  // keep the loads live; practically never stores
+}
+
 extern "C" {
 
 uint32_t gpk_synth_len(int cfg, uint64_t i) { return frame_len(cfg, i); }
@@ -344,6 +407,15 @@ uint64_t gpk_synth_tp_producer_stop(void* h) {
   uint64_t n = p->rearmed.load();
   delete p;
   return n;
+}
+
+// Launch the re-read probe over the whole regions of data[0, nbytes) on `stream`.
+int gpk_probe_reread(const uint8_t* data, uint64_t nbytes, uint32_t pkt, int mode, uint32_t* out, void* stream) {
+  const uint64_t waves = nbytes / (64ull * pkt), blocks = (waves + 3) / 4;
+  if (!pkt || !blocks) return -1;
+  hipLaunchKernelGGL(probe_reread_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, data, nbytes, pkt,
+                     mode, out);
+  return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
 // Launch the streaming-read probe over data[0, nbytes & ~15) on `stream`.

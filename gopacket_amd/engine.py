@@ -172,6 +172,7 @@ class Context:
                                                                lib().gpk_last_hip_error().decode()))
         stats = {k: getattr(st, k) for k, _ in _lib.ReplayStats._fields_}
         stats["error"] = st.error.decode(errors="replace")
+        stats["kernel"] = st.kernel.decode(errors="replace")
         res = None
         if collect:
             if parts:

@@ -152,6 +152,7 @@ typedef struct gpk_tp_pump_stats {
   double kernel_s; /* decode kernels alone                             */
   int status;      /* 0, or the GPK_TP_ERROR that ended the loop        */
   char error[160];
+  char kernel[96]; /* the decode kernel specialisation of the last launch */
 } gpk_tp_pump_stats;
 
 typedef void (*gpk_tp_pump_cb)(void* user, uint64_t first_packet, uint64_t n, const gpk_record* records,

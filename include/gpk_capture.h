@@ -162,6 +162,7 @@ typedef struct gpk_replay_stats {
   double deliver_s;      /* result callback                                      */
   int reader_status;     /* the GPK_CAP_END error: 0 = io.EOF (clean end)        */
   char error[160];
+  char kernel[96];       /* the decode kernel specialisation of the last launch */
 } gpk_replay_stats;
 
 /* Results of one device launch, in packet order, delivered on the calling

@@ -149,3 +149,24 @@ def test_replay_small_records_grow_device_index(gpu_ctx, tmp_path):
     for slot in (4096, 1 << 14):
         st = check(gpu_ctx, str(path), raw, slot_bytes=slot, slots=2, batch_pkts=777)
         assert st["error"] == "EOF"
+
+
+def test_replay_kernel_choice(gpu_ctx, tmp_path):
+    """The readable end a replay batch passes is measured from the base the
+    kernels get (the batch span understated it and the
+    dword-aligned small-packet window was never used): with the C1 parser
+    (no IPv6 decoder) and small packets the launch is the AL = 4 kernel, on
+    the device walk and on the host walk; packets still match the oracle."""
+    from gopacket_amd import synth
+    pk = [synth.packet(2, i) for i in range(20000)]
+    raw = pcapgen.ng_file(pk)
+    path = tmp_path / "small.pcapng"
+    path.write_bytes(raw)
+    for host_walk in (False, True):
+        if host_walk:
+            os.environ["GPK_REPLAY_HOST_WALK"] = "1"
+        try:
+            st = check(gpu_ctx, str(path), raw, cfg_name="eth_ip4_tcp_payload", slot_bytes=1 << 20, slots=2, batch_pkts=4096)
+        finally:
+            os.environ.pop("GPK_REPLAY_HOST_WALK", None)
+        assert st["kernel"].endswith(",5,7,4>"), (host_walk, st["kernel"])

@@ -79,6 +79,16 @@ def analyse(name, d, n_waves, out):
     bend = blk[:, :, 5].max(axis=1)
     idle = ((bend[:, None] - blk[:, :, 5]) * us).mean()
     lines.append("  block skew: a wave ends %.2f us before its block's last wave (LDS held meanwhile)" % idle)
+    # persistent kernels: tile t runs on wave t mod S (S = resident waves); the first S tiles
+    # should all start at the launch, a late one means its wave found no free slot
+    S = 24 * 256
+    if len(t) > 2 * S:
+        f0 = (t[:S, 0] - t[:, 0].min()) * us
+        lines.append("  start of tiles [0, %d): p50 %.2f us, p90 %.2f, p99 %.2f, max %.2f; after 1 %% of the span: %d" % (
+            S, *np.percentile(f0, [50, 90, 99]), f0.max(), int((f0 > 0.01 * span).sum())))
+        e = (t[:, 5] - t[:, 0].min()) * us
+        lines.append("  last tile end per wave slot: p10 %.1f us, p50 %.1f, min %.1f (span %.1f)" % (
+            *np.percentile([e[k::S].max() for k in range(0, S, 7)], [10, 50]), min(e[k::S].max() for k in range(0, S, 7)), span))
     lines.append("  phase-B region bytes per wave mean %.0f, job lanes mean %.1f" % (
         (pb & 0xffffffff).astype(np.float64).mean(), (pb >> 32).astype(np.float64).mean()))
     for ln in lines:
