@@ -59,8 +59,11 @@ struct gpk_parser {
 // several) each read their own copy: gopacket gives every parser its own
 // state (doc.go:211-228), and a launch on one stream must never see a table
 // rewritten for a launch on another. A copy is rewritten only for a new
-// version, and only after every launch that read it has completed (an event
-// recorded after each launch, per stream).
+// version, and everything is ordered on the device, never by blocking the
+// host: the upload is enqueued on the launching stream behind a wait for
+// every earlier launch that read the slot (done), from the slot's own pinned
+// staging buffer (the parser may change as soon as the call returns), and a
+// launch on another stream waits for the upload (ready).
 struct TabSlot {
   gpk::DevTables* dtab = nullptr;
   uint32_t* dctab = nullptr;  // compact blob (gpk::kCtDwords), valid when compact
@@ -69,10 +72,14 @@ struct TabSlot {
   gpk::CompactGeom cg{};
   uint64_t version = 0;       // parser table version held, 0 = empty
   uint64_t last_use = 0;      // LRU tick
-  // completes after every launch that read this copy so far: recorded on the
-  // context's own stream, which waits for each launch's stream (note_launch),
-  // so it never refers to a caller's stream that may be destroyed meanwhile
-  hipEvent_t done = nullptr;
+  uint8_t* staging = nullptr; // pinned: DevTables, then the compact blob; the last upload's source
+  // Both events are recorded on the context's aggregation stream (agg), which
+  // waits for the stream concerned first, so they never refer to a caller's
+  // stream that may be destroyed meanwhile.
+  hipEvent_t ready = nullptr;  // the slot's last upload has landed
+  hipEvent_t done = nullptr;   // every launch so far that read the slot has completed
+  bool uploaded = false, read = false;
+  bool ready_seen = false;     // ready has been observed complete (no wait needed)
 };
 constexpr int kTabSlots = 8;
 
@@ -85,6 +92,11 @@ struct gpk_ctx {
   void* dbuf = nullptr;
   size_t dbuf_bytes = 0;
   hipStream_t stream = nullptr;
+  // carries only waits and event records: the completion marks of launches and
+  // uploads on callers' streams (note_launch), so no caller stream is coupled to
+  // another and no event outlives the stream it was recorded on
+  hipStream_t agg = nullptr;
+  std::unordered_map<hipStream_t, hipEvent_t> stream_ev;  // one reusable event per caller stream
   std::mutex mu;
   // gpk_replay_file's staging buffers, kept for the next call (gpk_walk.h)
   void* replay_cache = nullptr;
@@ -236,12 +248,17 @@ int gpk_parser_set_udp_port(gpk_parser* p, uint32_t v, int32_t lt) {
 static void free_slots(gpk_ctx* c) {
   for (TabSlot& t : c->slots) {
     if (t.done) (void)hipEventDestroy(t.done);
-    t.done = nullptr;
+    if (t.ready) (void)hipEventDestroy(t.ready);
+    t.done = t.ready = nullptr;
     if (t.dtab) (void)hipFree(t.dtab);
     if (t.dctab) (void)hipFree(t.dctab);
+    if (t.staging) (void)hipHostFree(t.staging);
     t.dtab = nullptr;
     t.dctab = nullptr;
+    t.staging = nullptr;
   }
+  for (auto& kv : c->stream_ev) (void)hipEventDestroy(kv.second);
+  c->stream_ev.clear();
 }
 
 int gpk_ctx_create(gpk_ctx** out, int device) {
@@ -256,6 +273,11 @@ int gpk_ctx_create(gpk_ctx** out, int device) {
     delete c;
     return GPK_EHIP;
   }
+  if (hipStreamCreateWithFlags(&c->agg, hipStreamNonBlocking) != hipSuccess) {
+    (void)hipStreamDestroy(c->stream);
+    delete c;
+    return GPK_EHIP;
+  }
   *out = c;
   return GPK_OK;
 }
@@ -265,6 +287,7 @@ int gpk_ctx_destroy(gpk_ctx* c) {
   (void)hipSetDevice(c->device);
   (void)hipDeviceSynchronize();  // launches still reading the table copies
   if (c->stream) (void)hipStreamDestroy(c->stream);
+  if (c->agg) (void)hipStreamDestroy(c->agg);
   free_slots(c);
   if (c->dbuf) (void)hipFree(c->dbuf);
   if (c->replay_cache && c->replay_cache_free) c->replay_cache_free(c->replay_cache);
@@ -379,16 +402,36 @@ static uint32_t fast_flags(const gpk_parser* p) {
   return f;
 }
 
-// Wait until no launch reads slot t any more (it is about to be rewritten).
-static int drain_slot(TabSlot& t) {
-  if (t.done) HIPCHK(hipEventSynchronize(t.done));
+// The context's reusable event for caller stream s.
+static int stream_event(gpk_ctx* c, hipStream_t s, hipEvent_t* ev) {
+  auto it = c->stream_ev.find(s);
+  if (it == c->stream_ev.end()) {
+    hipEvent_t e = nullptr;
+    HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    it = c->stream_ev.emplace(s, e).first;
+  }
+  *ev = it->second;
   return GPK_OK;
 }
 
-// The device copy of parser p's tables (found, or written into a free or the
-// least recently used slot), and the table fields of P. Returns the slot
-// index in *slot for note_launch.
-static int upload(gpk_ctx* c, const gpk_parser* p, gpk::KParams& P, int* slot) {
+// Record on the aggregation stream, as mark, the point stream s has reached.
+static int mark_after(gpk_ctx* c, hipStream_t s, hipEvent_t mark) {
+  if (s != c->agg) {
+    hipEvent_t ev = nullptr;
+    int rc = stream_event(c, s, &ev);
+    if (rc) return rc;
+    HIPCHK(hipEventRecord(ev, s));
+    HIPCHK(hipStreamWaitEvent(c->agg, ev, 0));
+  }
+  HIPCHK(hipEventRecord(mark, c->agg));
+  return GPK_OK;
+}
+
+// The device copy of parser p's tables for a launch on stream s (found, or
+// written into a free or the least recently used slot), and the table fields
+// of P. Stream-ordered: returns without waiting for the device. Returns the
+// slot index in *slot for note_launch.
+static int upload(gpk_ctx* c, const gpk_parser* p, gpk::KParams& P, int* slot, hipStream_t s) {
   int k = -1;
   for (int i = 0; i < kTabSlots; i++)
     if (c->slots[i].version == p->version && c->slots[i].global_mode == c->force_global) k = i;
@@ -396,18 +439,43 @@ static int upload(gpk_ctx* c, const gpk_parser* p, gpk::KParams& P, int* slot) {
     for (int i = 0; i < kTabSlots; i++)
       if (k < 0 || c->slots[i].last_use < c->slots[k].last_use) k = i;  // empty slots have last_use 0
     TabSlot& t = c->slots[k];
-    int rc = drain_slot(t);
-    if (rc) return rc;
+    constexpr size_t kBlobOff = (sizeof(gpk::DevTables) + 255) & ~size_t(255);
     t.version = 0;
     if (!t.dtab && hipMalloc(&t.dtab, sizeof(gpk::DevTables)) != hipSuccess) return GPK_ENOMEM;
     if (!t.dctab && hipMalloc(&t.dctab, gpk::kCtDwords * 4) != hipSuccess) return GPK_ENOMEM;
-    static thread_local uint32_t blob[gpk::kCtDwords];
-    HIPCHK(hipMemcpyAsync(t.dtab, &p->tab, sizeof(gpk::DevTables), hipMemcpyHostToDevice, c->stream));
+    if (!t.staging && hipHostMalloc((void**)&t.staging, kBlobOff + gpk::kCtDwords * 4, hipHostMallocDefault) != hipSuccess)
+      return GPK_ENOMEM;
+    if (!t.ready) HIPCHK(hipEventCreateWithFlags(&t.ready, hipEventDisableTiming));
+    if (!t.done) HIPCHK(hipEventCreateWithFlags(&t.done, hipEventDisableTiming));
+    // the staging buffer is the source of the slot's previous upload: rewrite
+    // it once that copy has landed (long ago unless slots are thrashing)
+    if (t.uploaded && !t.ready_seen) HIPCHK(hipEventSynchronize(t.ready));
+    // every launch that read the old contents completes before the new upload
+    if (t.read) HIPCHK(hipStreamWaitEvent(s, t.done, 0));
+    memcpy(t.staging, &p->tab, sizeof(gpk::DevTables));
+    uint32_t* blob = reinterpret_cast<uint32_t*>(t.staging + kBlobOff);
     t.compact = !c->force_global && build_compact(p->tab, p->first, blob, t.cg);
-    if (t.compact) HIPCHK(hipMemcpyAsync(t.dctab, blob, gpk::kCtDwords * 4, hipMemcpyHostToDevice, c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));  // on the device before any launch; p->tab and blob may change
+    HIPCHK(hipMemcpyAsync(t.dtab, t.staging, sizeof(gpk::DevTables), hipMemcpyHostToDevice, s));
+    if (t.compact) HIPCHK(hipMemcpyAsync(t.dctab, blob, gpk::kCtDwords * 4, hipMemcpyHostToDevice, s));
+    int rc = mark_after(c, s, t.ready);
+    if (rc) return rc;
+    t.uploaded = true;
+    t.ready_seen = false;
     t.version = p->version;
     t.global_mode = c->force_global;
+  } else {
+    // uploaded by a launch on some stream: this launch waits for the copy
+    TabSlot& t = c->slots[k];
+    if (!t.ready_seen) {
+      const hipError_t q = hipEventQuery(t.ready);
+      if (q == hipSuccess) {
+        t.ready_seen = true;
+      } else if (q == hipErrorNotReady) {
+        HIPCHK(hipStreamWaitEvent(s, t.ready, 0));
+      } else {
+        return hip_fail(q, "hipEventQuery(ready)");
+      }
+    }
   }
   TabSlot& t = c->slots[k];
   t.last_use = ++c->tick;
@@ -430,31 +498,20 @@ static int upload(gpk_ctx* c, const gpk_parser* p, gpk::KParams& P, int* slot) {
   return GPK_OK;
 }
 
-// A launch on stream s reads slot k: record that, so the slot is rewritten
-// only after it completes. The context's stream waits for s at this point
-// (a transient event, released at once) and the slot's event is recorded
-// after that wait: it completes once every launch so far that read the slot
-// has, whatever happens to s afterwards.
+// A launch on stream s reads slot k: the slot's done mark moves past it (on
+// the aggregation stream, which waits for s there; one reusable event per
+// caller stream), so the slot is rewritten only after it completes.
 static int note_launch(gpk_ctx* c, int k, hipStream_t s) {
   TabSlot& t = c->slots[k];
-  if (s != c->stream) {
-    hipEvent_t ev = nullptr;
-    HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-    hipError_t e = hipEventRecord(ev, s);
-    if (e == hipSuccess) e = hipStreamWaitEvent(c->stream, ev, 0);
-    (void)hipEventDestroy(ev);
-    HIPCHK(e);
-  }
-  if (!t.done) HIPCHK(hipEventCreateWithFlags(&t.done, hipEventDisableTiming));
-  HIPCHK(hipEventRecord(t.done, c->stream));
+  int rc = mark_after(c, s, t.done);
+  if (rc) return rc;
+  t.read = true;
   return GPK_OK;
 }
 
 // Diagnostic builds (GPK_DIAG_TIMES) write per-wave timestamps here.
 static std::atomic<uint64_t*> g_diag{nullptr};
 
-// packet_bytes: the batch's packet bytes (summed capture lengths, or an
-// estimate) for the mean-size hint; 0 = data_bytes, as gpk.h documents.
 static int make_params(gpk_ctx* c, const gpk_parser* p, const gpk_batch* b, const gpk_results* o,
                        gpk::KParams& P, uint64_t packet_bytes = 0) {
   if (!c || !p || !b) return GPK_EINVAL;
@@ -506,7 +563,7 @@ int gpk_decode_batch(gpk_ctx* c, const gpk_parser* p, const gpk_batch* b, const 
   std::lock_guard<std::mutex> g(c->mu);
   HIPCHK(hipSetDevice(c->device));
   int slot = 0;
-  rc = upload(c, p, P, &slot);
+  rc = upload(c, p, P, &slot, s);
   if (rc) return rc;
   HIPCHK(gpk_launch_decode(&P, (p->outputs & GPK_OUT_L4_CSUM) != 0, o->layouts != nullptr, s));
   return note_launch(c, slot, s);
@@ -529,7 +586,7 @@ extern "C" __attribute__((visibility("hidden"))) int gpk_decode_batch_ex(gpk_ctx
   std::lock_guard<std::mutex> g(c->mu);
   HIPCHK(hipSetDevice(c->device));
   int slot = 0;
-  rc = upload(c, p, P, &slot);
+  rc = upload(c, p, P, &slot, s);
   if (rc) return rc;
   if (kname && kcap) gpk_launch_describe(&P, (p->outputs & GPK_OUT_L4_CSUM) != 0, o->layouts != nullptr, kname, kcap);
   HIPCHK(gpk_launch_decode(&P, (p->outputs & GPK_OUT_L4_CSUM) != 0, o->layouts != nullptr, s));
@@ -554,7 +611,7 @@ extern "C" __attribute__((visibility("hidden"))) int gpk_decode_batch_keys(gpk_c
   std::lock_guard<std::mutex> g(c->mu);
   HIPCHK(hipSetDevice(c->device));
   int slot = 0;
-  rc = upload(c, p, P, &slot);
+  rc = upload(c, p, P, &slot, s);
   if (rc) return rc;
   HIPCHK(gpk_launch_decode(&P, (p->outputs & GPK_OUT_L4_CSUM) != 0, o->layouts != nullptr, s));
   return note_launch(c, slot, s);
@@ -571,7 +628,7 @@ int gpk_decode_kernel_name(gpk_ctx* c, const gpk_parser* p, const gpk_batch* b, 
   std::lock_guard<std::mutex> g(c->mu);
   HIPCHK(hipSetDevice(c->device));
   int slot = 0;
-  rc = upload(c, p, P, &slot);
+  rc = upload(c, p, P, &slot, c->stream);
   if (rc) return rc;
   return gpk_launch_describe(&P, (p->outputs & GPK_OUT_L4_CSUM) != 0, with_layouts != 0, buf, cap);
 }
@@ -584,7 +641,7 @@ int gpk_decode_occupancy(gpk_ctx* c, const gpk_parser* p, const gpk_batch* b, in
   std::lock_guard<std::mutex> g(c->mu);
   HIPCHK(hipSetDevice(c->device));
   int slot = 0;
-  rc = upload(c, p, P, &slot);
+  rc = upload(c, p, P, &slot, c->stream);
   if (rc) return rc;
   HIPCHK(gpk_launch_occupancy(&P, (p->outputs & GPK_OUT_L4_CSUM) != 0, with_layouts != 0, blocks_per_cu));
   return GPK_OK;
@@ -630,7 +687,7 @@ int gpk_decode_batch_host(gpk_ctx* c, const gpk_parser* p, const gpk_batch* hb, 
   rc = make_params(c, p, &db, &dr, P);
   if (rc) return rc;
   int slot = 0;
-  rc = upload(c, p, P, &slot);
+  rc = upload(c, p, P, &slot, s);
   if (rc) return rc;
   HIPCHK(gpk_launch_decode(&P, (p->outputs & GPK_OUT_L4_CSUM) != 0, dr.layouts != nullptr, s));
   rc = note_launch(c, slot, s);
@@ -658,7 +715,7 @@ int gpk_decoded_list(gpk_ctx* c, const gpk_parser* p, const gpk_batch* b, uint64
   uint32_t* dn = (uint32_t*)((char*)c->dbuf + align_up(8 * (size_t)cap));
   hipStream_t s = c->stream;
   int slot = 0;
-  rc = upload(c, p, P, &slot);
+  rc = upload(c, p, P, &slot, s);
   if (rc) return rc;
   HIPCHK(gpk_launch_list(&P, index, dl, cap, dn, s));
   rc = note_launch(c, slot, s);
@@ -692,7 +749,7 @@ int gpk_decoded_list_host(gpk_ctx* c, const gpk_parser* p, const uint8_t* pkt, u
   rc = make_params(c, p, &db, nullptr, P);
   if (rc) return rc;
   int slot = 0;
-  rc = upload(c, p, P, &slot);
+  rc = upload(c, p, P, &slot, s);
   if (rc) return rc;
   HIPCHK(gpk_launch_list(&P, 0, (int64_t*)(d + o_list), cap, (uint32_t*)(d + o_n), s));
   rc = note_launch(c, slot, s);

@@ -43,10 +43,10 @@ def test_alternating_parsers_on_two_streams(gpu_ctx):
     torch.cuda.synchronize()
     for it in range(3):
         for k in names:
-            rec = torch.empty(n * 16, dtype=torch.uint8, device="cuda")
-            err = torch.zeros(2 * n, dtype=torch.int32, device="cuda")
-            fl = torch.empty(3 * n, dtype=torch.int64, device="cuda")
-            with torch.cuda.stream(streams[k]):
+            with torch.cuda.stream(streams[k]):  # the zero fill is ordered before the launch on its stream
+                rec = torch.empty(n * 16, dtype=torch.uint8, device="cuda")
+                err = torch.zeros(2 * n, dtype=torch.int32, device="cuda")
+                fl = torch.empty(3 * n, dtype=torch.int64, device="cuda")
                 gpu_ctx.decode_device(parsers[k], d, o, c, rec, err, fl, stream=streams[k])
             outs.append((k, rec, err, fl))
     torch.cuda.synchronize()
@@ -59,3 +59,67 @@ def test_alternating_parsers_on_two_streams(gpu_ctx):
         e = (got["status"] & 0x7F) != 0
         assert np.array_equal(err.cpu().numpy().view(np.uint32).reshape(n, 2)[e],
                               np.tile(ref["err_args"].reshape(n1, 2), (reps, 1))[e]), k
+
+
+def test_slot_eviction_across_three_streams(gpu_ctx):
+    """More parsers than the context keeps table copies (10 > kTabSlots = 8,
+    gpk_host.cpp), each with its own port / EtherType overrides, cycled over
+    three HIP streams on 8 M-packet batches with no synchronisation between
+    the calls: every launch takes a least-recently-used slot whose previous
+    readers may still be running on another stream. The rewrite is ordered on
+    the device, and each launch must match its own
+    parser's oracle bit for bit (ports.go:99-104, doc.go:211-228)."""
+    import torch
+    from gopacket_amd import _lib
+    g = pktutil.golden()
+    base = [bytes.fromhex(v["hex"]) for k, v in sorted(g.items()) if "hex" in v]
+    base += pktutil.read_pcap(pktutil.GOLDEN + "/test_ethernet.pcap")[1]
+    base += pktutil.read_pcap(pktutil.GOLDEN + "/test_dns.pcap")[1]
+    base += pktutil.fuzz_packets(91, 3000)
+    reps = (8 << 20) // len(base) + 1
+    n1 = len(base)
+    data1, off1, cap1 = pktutil.pack(base)
+    span = int(off1[-1]) + int(cap1[-1])
+    n = n1 * reps
+    data = np.zeros(span * reps + 64, np.uint8)
+    for r in range(reps):
+        data[r * span:(r + 1) * span] = data1[:span]
+    off = (np.tile(off1.astype(np.uint64), reps) + np.repeat(np.arange(reps, dtype=np.uint64) * span, n1))
+    cap = np.tile(cap1, reps)
+    cfgs = []
+    for i in range(10):
+        cfgs.append(dict(first=17, decoders=["ETHERNET", "DOT1Q", "IPV4", "IPV6", "TCP", "UDP", "PAYLOAD"],
+                         ethertype={0x88b5 + i: 20}, tcp_port={80: 1200 + i, 1024 + 7 * i: 2},
+                         udp_port={53: 2 if i % 2 else 1300 + i, 5353: 1400 + i},
+                         ipprotocol={(200 + i) & 255: 44}))
+    refs = [oracle_parser(cf).decode(data1, off1, cap1, nthreads=8) for cf in cfgs]
+    for i in range(1, 10):
+        assert not np.array_equal(refs[0]["err_args"], refs[i]["err_args"]), i
+    parsers = [device_parser(cf) for cf in cfgs]
+    d = torch.from_numpy(data).cuda()
+    o = torch.from_numpy(off.astype(np.int64)).cuda()
+    c = torch.from_numpy(cap.astype(np.int32)).cuda()
+    streams = [torch.cuda.Stream() for _ in range(3)]
+    outs = []
+    torch.cuda.synchronize()
+    k = 0
+    for it in range(2):
+        for i in range(10):
+            st = streams[k % 3]
+            k += 1
+            with torch.cuda.stream(st):  # the zero fill is ordered before the launch on its stream
+                rec = torch.empty(n * 16, dtype=torch.uint8, device="cuda")
+                err = torch.zeros(2 * n, dtype=torch.int32, device="cuda")
+                fl = torch.empty(3 * n, dtype=torch.int64, device="cuda")
+                gpu_ctx.decode_device(parsers[i], d, o, c, rec, err, fl, stream=st)
+            outs.append((i, rec, err, fl))
+    torch.cuda.synchronize()
+    for i, rec, err, fl in outs:
+        ref = refs[i]
+        got = rec.cpu().numpy().view(_lib.RECORD_DTYPE)
+        assert np.array_equal(got, np.tile(ref["records"], reps)), i
+        rf = ref["flows"].reshape(3, n1)
+        assert np.array_equal(fl.cpu().numpy().view(np.uint64).reshape(3, n), np.tile(rf, (1, reps))), i
+        e = (got["status"] & 0x7F) != 0
+        assert np.array_equal(err.cpu().numpy().view(np.uint32).reshape(n, 2)[e],
+                              np.tile(ref["err_args"].reshape(n1, 2), (reps, 1))[e]), i
