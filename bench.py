@@ -58,16 +58,18 @@ CONFIGS["c4s"] = dict(CONFIGS["c4"], strong=True,
                       workload="C4 strong: one 64M IMIX batch sharded over the ranks (byte-balanced cuts)")
 
 
-def dist_init(backend="nccl", same_device=False):
+def dist_init(backend="nccl", same_device=False, force=False):
     """One process per GPU (torchrun env). backend "nccl" is RCCL on ROCm;
-    "gloo" + same_device=True rehearses N ranks on one GPU (tests only)."""
+    "gloo" + same_device=True rehearses N ranks on one GPU (tests only).
+    force=True initialises the process group at world size 1 too, so the
+    barrier and the max-over-ranks run through the backend (tests only)."""
     import torch
     import torch.distributed as dist
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = 0 if same_device else int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
-    if world > 1:
+    if world > 1 or force:
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
@@ -78,7 +80,7 @@ def dist_init(backend="nccl", same_device=False):
 def barrier(world):
     import torch
     import torch.distributed as dist
-    if world > 1:
+    if world > 1 or dist.is_initialized():
         dist.barrier()
     torch.cuda.synchronize()
 
@@ -457,6 +459,36 @@ def c5_cpu(path, threads, nbytes=256 << 20):
     return out
 
 
+def htod_probe(total_bytes, slot_bytes=256 << 20, streams=4, reps=2):
+    """The host link's rate for C5's copy pattern, in the same run: pinned
+    slots of the replay's size -> device, one stream per slot, `streams`
+    copies in flight, `total_bytes` per round (the file's size); GB/s of the
+    best round, and the same with a single stream."""
+    import torch
+    hosts = [torch.ones(slot_bytes, dtype=torch.uint8).pin_memory() for _ in range(streams)]
+    devs = [torch.empty(slot_bytes, dtype=torch.uint8, device="cuda") for _ in range(streams)]
+    sts = [torch.cuda.Stream() for _ in range(streams)]
+    nslots = max(1, int(total_bytes // slot_bytes))
+
+    def run(k_streams):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(nslots):
+            k = i % k_streams
+            with torch.cuda.stream(sts[k]):
+                devs[k].copy_(hosts[k], non_blocking=True)
+        torch.cuda.synchronize()
+        return nslots * slot_bytes / (time.perf_counter() - t0) / 1e9
+
+    run(streams)  # warm
+    multi = max(run(streams) for _ in range(reps))
+    single = max(run(1) for _ in range(reps))
+    del hosts, devs
+    return dict(htod_probe_GBps=round(multi, 2), htod_probe_1stream_GBps=round(single, 2),
+                htod_pattern="%d x %d MiB pinned slots, %d streams, %.1f GB per round" % (
+                    streams, slot_bytes >> 20, streams, nslots * slot_bytes / 1e9))
+
+
 def c5_replay(ctx, gib=10.0, reps=2, threads=16, cpu_threads=16):
     """BASELINE config C5: a pcapng of the C4 IMIX mix (~gib GiB, written once
     to $TMPDIR, in the page cache) replayed end to end by gpk_replay_file:
@@ -499,6 +531,7 @@ def c5_replay(ctx, gib=10.0, reps=2, threads=16, cpu_threads=16):
         cpu = c5_cpu(path, cpu_threads)
     finally:
         os.unlink(path)
+    probe = htod_probe(size)
     st = min(runs, key=lambda x: x["wall_s"])
     idx = sorted(picked)
     pk = [synth.packet(4, i) for i in idx]
@@ -523,6 +556,8 @@ def c5_replay(ctx, gib=10.0, reps=2, threads=16, cpu_threads=16):
                                  gpu_copy_decode=round(st["gpu_s"], 4), kernel=round(st["kernel_s"], 4),
                                  deliver=round(st["deliver_s"], 4)),
                 batches=st["batches"], slots=st["slots"], l4_valid=valid[0], write_s=round(gen_s, 2),
+                kernel=st["kernel"], **probe,
+                frac_of_htod_probe=round(st["file_bytes"] / w / 1e9 / probe["htod_probe_GBps"], 4),
                 parity="%s (%d sampled packets vs oracle)" % ("bit-exact" if ok else "MISMATCH", len(idx)),
                 source="page-cached file in %s" % os.path.dirname(path), cpu_baseline=cpu)
 
@@ -797,10 +832,13 @@ def main():
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL (one rank per GPU); gloo + --same-device rehearses ranks on one GPU")
     ap.add_argument("--same-device", action="store_true", help="every rank on cuda:0 (rehearsal only)")
+    ap.add_argument("--force-dist", action="store_true",
+                    help="initialise the process group at world size 1 too (barrier / max over ranks through it)")
     args = ap.parse_args()
 
     import torch
-    rank, world, local = dist_init(args.dist_backend, args.same_device)
+    import torch.distributed as dist
+    rank, world, local = dist_init(args.dist_backend, args.same_device, args.force_dist)
     from gopacket_amd import engine
     ctx = engine.Context(local)
     if args.tables == "global":
@@ -838,6 +876,7 @@ def main():
                          "probe_read_GBps": r["probe_gbs"] and round(r["probe_gbs"], 1)},
             "parity": r["parity"],
             "full_parity": r["full_parity"],
+            "dist_backend": dist.get_backend() if dist.is_initialized() else None,
             "configs": {},
         }
         for name in names[1:]:
@@ -870,8 +909,7 @@ def main():
         else:
             out["cpu_baseline"] = None
         print(json.dumps(out))
-    if world > 1:
-        import torch.distributed as dist
+    if dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()
 

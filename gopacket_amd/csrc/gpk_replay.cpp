@@ -103,6 +103,12 @@ struct Src {  // the capture byte stream: plain file (parallel pread) or gzip (z
   }
 };
 
+struct Fill {      // one read of a slot's fresh bytes
+  uint64_t bytes;  // read
+  bool end;        // the stream ended with this read
+  double t0, t1;   // read start / end (GPK_REPLAY_TRACE=2)
+};
+
 struct Slot {
   uint8_t* host = nullptr;  // [carry region | fresh bytes | 16 B slack], pinned
   uint8_t* dev = nullptr;
@@ -117,7 +123,7 @@ struct Slot {
   hipEvent_t h2d = nullptr;  // the slot's HtoD finished: host buffer reusable
   hipError_t h2d_err = hipSuccess;  // the read thread's HtoD of the fresh bytes (device walk)
   bool h2d_pending = false;
-  std::future<uint64_t> fill;  // async read of the fresh bytes
+  std::shared_future<struct Fill> fill;  // async read of the fresh bytes
   bool fill_pending = false;
 };
 
@@ -422,19 +428,41 @@ extern "C" int gpk_replay_file(gpk_ctx* ctx, const gpk_parser* parser, const cha
   // walk and decode; only the short carry is copied later.
   int dev = 0;
   (void)hipGetDevice(&dev);
+  // Reads run ahead of the walk by up to slots-1 slots (a slot is refilled
+  // once its carry has moved on and its last HtoD has landed); they are
+  // chained, so the stream is still read strictly in order, one read at a
+  // time, and each read's HtoD is issued as soon as it has finished.
+  std::shared_future<Fill> last_fill;
   auto start_fill = [&](Slot& s) {
     s.h2d_err = hipSuccess;
-    s.fill = std::async(std::launch::async, [&src, &s, C, R, stats, dev, dev_walk] {
+    std::shared_future<Fill> prev = last_fill;
+    s.fill = std::async(std::launch::async, [&src, &s, C, R, stats, dev, dev_walk, prev] {
+      if (prev.valid()) prev.wait();
       double t = now_s();
-      uint64_t k = src.read(s.host + C, R);
-      stats->read_s += now_s() - t;
+      const uint64_t k = src.read(s.host + C, R);
+      const bool end = src.at_end;
+      const double t1 = now_s();
+      stats->read_s += t1 - t;
       if (dev_walk && k) {
         (void)hipSetDevice(dev);
         s.h2d_err = hipMemcpyAsync(s.dev + C, s.host + C, k, hipMemcpyHostToDevice, s.stream);
       }
-      return k;
-    });
+      return Fill{k, end, t, t1};
+    }).share();
     s.fill_pending = true;
+    last_fill = s.fill;
+  };
+  uint64_t next_fill = 0;  // sequence number of the next slot to fill
+  auto fill_ahead = [&](uint64_t upto) {  // issue the fills of slots [next_fill, upto)
+    while (good && next_fill < upto) {
+      Slot& N = pl.slots[next_fill % pl.slots.size()];
+      if (N.h2d_pending) {  // the slot's last HtoD read the host bytes about to be overwritten
+        good = pl.ok(hipEventSynchronize(N.h2d), "hipEventSynchronize");
+        N.h2d_pending = false;
+      }
+      if (good) start_fill(N);
+      next_fill++;
+    }
   };
 
   const double t_loop = now_s();
@@ -444,12 +472,15 @@ extern "C" int gpk_replay_file(gpk_ctx* ctx, const gpk_parser* parser, const cha
   uint64_t carry_len = 0, packet_index = 0;
   bool finished = false;
   rc = GPK_OK;
-  start_fill(pl.slots[0]);
+  fill_ahead(1);
   for (uint64_t si = 0; !finished && good; si++) {
     Slot& S = pl.slots[si % pl.slots.size()];
-    const uint64_t fresh = S.fill.get();  // reads are strictly sequential: one fill at a time
+    const double t_get = now_s();
+    const Fill fl = S.fill.get();
+    const double t_got = now_s();
     S.fill_pending = false;
-    const bool eof = src.at_end;
+    const uint64_t fresh = fl.bytes;
+    const bool eof = fl.end;
     if (carry_len > C) {  // a record longer than the carry region: not supported
       snprintf(stats->error, sizeof(stats->error), "capture record larger than the %llu-byte staging slot",
                (unsigned long long)C);
@@ -459,15 +490,9 @@ extern "C" int gpk_replay_file(gpk_ctx* ctx, const gpk_parser* parser, const cha
     const uint64_t start = C - carry_len, len = carry_len + fresh;
     if (carry_len) memmove(S.host + start, carry, carry_len);
     stats->stream_bytes += fresh;
-    // prefetch the next slot once its previous HtoD is done
-    Slot& N = pl.slots[(si + 1) % pl.slots.size()];
-    if (!eof) {
-      if (N.h2d_pending) {
-        good = pl.ok(hipEventSynchronize(N.h2d), "hipEventSynchronize");
-        N.h2d_pending = false;
-      }
-      if (good) start_fill(N);
-    }
+    // read ahead into every slot whose carry has moved on (the one just
+    // taken from slot si - 1 included)
+    if (!eof) fill_ahead(si + pl.slots.size());
     // walk the records of [start, start+len): on the device once the reader
     // is open (gpk_walk.h), the rest (and everything before) on the host
     // (parallel, gpk_capreader_index_all)
@@ -545,6 +570,7 @@ extern "C" int gpk_replay_file(gpk_ctx* ctx, const gpk_parser* parser, const cha
       st = gpk_capreader_index_all(rd, S.host + start, len, eof ? 1 : 0, walk_threads, &xi, &used);
     }
     stats->index_s += now_s() - t_ix;
+    const double t_walked = now_s();
     if (st < 0) {
       rc = st;
       finished = true;
@@ -633,6 +659,10 @@ extern "C" int gpk_replay_file(gpk_ctx* ctx, const gpk_parser* parser, const cha
       finished = true;
     }
     stats->slots++;
+    if (trace && trace[0] == '2')
+      fprintf(stderr, "gpk_replay slot %llu: read %.2f-%.2f ms, got %.2f (waited %.2f), walked %.2f, launched %.2f\n",
+              (unsigned long long)si, (fl.t0 - t_loop) * 1e3, (fl.t1 - t_loop) * 1e3, (t_got - t_loop) * 1e3,
+              (t_got - t_get) * 1e3, (t_walked - t_loop) * 1e3, (now_s() - t_loop) * 1e3);
     carry = S.host + pos;
     carry_len = start + len - pos;
     if (eof && !finished) {  // cannot happen: at the end of the stream the walker ends with an error

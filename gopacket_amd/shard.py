@@ -35,11 +35,12 @@ def byte_balanced_bounds(caplens, world):
 
 
 def max_over_ranks(x, world, device=None):
-    """Job time = the slowest rank's time (bench.py contract)."""
-    if world == 1:
-        return x
+    """Job time = the slowest rank's time (bench.py contract). At world size 1
+    without a process group it is x itself."""
     import torch
     import torch.distributed as dist
+    if world == 1 and not dist.is_initialized():
+        return x
     if dist.get_backend() == "gloo":
         device = None  # gloo reduces host tensors
     t = torch.tensor([float(x)], dtype=torch.float64, device=device)

@@ -117,3 +117,22 @@ def test_bench_two_ranks_strong_and_weak():
     assert c["scaling"] == "strong" and c["total_packets"] == 1 << 20
     assert c["parity"].startswith("bit-exact") and 1.0 <= c["byte_balance"] < 1.001
     assert r["roofline"]["kernel"].startswith("gpk::decode_kernel<true,false,true,false,")
+
+
+def test_bench_rccl_world_one():
+    """bench.py's RCCL branch on a one-GPU box: torchrun with one rank and
+    --force-dist, so init_process_group("nccl", device_id=...), the barriers
+    and the max over ranks run through RCCL. Multi-GPU
+    scaling itself stays unmeasured here (one GPU per box)."""
+    env = dict(os.environ, OMP_NUM_THREADS="4")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1", "--master-addr",
+           "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "1", "--force-dist",
+           "--configs", "c3,c2", "--packets", str(1 << 20), "--steps", "3", "--warmup", "1",
+           "--no-cpu-baseline", "--c5", "0", "--no-probe", "--no-full-parity"]
+    out = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=280)
+    assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-3000:]
+    line = [x for x in out.stdout.splitlines() if x.startswith("{")][-1]
+    r = json.loads(line)
+    assert r["dist_backend"] == "nccl"
+    assert r["n_gpus"] == 1 and r["steps"] == 3 and r["scaling"] == "weak" and r["value"] > 0
+    assert r["parity"].startswith("bit-exact") and r["configs"]["c2"]["parity"].startswith("bit-exact")
