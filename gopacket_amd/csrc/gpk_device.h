@@ -68,7 +68,6 @@ struct KParams {
   int32_t key_kind;
   uint32_t small_headers;   // no Dot1Q / IPv6 / IPv6-extension / TCP decoder: a 4-chunk window suffices
   uint32_t mid_headers;     // no IPv6 / IPv6-extension decoder: the small-packet kernel's 5-chunk window suffices
-  uint32_t tagless_headers; // ... and no Dot1Q decoder either: the 16-byte-aligned 5-chunk window suffices
   uint32_t big_packets;     // batch bytes / packets >= 1 KiB: launch choice only (occupancy)
   uint32_t* keys;
   uint64_t* khash;

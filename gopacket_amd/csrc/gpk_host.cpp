@@ -490,14 +490,10 @@ static int upload(gpk_ctx* c, const gpk_parser* p, gpk::KParams& P, int* slot, h
   // headers that fit the 5-chunk dword-aligned window (>= 77 bytes): no IPv6 decoder (Ethernet + two tags +
   // IPv4 + TCP with timestamps is 74 bytes)
   P.mid_headers = 1;
-  // headers that fit the 16-byte-aligned 5-chunk window (>= 65 bytes): no tags and no IPv6 either (Ethernet +
-  // IPv4 + TCP + the first option word is 58 bytes)
-  P.tagless_headers = 1;
   for (int t2 = 0; t2 < GPK_MAX_LAYER_TYPE; t2++) {
     const int kd = p->tab.dispatch[t2];
     if (kd == GPK_DEC_DOT1Q || kd == GPK_DEC_IPV6 || kd == GPK_DEC_IPV6_EXT || kd == GPK_DEC_TCP) P.small_headers = 0;
     if (kd == GPK_DEC_IPV6 || kd == GPK_DEC_IPV6_EXT) P.mid_headers = 0;
-    if (kd == GPK_DEC_IPV6 || kd == GPK_DEC_IPV6_EXT || kd == GPK_DEC_DOT1Q) P.tagless_headers = 0;
   }
   return GPK_OK;
 }
@@ -545,7 +541,6 @@ static int make_params(gpk_ctx* c, const gpk_parser* p, const gpk_batch* b, cons
   P.key_kind = 0;
   P.small_headers = 0;
   P.mid_headers = 0;
-  P.tagless_headers = 0;
   P.keys = nullptr;
   P.khash = nullptr;
   P.kcode = nullptr;

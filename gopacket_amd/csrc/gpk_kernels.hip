@@ -52,9 +52,6 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 #ifndef GPK_MID_W5
 #define GPK_MID_W5 1  // small-packet kernels of parsers without IPv6: dword-aligned 5-chunk window
 #endif
-#ifndef GPK_MID_A16
-#define GPK_MID_A16 0  // ... 16-byte-aligned (W = 5, AL = 16) for parsers with no Dot1Q / IPv6 decoder
-#endif
 #ifndef GPK_MID_IP6
 #define GPK_MID_IP6 0  // ... for parsers with IPv6 too
 #endif
@@ -1307,13 +1304,7 @@ Sel select(const gpk::KParams* P, int with_l4, int with_layout) {
     s.W = 4;
   } else if (!s.layout && !P->big_packets) {
     s.O = GPK_SMALL_WAVES;
-    if (GPK_MID_W5 && GPK_MID_A16 && P->tagless_headers) {
-      // no Dot1Q or IPv6 decoder: Ethernet + IPv4 + TCP + the first option
-      // word (58 bytes) fit the 16-byte-aligned 5-chunk window (>= 65 bytes),
-      // which keeps 7 blocks per CU without the dword-aligned loads' extra
-      // L2 misses (profiles/r10_c1_pmc.json)
-      s.W = 5;
-    } else if (GPK_MID_W5 && (P->mid_headers || GPK_MID_IP6) && P->data_end) {  // a dword-aligned 5-chunk window: 7 blocks per CU (LDS)
+    if (GPK_MID_W5 && (P->mid_headers || GPK_MID_IP6) && P->data_end) {  // a dword-aligned 5-chunk window: 7 blocks per CU (LDS)
       s.W = 5;
       s.AL = 4;
     }
@@ -1335,12 +1326,10 @@ hipError_t launch_sel(const gpk::KParams* P, const Sel& s, hipStream_t stream, i
   if (s.l4)
     return s.O == GPK_WAVES_PER_EU ? launch<true, false, kCompact>(P, stream, occ)
            : s.AL == 4             ? launch<true, false, kCompact, false, 5, GPK_SMALL_WAVES, 4>(P, stream, occ)
-           : s.W == 5              ? launch<true, false, kCompact, false, 5, GPK_SMALL_WAVES, 16>(P, stream, occ)
                                    : launch<true, false, kCompact, false, W, GPK_SMALL_WAVES>(P, stream, occ);
   if (s.layout) return launch<false, true, kCompact>(P, stream, occ);
   return s.O == GPK_WAVES_PER_EU ? launch<false, false, kCompact>(P, stream, occ)
          : s.AL == 4             ? launch<false, false, kCompact, false, 5, GPK_SMALL_WAVES, 4>(P, stream, occ)
-         : s.W == 5              ? launch<false, false, kCompact, false, 5, GPK_SMALL_WAVES, 16>(P, stream, occ)
                                  : launch<false, false, kCompact, false, W, GPK_SMALL_WAVES>(P, stream, occ);
 }
 
