@@ -73,7 +73,6 @@ struct KParams {
   uint64_t* khash;
   int32_t* kcode;
   uint64_t* diag;           // GPK_DIAG_TIMES builds only: 8 u64 per wave (gpk_diag_set_buffer)
-  uint32_t tiles_per_wave;  // persistent kernel: consecutive 64-packet tiles per wave (set at launch)
 };
 
 // Straight-line common-case parse (fast_parser below). Each bit says the

@@ -545,7 +545,6 @@ static int make_params(gpk_ctx* c, const gpk_parser* p, const gpk_batch* b, cons
   P.khash = nullptr;
   P.kcode = nullptr;
   P.diag = g_diag.load();
-  P.tiles_per_wave = 0;
   return GPK_OK;
 }
 

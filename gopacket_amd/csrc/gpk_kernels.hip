@@ -32,7 +32,6 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
-#include <cstdlib>
 
 #include "gpk_device.h"
 
@@ -86,17 +85,17 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 #ifndef GPK_DIAG_NOPARSE
 #define GPK_DIAG_NOPARSE 0  // timing only: skip DecodeLayers (fixed layout)
 #endif
-#ifndef GPK_PERSIST
-#define GPK_PERSIST 0  // persistent waves for the 6-chunk L4 kernels: next tile's windows by LDS-DMA during phase B
+#ifndef GPK_SF
+#define GPK_SF 0  // stream-first small-packet L4 kernel (decode_sf_kernel): header windows taken from phase B's stream
 #endif
-#ifndef GPK_PERS_TILES
-#define GPK_PERS_TILES 4  // ... consecutive tiles per wave (0: one resident grid, all tiles); env GPK_PERS_TILES overrides
+#ifndef GPK_SF_ALL
+#define GPK_SF_ALL 0  // ... also for the parsers that take the dword-aligned 5-chunk kernel (C1)
 #endif
-#ifndef GPK_PERS_DMA
-#define GPK_PERS_DMA 1  // ... 0 (diagnostic): each tile's windows loaded at its top through VGPRs, no prefetch
+#ifndef GPK_SF_DEPTH
+#define GPK_SF_DEPTH 4  // ... its stream depth (passes in flight)
 #endif
-#ifndef GPK_PERS_DO
-#define GPK_PERS_DO 7  // ... its phase-B depth as decode_packet's O (7: GPK_PB_DEPTH7 passes, 6: GPK_PB_DEPTH)
+#ifndef GPK_SF_WAVES
+#define GPK_SF_WAVES 6  // ... its register budget (waves per SIMD)
 #endif
 #ifndef GPK_DIAG_TIMES
 #define GPK_DIAG_TIMES 0  // diagnostic builds: per-wave phase timestamps into KParams.diag (tools/wave_times.py)
@@ -755,23 +754,12 @@ __device__ __forceinline__ uint32_t sparse_segment_sums(const KParams& P, bool j
   return own;
 }
 
-// What a caller runs once per wave between its last read of the LDS header
-// windows and phase B's stream (the persistent kernel issues the next tile's
-// window loads there), and where those loads must have landed (wait).
-struct NoHook {
-  __device__ __forceinline__ void operator()() const {}
-  __device__ __forceinline__ void wait() const {}
-  __device__ __forceinline__ void consume() const {}
-};
-
 // Word sums of every job lane's segment [s, e): the dense prefix stream (the
 // one started early, else one over the segments' region when that is
-// compact), else the per-segment stream. hook() runs once on every path,
-// after the head / tail chunks have been read and before the stream's loads.
-template <int D, int E, class Hook>
+// compact), else the per-segment stream.
+template <int D, int E>
 __device__ __forceinline__ uint32_t segment_sums(const KParams& P, Stream<D>& S, bool job, uint64_t s, uint64_t e,
-                                                 uint32_t lane, uint32_t hlds, uint32_t tlds, bool tafter,
-                                                 const Hook& hook) {
+                                                 uint32_t lane, uint32_t hlds, uint32_t tlds, bool tafter) {
   bool ta = false;
   // The early passes (E > 0: issued on every path) have landed during the
   // parse; waiting for them here (their registers as operands) puts any
@@ -779,13 +767,8 @@ __device__ __forceinline__ uint32_t segment_sums(const KParams& P, Stream<D>& S,
   // after the data is in.
   if (E > 0) stream_drain(S);
   if (E > 0 && S.on) {
-    if (!__ballot(job)) {  // nothing to sum
-      hook();
-      hook.wait();
-      return 0;
-    }
+    if (!__ballot(job)) return 0;  // nothing to sum
     const uint32_t L = dense_head_tail(P, S.R0, S.R, job, s, e, hlds, tlds, tafter, ta);
-    hook();  // landed by the stream's first waits (its loads are older than the stream's)
     stream_issue(P, S, S.R0, S.R, lane, E < D ? E : D, D);
     return dense_segment_sums<D>(P, S, job, s, e, lane, L, ta);
   }
@@ -795,25 +778,127 @@ __device__ __forceinline__ uint32_t segment_sums(const KParams& P, Stream<D>& S,
   uint32_t R;
   if (E == 0 && dense_region(job, s, e, R0, R)) {
     const uint32_t L = dense_head_tail(P, R0, R, job, s, e, hlds, tlds, tafter, ta);
-    hook();
     stream_issue(P, S, R0, R, lane, 0, D);
     return dense_segment_sums<D>(P, S, job, s, e, lane, L, ta);
   }
-  hook();
-  if (!__ballot(job)) {
-    hook.wait();
-    return 0;
+  if (!__ballot(job)) return 0;
+  return sparse_segment_sums(P, job, s, e, lane);
+}
+
+// ---- Stream-first (decode_sf_kernel) -------------------------------------
+// For waves of packed, ordered small packets the header windows are not
+// loaded on their own: phase B's coalesced stream runs first, over the
+// packets' extents, and every 16-byte granule that belongs to a packet's
+// header window is written from the stream into that packet's LDS slot on the
+// way (the window loads fetched those lines a second time: about a third of
+// C4's DRAM lines, profiles/r10_reread_*). The stream also captures, per lane,
+// the L-form prefix just before its packet's first granule and at its last
+// granule; after the parse the segment's sum is that packet sum minus the
+// bytes before s and after e, which lie in the window (or come from memory).
+//
+// Granule ownership: granules are numbered from the wave's region base R0;
+// packet q's window is granules [a_q, a_q + n_q). With packets in batch order,
+// not overlapping and at most one starting per granule (checked per wave, else
+// the wave runs the ordinary path), the packet owning granule g is the latest
+// one starting at or before it, and only the granule where a packet starts can
+// also end the previous packet's window. A per-wave LDS bitmap of start
+// granules (64 bits per pass) gives each lane its owner with one mbcnt.
+constexpr int kSfStride = 24;  // LDS dwords per lane: 6 whole chunks (16-byte aligned for ds_write_b128)
+constexpr int kSfBmDw = 72;    // start-bitmap dwords per wave: regions up to 36 KiB
+struct SfPkt {
+  uint32_t L;   // L-form sum of the packet's granules [a, b]
+  uint64_t R0;  // region base (batch offset, 16-byte aligned)
+  int32_t b;    // the packet's last granule (region-relative)
+  bool on;      // wave-uniform: the wave ran stream-first (else windows loaded, phase B after the parse)
+};
+
+// One pass of stream data (granule 64 p + lane) into the windows that hold it.
+__device__ __forceinline__ void sf_extract(const u32x4& v, uint32_t p, uint32_t lane, uint32_t bm, uint32_t slots,
+                                           uint32_t an, uint32_t& qs) {
+  const uint32_t* w = gpk_smem + (bm >> 2) + 2 * p;
+  const uint32_t mlo = w[0], mhi = w[1];  // start granules of this pass (wave-uniform words)
+  const uint32_t below = __builtin_amdgcn_mbcnt_hi(mhi, __builtin_amdgcn_mbcnt_lo(mlo, 0u));
+  const uint32_t here = (lane < 32 ? mlo >> lane : mhi >> (lane - 32)) & 1u;
+  const uint32_t g = 64u * p + lane;
+  const int32_t owner = (int32_t)(qs + below + here) - 1;
+  const uint32_t o1 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((uint32_t)owner << 2), (int)an);
+  const uint32_t o2 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((uint32_t)(owner - 1) << 2), (int)an);
+  const uint32_t c1 = g - (o1 & 0xffffffu), c2 = g - (o2 & 0xffffffu);
+  if (owner >= 0 && c1 < (o1 >> 24)) *reinterpret_cast<u32x4*>(reinterpret_cast<uint8_t*>(gpk_smem) + slots + 96u * (uint32_t)owner + 16u * c1) = v;
+  if (here && owner >= 1 && c2 < (o2 >> 24))
+    *reinterpret_cast<u32x4*>(reinterpret_cast<uint8_t*>(gpk_smem) + slots + 96u * (uint32_t)(owner - 1) + 16u * c2) = v;
+  qs += (uint32_t)__builtin_popcount(__builtin_amdgcn_readfirstlane(mlo)) +
+        (uint32_t)__builtin_popcount(__builtin_amdgcn_readfirstlane(mhi));
+}
+
+// The stream of a stream-first wave: region [R0, R0 + R), D passes in flight
+// (the dense stream's slots and waits), windows written on the way; returns
+// P(b) - P(a - 1) for the lane's packet (a - 1 = -1: none before it).
+template <int D>
+__device__ __forceinline__ uint32_t sf_stream(const KParams& P, Stream<D>& S, uint64_t R0, uint32_t R, uint32_t lane,
+                                              int32_t a1, int32_t b, uint32_t an, uint32_t bm, uint32_t slots) {
+  static_assert(kGran == 1, "one 16-byte granule per lane per pass");
+  stream_issue(P, S, R0, R, lane, 0, D);
+  const __amdgpu_buffer_rsrc_t rs = rsrc(P.data + R0, (R + 15) & ~15u);
+  const uint32_t np = (R + kPassBytes - 1) / kPassBytes;  // wave-uniform
+  const uint32_t vo = lane * kGranBytes;
+  Gran (&ring)[D] = S.ring;
+  const int32_t pa = a1 >> 6, pb = b >> 6;  // -1 never matches
+  const int32_t la = (a1 & 63) << 2, lb = (b & 63) << 2, ll = (int32_t)lane << 2;
+  uint32_t xa = 0, xb = 0, c = 0, qs = 0;
+  auto pass = [&](const int d, const int32_t p, const bool refill) __attribute__((always_inline)) {
+    const uint32_t gl = chunk_l(ring[d].c[0], 0u);
+    sf_extract(ring[d].c[0], (uint32_t)p, lane, bm, slots, an, qs);
+    if (refill) slot_load(ring[d].c, rs, vo, (uint32_t)(p + D) * kPassBytes);
+    const uint32_t sc = wave_scan(gl);
+    const uint32_t Pf = sc + c;
+    const bool ma = pa == p, mb = pb == p;
+    const uint32_t ya = (uint32_t)__builtin_amdgcn_ds_bpermute(ma ? la : ll, (int)Pf);
+    const uint32_t yb = (uint32_t)__builtin_amdgcn_ds_bpermute(mb ? lb : ll, (int)Pf);
+    xa = ma ? ya : xa;
+    xb = mb ? yb : xb;
+    c += readlane32(sc, 63);
+  };
+  // The first round runs on every path (passes past the region read
+  // range-checked zeros, add nothing and write no window chunk the parse
+  // reads): no edge bypasses the loop, so the slot registers the passes were
+  // issued into are the loop's own (a bypass made the allocator copy them
+  // while in flight: tools/check_stream_isa.py).
+  uint32_t p0 = 0;
+  do {
+#pragma unroll
+    for (int d = 0; d < D; d++) {
+      slot_wait<(D - 1) * kGran>(ring[d].c);
+      pass(d, (int32_t)(p0 + d), true);
+    }
+    p0 += D;
+  } while (p0 + D <= np);
+#pragma unroll
+  for (int d = 0; d < D - 1; d++) {
+    if (p0 + d >= np) break;
+    slot_wait_n(ring[d].c, D - 1 - d);
+    pass(d, (int32_t)(p0 + d), false);
   }
-  const uint32_t r = sparse_segment_sums(P, job, s, e, lane);
-  hook.wait();
-  return r;
+  stream_drain(S);
+  return xb - xa;
+}
+
+// 16 bytes of the batch at granule address ga (16-byte aligned) for a
+// stream-first lane: its own window chunk, the next packet's first chunk, or
+// memory.
+__device__ __forceinline__ u32x4 sf_chunk(const KParams& P, uint64_t ga, uint64_t wb, uint32_t nch, uint32_t slot_dw,
+                                          bool next_here, uint64_t nwb) {
+  const uint64_t k = (ga - wb) >> 4;
+  if (ga >= wb && k < nch) return lds_chunk(slot_dw * 4 + 16u * (uint32_t)k);
+  if (next_here && ga == nwb) return lds_chunk((slot_dw + kSfStride) * 4);
+  return *reinterpret_cast<const u32x4*>(P.data + ga);
 }
 
 template <bool kL4, bool kLayout, class TT, bool kKeys, int W, int O, int AL, int kSlotStride = W * 4 + 1,
-          int kEarly = -1, class Hook = NoHook>
+          int kEarly = -1, bool kSF = false>
 __device__ __forceinline__ void decode_packet(const KParams& P, const TT& T, uint64_t i, bool active, uint64_t off,
                                               uint32_t cl, const WinGeo& g, uint32_t slot_dw, uint32_t lane,
-                                              uint64_t* dt, const Hook& hook = Hook()) {
+                                              uint64_t* dt, const SfPkt sf = SfPkt{0, 0, -1, false}) {
   const uint32_t m = g.m, win = g.win;
   Rd r{P.data + off, slot_dw * 4 + m, win};
 
@@ -851,7 +936,6 @@ __device__ __forceinline__ void decode_packet(const KParams& P, const TT& T, uin
   if (active && P.fast) done = fast_parser(P, T, r, cl, q, s);
   if (active && !done) s = run_parser<false>(P, T, r, cl, q);
 #endif
-  hook.consume();
 
   uint32_t st = (s.err & GPK_ST_ERR_MASK) | (s.trunc ? GPK_ST_TRUNCATED : 0u) |
                 ((q.nlayers > GPK_ST_NLAYERS_MASK ? GPK_ST_NLAYERS_MASK : q.nlayers) << GPK_ST_NLAYERS_SHIFT);
@@ -957,7 +1041,33 @@ __device__ __forceinline__ void decode_packet(const KParams& P, const TT& T, uin
 #if GPK_DIAG_TIMES
   dt[3] = __builtin_amdgcn_s_memrealtime();
 #endif
-  if (kL4) {
+  if (kL4 && kSF && sf.on) {
+    // stream-first: the packet's granule sum minus the bytes of its granules
+    // before s (header bytes, in the window) and from e on (padding and the
+    // next packet's first bytes)
+    const uint32_t nch = active ? (m + win + 15) >> 4 : 0u;
+    const uint32_t nwb_lo = (uint32_t)__shfl_down((int)(uint32_t)g.wb, 1);
+    const uint32_t nwb_hi = (uint32_t)__shfl_down((int)(uint32_t)(g.wb >> 32), 1);
+    const uint32_t nnch = (uint32_t)__shfl_down((int)nch, 1);
+    const uint64_t nwb = (uint64_t)nwb_hi << 32 | nwb_lo;
+    const bool next_here = lane < 63 && nnch != 0;
+    uint32_t L = sf.L;
+    if (job) {
+      const uint32_t hl = (uint32_t)(js - g.wb);
+      for (uint32_t k = 0; k < (hl >> 4); k++) L -= chunk_l(sf_chunk(P, g.wb + 16u * k, g.wb, nch, slot_dw, next_here, nwb), 0u);
+      L -= chunk_l_below(sf_chunk(P, g.wb + (hl & ~15u), g.wb, nch, slot_dw, next_here, nwb), hl & 15u, 0u);
+      const uint64_t gend = sf.R0 + 16ull * (uint64_t)(sf.b + 1), gj = je & ~15ull;
+      for (uint64_t ga = gj; ga < gend; ga += 16) L -= chunk_l(sf_chunk(P, ga, g.wb, nch, slot_dw, next_here, nwb), 0u);
+      if (gj < gend) L += chunk_l_below(sf_chunk(P, gj, g.wb, nch, slot_dw, next_here, nwb), (uint32_t)(je & 15), 0u);
+      const uint32_t sum = l_to_words(L, (uint32_t)js & 1u);
+      l4c = fold(jinit + sum - jexist);
+      const bool udp = (st & GPK_ST_L4_UDP) != 0;
+      if (l4c == jexist || (udp && jexist == 0)) st |= GPK_ST_L4_VALID;
+    }
+#if GPK_DIAG_TIMES
+    dt[4] = __builtin_amdgcn_s_memrealtime();
+#endif
+  } else if (kL4) {
     // the segment's first and last chunk in an LDS header window: its own,
     // or (the segment ending where the next packet starts) the next lane's
     const uint32_t nch = active ? (m + win + 15) >> 4 : 0u;
@@ -992,7 +1102,7 @@ __device__ __forceinline__ void decode_packet(const KParams& P, const TT& T, uin
         tafter = true;
       }
     }
-    const uint32_t sum = segment_sums<D, E>(P, S, job, js, je, lane, hlds, tlds, tafter, hook);
+    const uint32_t sum = segment_sums<D, E>(P, S, job, js, je, lane, hlds, tlds, tafter);
 #if GPK_DIAG_TIMES
     dt[4] = __builtin_amdgcn_s_memrealtime();
     dt[7] = (uint64_t)(S.on ? S.R : 0u) | (uint64_t)__popcll(__ballot(job)) << 32;
@@ -1002,9 +1112,6 @@ __device__ __forceinline__ void decode_packet(const KParams& P, const TT& T, uin
       const bool udp = (st & GPK_ST_L4_UDP) != 0;
       if (l4c == jexist || (udp && jexist == 0)) st |= GPK_ST_L4_VALID;
     }
-  } else {
-    hook();
-    hook.wait();
   }
   if (active)  // written once, never read back here: non-temporal
     __builtin_nontemporal_store(u32x4{lay_lo, lay_hi, st, ip4c | (l4c << 16)}, reinterpret_cast<u32x4*>(P.records) + i);
@@ -1080,145 +1187,108 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W == 4 ?
 #endif
 }
 
-// ---- persistent waves ------------------------------------------------------
-// A wave decodes 64-packet tiles t, t + S, t + 2S, ... (S = the waves of the
-// grid, which is sized to be resident at once, so the tiles active across the
-// chip stay one contiguous window of the batch). No wave ends between tiles:
-// the per-wave start-up of the one-tile kernel (dispatch, index round trip,
-// header-window round trip, the block's LDS held until its last wave ends;
-// tools/wave_times.py) is paid once. The next tile's index is loaded at the
-// top of each tile and its header windows go straight into this wave's LDS
-// slots by LDS-DMA (no VGPRs) once phase B no longer reads them, so they land
-// while the current tile's segments stream.
-
-// 16 bytes per lane into LDS: lane l's bytes land at LDS byte `lds` + 16 l
-// (wave-uniform destination, per-lane source; tools/probes/lds_dma.hip).
-__device__ __forceinline__ void dma16(uint64_t src, uint32_t lds) {
-  uint32_t keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep)
-               : "v"(src), "s"(lds)
-               : "memory");
-}
-
-// The W-chunk header windows of a tile's 64 packets into the wave's slots
-// (slot q at byte 16 W q of `region`, no padding dword: one LDS-DMA
-// instruction writes 1 KiB contiguously). Instruction k's lane l carries
-// cell 64 k + l = chunk c of packet q (q = cell / W), so every lane fetches
-// packet q's window base and chunk count from lane q (ds_bpermute). Chunks
-// past a packet's window re-read its last chunk, a packet with none the
-// parser's table copy, as load_window does.
-template <int W>
-struct WinDma {
-  const uint8_t* data;
-  const void* tab;
-  Idx x;         // the next tile's index entry of this lane
-  bool active;   // ... is a packet of the batch
-  bool more;     // wave-uniform: there is a next tile
-  uint32_t region, lane;
-  __device__ __forceinline__ void operator()() const {
-    if (!more || !GPK_PERS_DMA) return;
-    const uint32_t m = (uint32_t)(x.off & 15), win = x.cl < 16u * W - m ? x.cl : 16u * W - m;
-    const uint32_t nch = active ? (m + win + 15) >> 4 : 0u;
-    const uint64_t src = nch ? (uint64_t)(uintptr_t)(data + (x.off - m)) : (uint64_t)(uintptr_t)tab;
-    const uint32_t last = nch ? nch - 1 : 0u;
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of the old windows are done
-#pragma unroll
-    for (int k = 0; k < W; k++) {
-      const uint32_t e = 64u * k + lane, q = e / W, c = e - q * W;
-      const int qa = (int)(q << 2);
-      const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute(qa, (int)(uint32_t)src);
-      const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute(qa, (int)(uint32_t)(src >> 32));
-      const uint32_t lq = (uint32_t)__builtin_amdgcn_ds_bpermute(qa, (int)last);
-      dma16(((uint64_t)hi << 32 | lo) + 16u * (c < lq ? c : lq), region + 1024u * k);
-    }
-  }
-  // the windows have landed (paths whose own waits do not cover them)
-  __device__ __forceinline__ void wait() const {
-    if (more && GPK_PERS_DMA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  // The next index is waited for here, on every path (after the parse: it was
-  // loaded at the top of the tile, and no store of this tile is in flight yet).
-  // Otherwise the copy into the loop's registers at the back edge waits for it
-  // with vmcnt(0), i.e. for this tile's record and flow stores too.
-  __device__ __forceinline__ void consume() const { asm volatile("" ::"v"(x.off), "v"(x.cl)); }
-};
-
-template <bool kL4, bool kCompact, int W, int O>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(O, 8))) void decode_pers_kernel(KParams Pv) {
-  const KParams& P0 = Pv;
-  constexpr int kStride = 4 * W;  // LDS dwords per lane
-  const uint32_t tid = threadIdx.x, lane0 = tid & 63;
+// Stream-first L4 kernel for batches of small packets (see sf_stream): W = 6
+// header windows, 16-byte aligned, 24-dword slots (6 blocks per CU with the
+// start bitmaps and the table blob). A wave whose packets are not packed and
+// ordered runs the ordinary path (windows loaded, then the parse, then phase B).
+template <bool kCompact, int O>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(O, 8))) void decode_sf_kernel(KParams P) {
+  // O: the register budget (6 blocks per CU by LDS: 80 VGPRs cost nothing); the
+  // phase-B depth and the fallback's specialisation are the 72-VGPR kernel's
+  constexpr int W = 6, OP = GPK_SMALL_WAVES;
+  constexpr int D = GPK_SF_DEPTH;
+  const uint32_t tid = threadIdx.x, lane = tid & 63;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const uint32_t base = kBlock * kStride;
-  if (kCompact) {  // the table blob, once per block
+  const uint32_t slot_dw = tid * kSfStride;
+  const uint32_t bm = (kBlock * kSfStride + wave * kSfBmDw) * 4;  // LDS byte address of this wave's bitmap
+  const uint32_t base = kBlock * kSfStride + kWaves * kSfBmDw;     // table blob (dwords)
+  if ((uint64_t)blockIdx.x * kBlock >= P.n) return;  // uniform over the block
+  const uint64_t i0 = (uint64_t)blockIdx.x * kBlock + tid;
+  const bool active = i0 < P.n;
+  uint64_t dt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#if GPK_DIAG_TIMES
+  dt[0] = __builtin_amdgcn_s_memrealtime();
+#endif
+  const Idx c0 = load_index(P, i0);
+  const WinGeo g0 = win_geo<W, 16>(P, c0, active);
+  if (kCompact) {
     static_assert(kCtDwords <= 3 * kBlock, "three blob words per thread");
-    const uint32_t last = P0.cg.words - 1;
+    const uint32_t last = P.cg.words - 1;
 #pragma unroll
     for (uint32_t k = 0; k < 3; k++) {
       const uint32_t j = tid + k * kBlock < last ? tid + k * kBlock : last;
-      gpk_smem[base + j] = P0.ctab[j];
+      gpk_smem[base + j] = P.ctab[j];
     }
     __syncthreads();
   }
-  // a wave decodes tiles [first, end): P.tiles_per_wave consecutive tiles
-  const uint64_t ntiles = (P0.n + 63) >> 6;
-  const uint64_t first = ((uint64_t)blockIdx.x * kWaves + wave) * P0.tiles_per_wave;
-  if (first >= ntiles) return;
-  const uint64_t end = first + P0.tiles_per_wave < ntiles ? first + P0.tiles_per_wave : ntiles;
-  uint64_t t = first;
-  const uint32_t region =
-      __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)gpk_smem + wave * (64u * kStride * 4u));
-  Idx cur = load_index(P0, t * 64 + lane0);
-  if (GPK_PERS_DMA) {
-    const WinDma<W> h{P0.data, P0.tab, cur, t * 64 + lane0 < P0.n, true, region, lane0};
-    h();
-    h.wait();
+#if GPK_DIAG_TIMES
+  dt[1] = dt[2] = __builtin_amdgcn_s_memrealtime();
+#endif
+  // the wave's plan: packed (dense_region over the packet extents), in order,
+  // not overlapping, one start per granule, and the bitmap large enough
+  uint64_t R0 = 0;
+  uint32_t R = 0;
+  bool ok = dense_region(active, c0.off, c0.off + c0.cl, R0, R);
+  {
+    const uint64_t end = c0.off + c0.cl;
+    const uint32_t pe_lo = (uint32_t)__shfl_up((int)(uint32_t)end, 1), pe_hi = (uint32_t)__shfl_up((int)(uint32_t)(end >> 32), 1);
+    const uint32_t pw_lo = (uint32_t)__shfl_up((int)(uint32_t)g0.wb, 1), pw_hi = (uint32_t)__shfl_up((int)(uint32_t)(g0.wb >> 32), 1);
+    const uint64_t pend = (uint64_t)pe_hi << 32 | pe_lo, pwb = (uint64_t)pw_hi << 32 | pw_lo;
+    const bool bad = active && lane > 0 && (c0.off < pend || g0.wb <= pwb);
+    ok = ok && !__ballot(bad) && R <= (uint32_t)kSfBmDw * 32u * 16u;
   }
-  for (;;) {
-    const KParams& P = Pv;
-    // lane-derived values re-formed per tile as well (hoisted, they are spilled)
-    uint32_t lane = lane0;
-    asm volatile("" : "+v"(lane));
-    const uint32_t slot_dw = (wave * 64u + lane) * kStride;
-    const uint64_t tn = t + 1;
-    const bool more = tn < end;
-    const uint64_t i = t * 64 + lane, in = (more ? tn : t) * 64 + lane;
-    uint64_t dt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint32_t L = 0;
+  int32_t b = -1;
+  if (ok) {
+    // start bitmap: granule a of every packet (region-relative)
+    const uint32_t a = active ? (uint32_t)((g0.wb - R0) >> 4) : 0xffffffu;
+    const uint32_t an = active ? (a | g0.nch << 24) : 0xffffffu;
+    const uint32_t np = (R + kPassBytes - 1) / kPassBytes;
+    uint32_t* bmw = gpk_smem + (bm >> 2);
+    const uint32_t nw = 2 * (np > (uint32_t)D ? np : (uint32_t)D);  // the first round's passes too
+    if (lane < nw) bmw[lane] = 0u;
+    if (lane + 64 < nw) bmw[lane + 64] = 0u;
+    if (active) __hip_atomic_fetch_or(bmw + (a >> 5), 1u << (a & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    const int32_t a1 = active ? (int32_t)a - 1 : -1;
+    b = active ? (int32_t)(((c0.off + c0.cl) - 1 - R0) >> 4) : -1;
+    Stream<D> S;
+    S.on = true;
+    L = sf_stream<D>(P, S, R0, R, lane, a1, b, an, bm, (wave * 64u * kSfStride) * 4u);
+  } else {
+    WinT<W> w;
+    load_window<W, 16>(P, g0, w);
+    store_window<W, 16>(slot_dw, w);
+  }
 #if GPK_DIAG_TIMES
-    dt[0] = dt[1] = dt[2] = __builtin_amdgcn_s_memrealtime();
+  dt[3] = __builtin_amdgcn_s_memrealtime();
 #endif
-    const Idx nxt = load_index(P, in);
-    const WinGeo g = win_geo<W, 16>(P, cur, i < P.n);
-    if (!GPK_PERS_DMA) {
-      WinT<W> w;
-      load_window<W, 16>(P, g, w);
-      store_window<W, 16>(slot_dw, w);
+  // Only the index entry crosses the stream: everything derived from it is
+  // formed again here (kept live, it was spilled around the stream).
+  uint32_t off_lo = (uint32_t)c0.off, off_hi = (uint32_t)(c0.off >> 32), ccl = c0.cl;
+  asm volatile("" : "+v"(off_lo), "+v"(off_hi), "+v"(ccl));
+  const Idx c1{(uint64_t)off_hi << 32 | off_lo, ccl};
+  const uint32_t tid1 = threadIdx.x;
+  const uint64_t i1 = (uint64_t)blockIdx.x * kBlock + tid1;
+  const WinGeo g1 = win_geo<W, 16>(P, c1, i1 < P.n);
+  if (kCompact)
+    decode_packet<true, false, LTab, false, W, OP, 16, kSfStride, 0, true>(P, LTab{P.cg, base}, i1, i1 < P.n, c1.off,
+                                                                          c1.cl, g1, tid1 * kSfStride, tid1 & 63, dt,
+                                                                          SfPkt{L, R0, b, ok});
+  else
+    decode_packet<true, false, GTab, false, W, OP, 16, kSfStride, 0, true>(P, GTab{P.tab}, i1, i1 < P.n, c1.off, c1.cl,
+                                                                          g1, tid1 * kSfStride, tid1 & 63, dt,
+                                                                          SfPkt{L, R0, b, ok});
 #if GPK_DIAG_TIMES
-      dt[2] = __builtin_amdgcn_s_memrealtime();
-#endif
-    }
-    const WinDma<W> h{P.data, P.tab, nxt, in < P.n, more, region, lane};
-    if (kCompact)
-      decode_packet<kL4, false, LTab, false, W, GPK_PERS_DO, 16, kStride, 0, WinDma<W>>(P, LTab{P.cg, base}, i, i < P.n, cur.off,
-                                                                             cur.cl, g, slot_dw, lane, dt, h);
-    else
-      decode_packet<kL4, false, GTab, false, W, GPK_PERS_DO, 16, kStride, 0, WinDma<W>>(P, GTab{P.tab}, i, i < P.n, cur.off,
-                                                                             cur.cl, g, slot_dw, lane, dt, h);
-#if GPK_DIAG_TIMES
-    dt[5] = __builtin_amdgcn_s_memrealtime();
-    dt[6] = (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 4) | (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32;
-    if (P.diag && lane < 8) {
-      uint64_t v = dt[0];
+  dt[5] = __builtin_amdgcn_s_memrealtime();
+  dt[6] = (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 4) | (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32;
+  dt[7] = ok ? (uint64_t)R | (uint64_t)__builtin_popcountll(__ballot(active)) << 32 : 0;  // the stream-first region
+  if (P.diag && lane < 8) {
+    uint64_t v = dt[0];
 #pragma unroll
-      for (int k = 1; k < 8; k++) v = lane == (uint32_t)k ? dt[k] : v;
-      P.diag[t * 8 + lane] = v;
-    }
-#endif
-    if (!more) break;
-    t = tn;
-    cur = nxt;
+    for (int k = 1; k < 8; k++) v = lane == (uint32_t)k ? dt[k] : v;
+    P.diag[((uint64_t)blockIdx.x * kWaves + wave) * 8 + lane] = v;
   }
+#endif
 }
 
 // Full decoded list of one packet (lists longer than the 16 inline codes).
@@ -1254,38 +1324,15 @@ hipError_t launch(const gpk::KParams* P, hipStream_t stream, int* occ) {
   return hipGetLastError();
 }
 
-// Persistent kernel: as many blocks as are resident at once (LDS, registers).
-template <bool kL4, bool kCompact, int W, int O>
-hipError_t launch_pers(const gpk::KParams* P, hipStream_t stream, int* occ) {
+template <bool kCompact>
+hipError_t launch_sf(const gpk::KParams* P, hipStream_t stream, int* occ) {
   using namespace gpk;
-  constexpr int slot_lds = kBlock * 4 * W * 4;
-  const int lds = kCompact ? slot_lds + (int)((P->cg.words + GPK_BLOB_ROUND - 1) & ~(GPK_BLOB_ROUND - 1u)) * 4 : slot_lds;
-  int per_cu = 0;
-  hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, decode_pers_kernel<kL4, kCompact, W, O>, kBlock, lds);
-  if (e != hipSuccess) return e;
-  if (occ) {
-    *occ = per_cu;
-    return hipSuccess;
-  }
-  int dev = 0, cus = 0;
-  if ((e = hipGetDevice(&dev)) != hipSuccess) return e;
-  if ((e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess) return e;
-  // tiles per wave: all of a wave's share when the grid is one resident wave of
-  // blocks (GPK_PERS_TILES=0), else that many consecutive tiles per wave with
-  // the hardware's dispatcher balancing the blocks
-  const uint64_t tiles = (P->n + 63) / 64;
-  const uint64_t resident = (uint64_t)(per_cu > 0 ? per_cu : 1) * (uint64_t)(cus > 0 ? cus : 1) * kWaves;
-  static const long env_t = [] {
-    const char* e = getenv("GPK_PERS_TILES");
-    return e ? strtol(e, nullptr, 10) : (long)GPK_PERS_TILES;
-  }();
-  uint64_t T = env_t > 0 ? (uint64_t)env_t : (tiles + resident - 1) / resident;
-  if (T < 1) T = 1;
-  KParams Q = *P;
-  Q.tiles_per_wave = (uint32_t)T;
-  const uint64_t grid = (tiles + T * kWaves - 1) / (T * kWaves);
+  constexpr int fixed = kBlock * kSfStride * 4 + kWaves * kSfBmDw * 4;
+  const int lds = kCompact ? fixed + (int)((P->cg.words + GPK_BLOB_ROUND - 1) & ~(GPK_BLOB_ROUND - 1u)) * 4 : fixed;
+  if (occ) return hipOccupancyMaxActiveBlocksPerMultiprocessor(occ, decode_sf_kernel<kCompact, GPK_SF_WAVES>, kBlock, lds);
+  const uint64_t grid = (P->n + kBlock - 1) / kBlock;
   if (grid > 0xffffffffull) return hipErrorInvalidValue;
-  hipLaunchKernelGGL((decode_pers_kernel<kL4, kCompact, W, O>), dim3((unsigned)grid), dim3(kBlock), lds, stream, Q);
+  hipLaunchKernelGGL((decode_sf_kernel<kCompact, GPK_SF_WAVES>), dim3((unsigned)grid), dim3(kBlock), lds, stream, *P);
   return hipGetLastError();
 }
 
@@ -1293,7 +1340,7 @@ hipError_t launch_pers(const gpk::KParams* P, hipStream_t stream, int* occ) {
 struct Sel {
   bool l4, layout, compact, keys;
   int W, O, AL;
-  bool pers;
+  bool sf;
 };
 Sel select(const gpk::KParams* P, int with_l4, int with_layout) {
   Sel s{with_l4 != 0, with_layout != 0, P->ctab != nullptr, P->key_kind != 0, gpk::kWinChunks, GPK_WAVES_PER_EU, 16,
@@ -1304,21 +1351,20 @@ Sel select(const gpk::KParams* P, int with_l4, int with_layout) {
     s.W = 4;
   } else if (!s.layout && !P->big_packets) {
     s.O = GPK_SMALL_WAVES;
-    if (GPK_MID_W5 && (P->mid_headers || GPK_MID_IP6) && P->data_end) {  // a dword-aligned 5-chunk window: 7 blocks per CU (LDS)
+    if (GPK_MID_W5 && !(GPK_SF && GPK_SF_ALL) && (P->mid_headers || GPK_MID_IP6) && P->data_end) {  // a dword-aligned 5-chunk window: 7 blocks per CU (LDS)
       s.W = 5;
       s.AL = 4;
     }
+    // stream-first: the small-packet L4 kernel with the 6-chunk window
+    s.sf = GPK_SF && s.l4 && s.W == gpk::kWinChunks && s.AL == 16;
   }
-  // persistent waves: the 6-chunk, 16-byte-aligned L4 kernels (C3, C4)
-  s.pers = GPK_PERSIST && s.l4 && !s.layout && !s.keys && s.W == gpk::kWinChunks && s.AL == 16;
-  if (s.pers) s.O = GPK_WAVES_PER_EU;  // 6 blocks per CU by LDS: the 80-VGPR budget costs no occupancy
   return s;
 }
 
 template <bool kCompact>
 hipError_t launch_sel(const gpk::KParams* P, const Sel& s, hipStream_t stream, int* occ) {
   constexpr int W = gpk::kWinChunks;
-  if (s.pers) return launch_pers<true, kCompact, W, GPK_WAVES_PER_EU>(P, stream, occ);
+  if (s.sf) return launch_sf<kCompact>(P, stream, occ);
   if (s.keys)
     return s.l4 ? launch<true, false, kCompact, true>(P, stream, occ) : launch<false, false, kCompact, true>(P, stream, occ);
   if (s.W == 4) return launch<false, false, kCompact, false, 4>(P, stream, occ);
@@ -1351,8 +1397,7 @@ extern "C" hipError_t gpk_launch_occupancy(const gpk::KParams* P, int with_l4, i
 // Name of the kernel specialisation gpk_launch_decode would launch.
 extern "C" int gpk_launch_describe(const gpk::KParams* P, int with_l4, int with_layout, char* buf, size_t cap) {
   const Sel s = select(P, with_l4, with_layout);
-  if (s.pers)
-    return snprintf(buf, cap, "gpk::decode_pers_kernel<true,%s,%d,%d>", s.compact ? "true" : "false", s.W, s.O);
+  if (s.sf) return snprintf(buf, cap, "gpk::decode_sf_kernel<%s,%d>", s.compact ? "true" : "false", s.O);
   return snprintf(buf, cap, "gpk::decode_kernel<%s,%s,%s,%s,%d,%d,%d>", s.l4 ? "true" : "false",
                   s.layout ? "true" : "false", s.compact ? "true" : "false", s.keys ? "true" : "false", s.W,
                   s.W == 4 ? 6 : s.O, s.AL);

@@ -210,6 +210,7 @@ struct Pipeline {
 };
 
 constexpr uint32_t kMaxSeg = 65536;  // device-walk segments per slot (>= 4 KiB each)
+constexpr uint64_t kOpenPrefix = 64 << 10;  // host-read bytes before the device walk when the reader is not open
 
 #define ALLOC_OK(call, what) \
   do {                       \
@@ -503,7 +504,7 @@ extern "C" int gpk_replay_file(gpk_ctx* ctx, const gpk_parser* parser, const cha
     const int walk_threads = std::min(64, 4 * opt.read_threads);
     gpk::WalkState ws;
     const bool dwalk = dev_walk;  // device index (S.d_*), slot layout mirrored on the device
-    const bool on_dev = dev_walk && gpk_capreader_walk_state(rd, &ws);  // ... and the walk runs there
+    bool on_dev = dev_walk && gpk_capreader_walk_state(rd, &ws);  // ... and the walk runs there
     // positions relative to the 16-byte-aligned base the kernels get
     const uint64_t base_off = start & ~15ull, p0 = start & 15, L = p0 + len;
     int st = GPK_CAP_MORE;
@@ -515,57 +516,125 @@ extern "C" int gpk_replay_file(gpk_ctx* ctx, const gpk_parser* parser, const cha
                      "HtoD carry");
       good = good && pl.ok(hipEventRecord(S.h2d, S.stream), "hipEventRecord");
       S.h2d_pending = true;
-      uint64_t pos = p0;
+      uint64_t pos = p0, dev_pk = 0, g_emit = 0;  // g_emit: index entries sized for the emit kernel
+      bool ended = false;  // a host stretch met the reader's end (GPK_CAP_END or an error): no further call
+      std::vector<std::pair<uint64_t, gpk_capindex>> chunks;  // host stretches: (first index, packets)
+      if (good && dev_walk && !on_dev && L - pos > kOpenPrefix) {
+        // the reader is not open yet (the file's first slot): the host reads
+        // the section header and interfaces, then the device walks the rest
+        gpk_capindex hx{};
+        uint64_t hu = 0;
+        st = gpk_capreader_index_all(rd, S.host + base_off + pos, kOpenPrefix, 0, walk_threads, &hx, &hu);
+        for (uint64_t i = 0; i < hx.n; i++) hx.offsets[i] += pos;
+        if (hx.n) chunks.push_back({G, hx});
+        else gpk_capindex_free(&hx);
+        G += hx.n;
+        pos += hu;
+        ended = st != GPK_CAP_MORE;
+        on_dev = !ended && gpk_capreader_walk_state(rd, &ws);
+      }
       if (good && on_dev) {
         const uint64_t seg = std::max<uint64_t>(4096, ((L + kMaxSeg - 1) / kMaxSeg + 3) & ~3ull);
         const uint32_t nseg = (uint32_t)((L + seg - 1) / seg);
-        good = pl.ok(gpk_walk_segments(S.dev + base_off, p0, L, seg, nseg, ws, S.d_seg, S.stream), "walk kernel") &&
+        good = pl.ok(gpk_walk_segments(S.dev + base_off, pos, L, seg, nseg, ws, S.d_seg, S.stream), "walk kernel") &&
                pl.ok(hipMemcpyAsync(S.h_seg.sync, S.d_seg.sync, nseg * 8ull, hipMemcpyDeviceToHost, S.stream),
                      "DtoH walk") &&
                pl.ok(hipMemcpyAsync(S.h_seg.end, S.d_seg.end, nseg * 8ull, hipMemcpyDeviceToHost, S.stream), "DtoH walk") &&
                pl.ok(hipMemcpyAsync(S.h_seg.count, S.d_seg.count, nseg * 4ull, hipMemcpyDeviceToHost, S.stream),
                      "DtoH walk") &&
                pl.ok(hipStreamSynchronize(S.stream), "hipStreamSynchronize");
-        // accept segments while each starts where the previous one's chain
-        // ended (segment 0 starts where the reader stands); stop after a
-        // chain that ended inside its segment (a block that is not plain)
-        bool go = good;
-        for (uint32_t k = 0; k < nseg; k++) {
-          const uint64_t s1 = std::min<uint64_t>(L, (uint64_t)(k + 1) * seg);
-          if (go && S.h_seg.sync[k] == pos) {
+        // Accept segments while each starts where the previous one's chain
+        // ended (segment 0 starts where the reader stands) and covers its
+        // segment. Where one does not, the exact reader walks on the host from
+        // there up to a later segment's chain start; if it lands on it exactly
+        // with its walk state unchanged (a real block boundary, read the way the
+        // device chain assumed), the device segments resume there. A fake
+        // chain inside a payload, or one block longer than a segment, costs a
+        // host walk of that stretch, not of the rest of the slot.
+        for (uint32_t q = 0; q < nseg; q++) S.h_seg.base[q] = ~0ull;
+        uint32_t k = (uint32_t)(pos / seg);  // the segment the reader stands in
+        while (good && k < nseg) {
+          while (k < nseg && S.h_seg.sync[k] == pos) {
+            const uint64_t s1 = std::min<uint64_t>(L, (uint64_t)(k + 1) * seg);
             S.h_seg.base[k] = G;
             G += S.h_seg.count[k];
+            dev_pk += S.h_seg.count[k];
             pos = S.h_seg.end[k];
-            go = pos >= s1;
-          } else {
-            S.h_seg.base[k] = ~0ull;
-            go = false;
+            k++;
+            if (pos < s1) break;  // a block that is not plain ended the chain
           }
+          uint32_t j = k;  // the next chain start past pos
+          while (j < nseg && (S.h_seg.sync[j] == ~0ull || S.h_seg.sync[j] <= pos)) j++;
+          if (j >= nseg) break;
+          gpk_capindex hx{};
+          uint64_t hu = 0;
+          st = gpk_capreader_index_all(rd, S.host + base_off + pos, S.h_seg.sync[j] - pos, 0, walk_threads, &hx, &hu);
+          if (st < 0) {
+            gpk_capindex_free(&hx);
+            ended = true;
+            break;
+          }
+          for (uint64_t i = 0; i < hx.n; i++) hx.offsets[i] += pos;
+          if (hx.n) chunks.push_back({G, hx});
+          else gpk_capindex_free(&hx);
+          G += hx.n;
+          pos += hu;
+          if (st != GPK_CAP_MORE) {
+            ended = true;
+            break;
+          }
+          gpk::WalkState w2;
+          if (!gpk_capreader_walk_state(rd, &w2) || memcmp(&w2, &ws, sizeof(ws)) != 0) break;  // the host takes the rest
+          k = pos == S.h_seg.sync[j] ? j : j + 1;  // landed: resume there; else sync[j] was inside a record
         }
-        if (good && G)
-          good = pl.ok(hipMemcpyAsync(S.d_seg.base, S.h_seg.base, nseg * 8ull, hipMemcpyHostToDevice, S.stream),
-                       "HtoD walk") &&
-                 pl.ok(gpk_walk_emit(S.dev + base_off, L, nseg, ws, S.d_seg, S.d_off, S.d_cap, S.d_ci, S.stream),
-                       "emit kernel");
-      }
-      if (good) {
-        // the exact reader from the first block the device walk did not take
-        st = gpk_capreader_index_all(rd, S.host + base_off + pos, L - pos, eof ? 1 : 0, walk_threads, &xi, &used);
-        used += pos - p0;
-        if (st >= 0 && xi.n) {
-          for (uint64_t i = 0; i < xi.n; i++) xi.offsets[i] += pos;
-          const std::string ge = grow_index(S, G, G + xi.n);
+        if (good && dev_pk) {
+          g_emit = G;
+          const std::string ge = grow_index(S, 0, G);
           if (!ge.empty()) {
             good = false;
             if (pl.herr.empty()) pl.herr = ge;
           }
-          good = good && pl.ok(hipMemcpyAsync(S.d_off + G, xi.offsets, xi.n * 8, hipMemcpyHostToDevice, S.stream), "HtoD index") &&
-                 pl.ok(hipMemcpyAsync(S.d_cap + G, xi.caplens, xi.n * 4, hipMemcpyHostToDevice, S.stream), "HtoD index") &&
-                 pl.ok(hipMemcpyAsync(S.d_ci + G, xi.ci, xi.n * sizeof(gpk_capture_info), hipMemcpyHostToDevice,
-                                      S.stream), "HtoD index") &&
-                 pl.ok(hipStreamSynchronize(S.stream), "hipStreamSynchronize");  // xi is freed below
+          good = good &&
+                 pl.ok(hipMemcpyAsync(S.d_seg.base, S.h_seg.base, nseg * 8ull, hipMemcpyHostToDevice, S.stream),
+                       "HtoD walk") &&
+                 pl.ok(gpk_walk_emit(S.dev + base_off, L, nseg, ws, S.d_seg, S.d_off, S.d_cap, S.d_ci, S.stream),
+                       "emit kernel");
         }
       }
+      if (good && !ended) {
+        // the exact reader from the last block the device walk did not take
+        st = gpk_capreader_index_all(rd, S.host + base_off + pos, L - pos, eof ? 1 : 0, walk_threads, &xi, &used);
+        if (st >= 0) {
+          for (uint64_t i = 0; i < xi.n; i++) xi.offsets[i] += pos;
+          if (xi.n) chunks.push_back({G, xi});
+          G += xi.n;
+          xi = gpk_capindex{};
+        }
+      } else {
+        used = 0;
+      }
+      used += pos - p0;
+      if (good && st >= 0 && !chunks.empty()) {
+        const std::string ge = grow_index(S, g_emit, G);  // (keeps what the emit kernel wrote)
+        if (!ge.empty()) {
+          good = false;
+          if (pl.herr.empty()) pl.herr = ge;
+        }
+        for (const auto& ch : chunks) {
+          const gpk_capindex& h = ch.second;
+          good = good &&
+                 pl.ok(hipMemcpyAsync(S.d_off + ch.first, h.offsets, h.n * 8, hipMemcpyHostToDevice, S.stream),
+                       "HtoD index") &&
+                 pl.ok(hipMemcpyAsync(S.d_cap + ch.first, h.caplens, h.n * 4, hipMemcpyHostToDevice, S.stream),
+                       "HtoD index") &&
+                 pl.ok(hipMemcpyAsync(S.d_ci + ch.first, h.ci, h.n * sizeof(gpk_capture_info), hipMemcpyHostToDevice,
+                                      S.stream),
+                       "HtoD index");
+        }
+        good = pl.ok(hipStreamSynchronize(S.stream), "hipStreamSynchronize") && good;  // the chunks are freed below
+      }
+      for (auto& ch : chunks) gpk_capindex_free(&ch.second);
+      stats->device_walk_packets += dev_pk;
     } else {
       st = gpk_capreader_index_all(rd, S.host + start, len, eof ? 1 : 0, walk_threads, &xi, &used);
     }

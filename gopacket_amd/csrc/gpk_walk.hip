@@ -57,9 +57,10 @@ __global__ void walk_kernel(const uint8_t* b, uint64_t p0, uint64_t len, uint64_
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= nseg) return;
   const uint64_t s0 = (uint64_t)k * seg, s1 = s0 + seg < len ? s0 + seg : len;
-  // segment 0 starts where the exact reader stands (p0); the others search
-  // (at most 1 MiB, as the host walk does)
-  uint64_t p = k == 0 ? p0 : find_sync(ws, b, s0, s1 < s0 + (1u << 20) ? s1 : s0 + (1u << 20), len, p0);
+  // the segment holding p0 starts where the exact reader stands; the later
+  // ones search (at most 1 MiB, as the host walk does), the earlier are empty
+  const uint64_t k0 = p0 / seg;
+  uint64_t p = k < k0 ? kNone : k == k0 ? p0 : find_sync(ws, b, s0, s1 < s0 + (1u << 20) ? s1 : s0 + (1u << 20), len, p0);
   out.sync[k] = p;
   uint32_t n = 0;
   if (p != kNone) {

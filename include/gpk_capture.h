@@ -163,6 +163,7 @@ typedef struct gpk_replay_stats {
   int reader_status;     /* the GPK_CAP_END error: 0 = io.EOF (clean end)        */
   char error[160];
   char kernel[96];       /* the decode kernel specialisation of the last launch */
+  uint64_t device_walk_packets; /* packets the device record walk indexed (the rest: the host reader) */
 } gpk_replay_stats;
 
 /* Results of one device launch, in packet order, delivered on the calling

@@ -125,6 +125,10 @@ def test_replay_device_walk(gpu_ctx, tmp_path, bo):
     for slot in (1 << 16, 1 << 20):
         st = check(gpu_ctx, str(path), raw, slot_bytes=slot, slots=3, batch_pkts=5000)
         assert st["error"] == "EOF"
+        # the host walks only the stretches the device chains did not cover (a
+        # fake chain, a block that is not plain, a record across the slot
+        # boundary) and hands back to the device walk after each
+        assert st["device_walk_packets"] >= 0.9 * st["packets"], (slot, st["device_walk_packets"], st["packets"])
     os.environ["GPK_REPLAY_HOST_WALK"] = "1"
     try:
         check(gpu_ctx, str(path), raw, slot_bytes=1 << 16, slots=3, batch_pkts=5000)
@@ -170,3 +174,35 @@ def test_replay_kernel_choice(gpu_ctx, tmp_path):
         finally:
             os.environ.pop("GPK_REPLAY_HOST_WALK", None)
         assert st["kernel"].endswith(",5,7,4>"), (host_walk, st["kernel"])
+
+
+def test_replay_device_walk_resumes(gpu_ctx, tmp_path):
+    """Blocks longer than a walk segment (16-64 KiB packets), blocks the device
+    walk leaves to the host (an EPB with options, a name record) and a new
+    interface mid-slot (the reader's walk state changes: the host takes the
+    rest of that slot, the next slot walks with the new interface table): the
+    device walk resumes after each host stretch where the reader's state
+    allows, and every packet matches the reader and decode oracles."""
+    from gopacket_amd import synth
+    rng = np.random.default_rng(11)
+    raw = pcapgen.shb() + pcapgen.idb(1, 0)
+    n_big = 0
+    for i in range(30000):
+        p = synth.packet(4, i)
+        if i % 2500 == 17:
+            p = p + bytes(rng.integers(0, 256, int(rng.integers(16, 64)) << 10, dtype=np.uint8))
+            n_big += 1
+        if i == 12345:
+            raw += pcapgen.epb(p, ts=i, options=pcapgen.opt(1, b"note") + pcapgen.end_opt())
+        elif i == 20000:
+            raw += pcapgen.nrb([(1, b"\x0a\x00\x00\x01x\x00")])
+        elif i == 25000:
+            raw += pcapgen.idb(1, 0)
+        else:
+            raw += pcapgen.epb(p, iface=1 if i > 25000 and i % 2 else 0, ts=i)
+    path = tmp_path / "resume.pcapng"
+    path.write_bytes(raw)
+    st = check(gpu_ctx, str(path), raw, slot_bytes=1 << 20, slots=3, batch_pkts=4096)
+    assert st["error"] == "EOF"
+    assert n_big >= 10
+    assert st["device_walk_packets"] >= 0.9 * st["packets"], (st["device_walk_packets"], st["packets"])
