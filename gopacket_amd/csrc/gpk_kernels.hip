@@ -314,10 +314,19 @@ struct WinT {
   uint4 v[W];
   uint32_t x;  // AL = 4: the window's 4W+1-th dword (the slot's odd dword)
 };
-// LDS dwords per lane for a window of W chunks (odd: see kSlotDw)
-template <int W>
+// LDS dwords per lane for a window of W chunks: W * 4 + 1 (the odd stride puts
+// lanes reading equal packet positions on distinct banks; AL = 4 uses the odd
+// dword as window bytes), except 6-chunk windows: 24 dwords, so a block with
+// the table blob (<= 2 KiB) stays within the 26 KiB that 6 blocks per CU allow
+// (25 dwords fit 5: tools/probes/occ_probe.hip; A/B r12 C4 -0.7..-3.6 %, C3
+// -1 %, profiles/r12_ab_slot24.txt). The 4-chunk kernel fits 8 blocks either way
+// and keeps the pad (C2 +4-7 % without it).
+#ifndef GPK_SLOT_PAD6
+#define GPK_SLOT_PAD6 0
+#endif
+template <int W, int AL>
 constexpr int slot_dw_of() {
-  return W * 4 + 1;
+  return W * 4 + (AL == 4 ? 1 : (W >= 6 ? GPK_SLOT_PAD6 : 1));
 }
 
 struct Idx {
@@ -894,7 +903,7 @@ __device__ __forceinline__ u32x4 sf_chunk(const KParams& P, uint64_t ga, uint64_
   return *reinterpret_cast<const u32x4*>(P.data + ga);
 }
 
-template <bool kL4, bool kLayout, class TT, bool kKeys, int W, int O, int AL, int kSlotStride = W * 4 + 1,
+template <bool kL4, bool kLayout, class TT, bool kKeys, int W, int O, int AL, int kSlotStride = slot_dw_of<W, AL>(),
           int kEarly = -1, bool kSF = false>
 __device__ __forceinline__ void decode_packet(const KParams& P, const TT& T, uint64_t i, bool active, uint64_t off,
                                               uint32_t cl, const WinGeo& g, uint32_t slot_dw, uint32_t lane,
@@ -1135,8 +1144,8 @@ template <bool kL4, bool kLayout, bool kCompact, bool kKeys = false, int W = kWi
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W == 4 ? GPK_W4_WAVES : O, 8))) void decode_kernel(
     KParams P) {
   const uint32_t tid = threadIdx.x;
-  const uint32_t slot_dw = tid * slot_dw_of<W>();
-  const uint32_t base = kBlock * slot_dw_of<W>();
+  const uint32_t slot_dw = tid * slot_dw_of<W, AL>();
+  const uint32_t base = kBlock * slot_dw_of<W, AL>();
   if ((uint64_t)blockIdx.x * kBlock >= P.n) return;  // uniform over the block
   // Every packet's index, then its header window and the table blob are in
   // flight together: two dependent memory round trips per packet.
@@ -1306,17 +1315,34 @@ __global__ void list_kernel(KParams P, uint64_t index, int64_t* out, uint32_t ca
 
 namespace {
 
+// Workgroups of `lds` bytes of LDS that are resident on one CU at once: the
+// occupancy API's count, capped by what gfx950 places (measured,
+// tools/probes/occ_probe.hip, profiles/r12_occupancy.json: 8 blocks up to
+// 20480 bytes, 7 up to 23040, 6 up to 26624, 5 up to 31744; the API allows one
+// more block above 27136 and 32256 bytes than are ever resident).
+int lds_blocks_per_cu(int lds) {
+  static const int lim[] = {0, 163840, 81920, 53248, 39936, 31744, 26624, 23040, 20480};
+  int b = 8;
+  while (b > 1 && lds > lim[b]) b--;
+  return b;
+}
+template <class K>
+hipError_t resident_blocks(K kernel, int lds, int* blocks) {
+  hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, kernel, gpk::kBlock, lds);
+  if (e == hipSuccess && *blocks > lds_blocks_per_cu(lds)) *blocks = lds_blocks_per_cu(lds);
+  return e;
+}
+
 // Launch one specialisation on `stream`, or (occ != nullptr) report how many of
 // its blocks fit a CU with this launch's LDS size instead.
 template <bool kL4, bool kLayout, bool kCompact, bool kKeys = false, int W = gpk::kWinChunks,
           int O = GPK_WAVES_PER_EU, int AL = 16>
 hipError_t launch(const gpk::KParams* P, hipStream_t stream, int* occ) {
   using namespace gpk;
-  constexpr int slot_lds = kBlock * slot_dw_of<W>() * 4;
+  constexpr int slot_lds = kBlock * slot_dw_of<W, AL>() * 4;
   // the table blob takes only the words this parser's tables use
   const int lds = kCompact ? slot_lds + (int)((P->cg.words + GPK_BLOB_ROUND - 1) & ~(GPK_BLOB_ROUND - 1u)) * 4 : slot_lds;
-  if (occ) return hipOccupancyMaxActiveBlocksPerMultiprocessor(occ, decode_kernel<kL4, kLayout, kCompact, kKeys, W, O, AL>,
-                                                              kBlock, lds);
+  if (occ) return resident_blocks(decode_kernel<kL4, kLayout, kCompact, kKeys, W, O, AL>, lds, occ);
   const uint64_t grid = (P->n + kBlock - 1) / kBlock;
   if (grid > 0xffffffffull) return hipErrorInvalidValue;
   hipLaunchKernelGGL((decode_kernel<kL4, kLayout, kCompact, kKeys, W, O, AL>), dim3((unsigned)grid), dim3(kBlock), lds,
@@ -1329,7 +1355,7 @@ hipError_t launch_sf(const gpk::KParams* P, hipStream_t stream, int* occ) {
   using namespace gpk;
   constexpr int fixed = kBlock * kSfStride * 4 + kWaves * kSfBmDw * 4;
   const int lds = kCompact ? fixed + (int)((P->cg.words + GPK_BLOB_ROUND - 1) & ~(GPK_BLOB_ROUND - 1u)) * 4 : fixed;
-  if (occ) return hipOccupancyMaxActiveBlocksPerMultiprocessor(occ, decode_sf_kernel<kCompact, GPK_SF_WAVES>, kBlock, lds);
+  if (occ) return resident_blocks(decode_sf_kernel<kCompact, GPK_SF_WAVES>, lds, occ);
   const uint64_t grid = (P->n + kBlock - 1) / kBlock;
   if (grid > 0xffffffffull) return hipErrorInvalidValue;
   hipLaunchKernelGGL((decode_sf_kernel<kCompact, GPK_SF_WAVES>), dim3((unsigned)grid), dim3(kBlock), lds, stream, *P);

@@ -59,6 +59,8 @@ def analyse(name, d, n_waves, out):
             nm, ph[:, k].mean(), np.percentile(ph[:, k], 50), np.percentile(ph[:, k], 90),
             100 * ph[:, k].sum() / life.sum(), ph[:, k].sum() / (nsimd * span)))
     lines.append("  resident waves per SIMD (mean over the span): %.2f" % res)
+    lines.append("  resident waves per SIMD by XCD: %s" % " ".join(
+        "%.2f" % (life[xcc == x].sum() / (max(1, len(np.unique(key_simd[xcc == x]))) * span)) for x in range(8)))
     # steady state: the middle 80 % of the span
     t0, t1 = t[:, 0].min() + 0.1 * (span / us), t[:, 0].min() + 0.9 * (span / us)
     ov = np.clip(np.minimum(t[:, 5], t1) - np.maximum(t[:, 0], t0), 0, None) * us
@@ -79,6 +81,34 @@ def analyse(name, d, n_waves, out):
     bend = blk[:, :, 5].max(axis=1)
     idle = ((bend[:, None] - blk[:, :, 5]) * us).mean()
     lines.append("  block skew: a wave ends %.2f us before its block's last wave (LDS held meanwhile)" % idle)
+    # blocks resident per CU: a block holds its CU from its first wave's entry to its last wave's exit
+    hwb = d[: nb * 4, 6].reshape(nb, 4)[good][:, 0]
+    hwid_b = (hwb & 0xffffffff).astype(np.int64)
+    cu_b = ((((hwb >> 32).astype(np.int64) & 0xf) * 8 + ((hwid_b >> 13) & 7)) * 2 + ((hwid_b >> 12) & 1)) * 16 + ((hwid_b >> 8) & 15)
+    bstart = blk[:, :, 0].min(axis=1)
+    ev_t = np.concatenate([bstart, bend])
+    ev_d = np.concatenate([np.ones(len(bstart), np.int64), -np.ones(len(bend), np.int64)])
+    ev_c = np.concatenate([cu_b, cu_b])
+    o = np.lexsort((ev_d, ev_t, ev_c))
+    ev_t, ev_d, ev_c = ev_t[o], ev_d[o], ev_c[o]
+    conc = np.zeros(len(ev_t), np.int64)
+    for c in np.unique(ev_c):
+        m = ev_c == c
+        conc[m] = np.cumsum(ev_d[m])
+    maxc = np.array([conc[ev_c == c].max() for c in np.unique(ev_c)])
+    # time-weighted share of the middle 80 % of the span at k resident blocks (all CUs)
+    lo, hi = t[:, 0].min() + 0.1 * (span / us), t[:, 0].min() + 0.9 * (span / us)
+    share = {}
+    for c in np.unique(ev_c):
+        m = ev_c == c
+        tt, cc = ev_t[m], conc[m]
+        dur = np.clip(np.minimum(np.append(tt[1:], tt[-1]), hi) - np.maximum(tt, lo), 0, None)
+        for k in np.unique(cc):
+            share[int(k)] = share.get(int(k), 0) + int(dur[cc == k].sum())
+    tot = sum(share.values()) or 1
+    lines.append("  blocks resident per CU: max over the span p10 %d p50 %d max %d; time share (middle 80 %%): %s" % (
+        np.percentile(maxc, 10), np.percentile(maxc, 50), maxc.max(),
+        " ".join("%d:%.1f%%" % (k, 100.0 * v / tot) for k, v in sorted(share.items()))))
     # persistent kernels: tile t runs on wave t mod S (S = resident waves); the first S tiles
     # should all start at the launch, a late one means its wave found no free slot
     S = 24 * 256
