@@ -85,17 +85,14 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 #ifndef GPK_DIAG_NOPARSE
 #define GPK_DIAG_NOPARSE 0  // timing only: skip DecodeLayers (fixed layout)
 #endif
-#ifndef GPK_SF
-#define GPK_SF 0  // stream-first small-packet L4 kernel (decode_sf_kernel): header windows taken from phase B's stream
+#ifndef GPK_SB
+#define GPK_SB 1  // stream-before-parse small-packet L4 kernel (decode_sb_kernel; A/B r12: C4 -3.6..-4.7 %)
 #endif
-#ifndef GPK_SF_ALL
-#define GPK_SF_ALL 0  // ... also for the parsers that take the dword-aligned 5-chunk kernel (C1)
+#ifndef GPK_SB_BIG
+#define GPK_SB_BIG 0  // ... for big-packet batches too (C3: +1.2 %, not used)
 #endif
-#ifndef GPK_SF_DEPTH
-#define GPK_SF_DEPTH 4  // ... its stream depth (passes in flight)
-#endif
-#ifndef GPK_SF_WAVES
-#define GPK_SF_WAVES 6  // ... its register budget (waves per SIMD)
+#ifndef GPK_SB_DEPTH
+#define GPK_SB_DEPTH 6  // ... its stream depth (passes in flight; 8 no better)
 #endif
 #ifndef GPK_DIAG_TIMES
 #define GPK_DIAG_TIMES 0  // diagnostic builds: per-wave phase timestamps into KParams.diag (tools/wave_times.py)
@@ -794,58 +791,26 @@ __device__ __forceinline__ uint32_t segment_sums(const KParams& P, Stream<D>& S,
   return sparse_segment_sums(P, job, s, e, lane);
 }
 
-// ---- Stream-first (decode_sf_kernel) -------------------------------------
-// For waves of packed, ordered small packets the header windows are not
-// loaded on their own: phase B's coalesced stream runs first, over the
-// packets' extents, and every 16-byte granule that belongs to a packet's
-// header window is written from the stream into that packet's LDS slot on the
-// way (the window loads fetched those lines a second time: about a third of
-// C4's DRAM lines, profiles/r10_reread_*). The stream also captures, per lane,
-// the L-form prefix just before its packet's first granule and at its last
-// granule; after the parse the segment's sum is that packet sum minus the
-// bytes before s and after e, which lie in the window (or come from memory).
-//
-// Granule ownership: granules are numbered from the wave's region base R0;
-// packet q's window is granules [a_q, a_q + n_q). With packets in batch order,
-// not overlapping and at most one starting per granule (checked per wave, else
-// the wave runs the ordinary path), the packet owning granule g is the latest
-// one starting at or before it, and only the granule where a packet starts can
-// also end the previous packet's window. A per-wave LDS bitmap of start
-// granules (64 bits per pass) gives each lane its owner with one mbcnt.
-constexpr int kSfStride = 24;  // LDS dwords per lane: 6 whole chunks (16-byte aligned for ds_write_b128)
-constexpr int kSfBmDw = 72;    // start-bitmap dwords per wave: regions up to 36 KiB
-struct SfPkt {
+// ---- Stream before the parse (decode_sb_kernel) ---------------------------
+// For waves of packed small packets phase B's stream runs before the parse,
+// over the packets' extents, and captures per lane the L-form prefix just
+// before its packet's first granule and at its last granule; after the parse
+// the segment's sum is that packet sum minus the bytes before s and after e,
+// which lie in the header windows (or come from memory).
+constexpr int kSbStride = 24;  // LDS dwords per lane: 6 whole 16-byte cells (the LDS-DMA layout)
+struct SbPkt {
   uint32_t L;   // L-form sum of the packet's granules [a, b]
   uint64_t R0;  // region base (batch offset, 16-byte aligned)
   int32_t b;    // the packet's last granule (region-relative)
   bool on;      // wave-uniform: the wave ran stream-first (else windows loaded, phase B after the parse)
 };
 
-// One pass of stream data (granule 64 p + lane) into the windows that hold it.
-__device__ __forceinline__ void sf_extract(const u32x4& v, uint32_t p, uint32_t lane, uint32_t bm, uint32_t slots,
-                                           uint32_t an, uint32_t& qs) {
-  const uint32_t* w = gpk_smem + (bm >> 2) + 2 * p;
-  const uint32_t mlo = w[0], mhi = w[1];  // start granules of this pass (wave-uniform words)
-  const uint32_t below = __builtin_amdgcn_mbcnt_hi(mhi, __builtin_amdgcn_mbcnt_lo(mlo, 0u));
-  const uint32_t here = (lane < 32 ? mlo >> lane : mhi >> (lane - 32)) & 1u;
-  const uint32_t g = 64u * p + lane;
-  const int32_t owner = (int32_t)(qs + below + here) - 1;
-  const uint32_t o1 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((uint32_t)owner << 2), (int)an);
-  const uint32_t o2 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((uint32_t)(owner - 1) << 2), (int)an);
-  const uint32_t c1 = g - (o1 & 0xffffffu), c2 = g - (o2 & 0xffffffu);
-  if (owner >= 0 && c1 < (o1 >> 24)) *reinterpret_cast<u32x4*>(reinterpret_cast<uint8_t*>(gpk_smem) + slots + 96u * (uint32_t)owner + 16u * c1) = v;
-  if (here && owner >= 1 && c2 < (o2 >> 24))
-    *reinterpret_cast<u32x4*>(reinterpret_cast<uint8_t*>(gpk_smem) + slots + 96u * (uint32_t)(owner - 1) + 16u * c2) = v;
-  qs += (uint32_t)__builtin_popcount(__builtin_amdgcn_readfirstlane(mlo)) +
-        (uint32_t)__builtin_popcount(__builtin_amdgcn_readfirstlane(mhi));
-}
-
-// The stream of a stream-first wave: region [R0, R0 + R), D passes in flight
-// (the dense stream's slots and waits), windows written on the way; returns
-// P(b) - P(a - 1) for the lane's packet (a - 1 = -1: none before it).
+// The stream of a stream-before-parse wave: region [R0, R0 + R), D passes in
+// flight (the dense stream's slots and waits); returns P(b) - P(a1) for the
+// lane's packet (a1 = -1: none before it).
 template <int D>
-__device__ __forceinline__ uint32_t sf_stream(const KParams& P, Stream<D>& S, uint64_t R0, uint32_t R, uint32_t lane,
-                                              int32_t a1, int32_t b, uint32_t an, uint32_t bm, uint32_t slots) {
+__device__ __forceinline__ uint32_t sb_stream(const KParams& P, Stream<D>& S, uint64_t R0, uint32_t R, uint32_t lane,
+                                              int32_t a1, int32_t b) {
   static_assert(kGran == 1, "one 16-byte granule per lane per pass");
   stream_issue(P, S, R0, R, lane, 0, D);
   const __amdgpu_buffer_rsrc_t rs = rsrc(P.data + R0, (R + 15) & ~15u);
@@ -854,10 +819,9 @@ __device__ __forceinline__ uint32_t sf_stream(const KParams& P, Stream<D>& S, ui
   Gran (&ring)[D] = S.ring;
   const int32_t pa = a1 >> 6, pb = b >> 6;  // -1 never matches
   const int32_t la = (a1 & 63) << 2, lb = (b & 63) << 2, ll = (int32_t)lane << 2;
-  uint32_t xa = 0, xb = 0, c = 0, qs = 0;
+  uint32_t xa = 0, xb = 0, c = 0;
   auto pass = [&](const int d, const int32_t p, const bool refill) __attribute__((always_inline)) {
     const uint32_t gl = chunk_l(ring[d].c[0], 0u);
-    sf_extract(ring[d].c[0], (uint32_t)p, lane, bm, slots, an, qs);
     if (refill) slot_load(ring[d].c, rs, vo, (uint32_t)(p + D) * kPassBytes);
     const uint32_t sc = wave_scan(gl);
     const uint32_t Pf = sc + c;
@@ -869,8 +833,7 @@ __device__ __forceinline__ uint32_t sf_stream(const KParams& P, Stream<D>& S, ui
     c += readlane32(sc, 63);
   };
   // The first round runs on every path (passes past the region read
-  // range-checked zeros, add nothing and write no window chunk the parse
-  // reads): no edge bypasses the loop, so the slot registers the passes were
+  // range-checked zeros and add nothing): no edge bypasses the loop, so the slot registers the passes were
   // issued into are the loop's own (a bypass made the allocator copy them
   // while in flight: tools/check_stream_isa.py).
   uint32_t p0 = 0;
@@ -893,21 +856,21 @@ __device__ __forceinline__ uint32_t sf_stream(const KParams& P, Stream<D>& S, ui
 }
 
 // 16 bytes of the batch at granule address ga (16-byte aligned) for a
-// stream-first lane: its own window chunk, the next packet's first chunk, or
+// stream-before-parse lane: its own window chunk, the next packet's first chunk, or
 // memory.
-__device__ __forceinline__ u32x4 sf_chunk(const KParams& P, uint64_t ga, uint64_t wb, uint32_t nch, uint32_t slot_dw,
+__device__ __forceinline__ u32x4 sb_chunk(const KParams& P, uint64_t ga, uint64_t wb, uint32_t nch, uint32_t slot_dw,
                                           bool next_here, uint64_t nwb) {
   const uint64_t k = (ga - wb) >> 4;
   if (ga >= wb && k < nch) return lds_chunk(slot_dw * 4 + 16u * (uint32_t)k);
-  if (next_here && ga == nwb) return lds_chunk((slot_dw + kSfStride) * 4);
+  if (next_here && ga == nwb) return lds_chunk((slot_dw + kSbStride) * 4);
   return *reinterpret_cast<const u32x4*>(P.data + ga);
 }
 
 template <bool kL4, bool kLayout, class TT, bool kKeys, int W, int O, int AL, int kSlotStride = slot_dw_of<W, AL>(),
-          int kEarly = -1, bool kSF = false>
+          int kEarly = -1, bool kSB = false>
 __device__ __forceinline__ void decode_packet(const KParams& P, const TT& T, uint64_t i, bool active, uint64_t off,
                                               uint32_t cl, const WinGeo& g, uint32_t slot_dw, uint32_t lane,
-                                              uint64_t* dt, const SfPkt sf = SfPkt{0, 0, -1, false}) {
+                                              uint64_t* dt, const SbPkt sb = SbPkt{0, 0, -1, false}) {
   const uint32_t m = g.m, win = g.win;
   Rd r{P.data + off, slot_dw * 4 + m, win};
 
@@ -1050,24 +1013,42 @@ __device__ __forceinline__ void decode_packet(const KParams& P, const TT& T, uin
 #if GPK_DIAG_TIMES
   dt[3] = __builtin_amdgcn_s_memrealtime();
 #endif
-  if (kL4 && kSF && sf.on) {
-    // stream-first: the packet's granule sum minus the bytes of its granules
-    // before s (header bytes, in the window) and from e on (padding and the
-    // next packet's first bytes)
+  if (kL4 && kSB && sb.on) {
+    // stream before the parse: the packet's granule sum minus the bytes of its
+    // granules before s (header bytes, in the window) and from e on (padding
+    // and the next packet's first bytes)
     const uint32_t nch = active ? (m + win + 15) >> 4 : 0u;
     const uint32_t nwb_lo = (uint32_t)__shfl_down((int)(uint32_t)g.wb, 1);
     const uint32_t nwb_hi = (uint32_t)__shfl_down((int)(uint32_t)(g.wb >> 32), 1);
     const uint32_t nnch = (uint32_t)__shfl_down((int)nch, 1);
     const uint64_t nwb = (uint64_t)nwb_hi << 32 | nwb_lo;
     const bool next_here = lane < 63 && nnch != 0;
-    uint32_t L = sf.L;
+    uint32_t L = sb.L;
     if (job) {
-      const uint32_t hl = (uint32_t)(js - g.wb);
-      for (uint32_t k = 0; k < (hl >> 4); k++) L -= chunk_l(sf_chunk(P, g.wb + 16u * k, g.wb, nch, slot_dw, next_here, nwb), 0u);
-      L -= chunk_l_below(sf_chunk(P, g.wb + (hl & ~15u), g.wb, nch, slot_dw, next_here, nwb), hl & 15u, 0u);
-      const uint64_t gend = sf.R0 + 16ull * (uint64_t)(sf.b + 1), gj = je & ~15ull;
-      for (uint64_t ga = gj; ga < gend; ga += 16) L -= chunk_l(sf_chunk(P, ga, g.wb, nch, slot_dw, next_here, nwb), 0u);
-      if (gj < gend) L += chunk_l_below(sf_chunk(P, gj, g.wb, nch, slot_dw, next_here, nwb), (uint32_t)(je & 15), 0u);
+      // header bytes [wb, js): whole window chunks below the chunk of js and
+      // its bytes before js, from LDS; headers past the window (the general
+      // decoder's long ones) from memory
+      const uint32_t hl = (uint32_t)(js - g.wb), hk = hl >> 4;
+      if (hl < 16u * nch) {
+        for (uint32_t k = 0; k < hk; k++) L -= chunk_l(lds_chunk(slot_dw * 4 + 16u * k), 0u);
+        L -= chunk_l_below(lds_chunk(slot_dw * 4 + 16u * hk), hl & 15u, 0u);
+      } else {
+        for (uint32_t k = 0; k < hk; k++) L -= chunk_l(*reinterpret_cast<const u32x4*>(P.data + g.wb + 16u * k), 0u);
+        L -= chunk_l_below(*reinterpret_cast<const u32x4*>(P.data + g.wb + 16u * hk), hl & 15u, 0u);
+      }
+      // bytes [je, gend) of the packet's last granule(s): the granule of je is
+      // in this packet's window or is the next packet's first window chunk
+      // (else from memory); granules after it only with >= 16 padding bytes
+      const uint64_t gend = sb.R0 + 16ull * (uint64_t)(sb.b + 1), gj = je & ~15ull;
+      if (gj < gend) {
+        const uint64_t kk = (gj - g.wb) >> 4;
+        const bool own = kk < nch, nxt = !own && next_here && gj == nwb;
+        u32x4 c = lds_chunk(own ? slot_dw * 4 + 16u * (uint32_t)kk : (slot_dw + kSlotStride) * 4);
+        if (!own && !nxt) c = *reinterpret_cast<const u32x4*>(P.data + gj);
+        L -= chunk_l(c, 0u) - chunk_l_below(c, (uint32_t)(je & 15), 0u);
+        for (uint64_t ga = gj + 16; ga < gend; ga += 16)
+          L -= chunk_l(sb_chunk(P, ga, g.wb, nch, slot_dw, next_here, nwb), 0u);
+      }
       const uint32_t sum = l_to_words(L, (uint32_t)js & 1u);
       l4c = fold(jinit + sum - jexist);
       const bool udp = (st & GPK_ST_L4_UDP) != 0;
@@ -1196,21 +1177,52 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W == 4 ?
 #endif
 }
 
-// Stream-first L4 kernel for batches of small packets (see sf_stream): W = 6
-// header windows, 16-byte aligned, 24-dword slots (6 blocks per CU with the
-// start bitmaps and the table blob). A wave whose packets are not packed and
-// ordered runs the ordinary path (windows loaded, then the parse, then phase B).
+// Stream-before-parse L4 kernel (GPK_SB): the header windows go into LDS by
+// LDS-DMA (no registers held) and phase B's stream over the wave's packets is
+// issued right behind them, before DecodeLayers: the window's latency hides
+// under the stream, the stream re-reads the window lines while they are still
+// in L2, and the parse that follows has the whole register file. The stream
+// keeps, per lane, the L-form sum of its packet's granules (sb_stream); after
+// the parse decode_packet's stream-before-parse branch subtracts the header
+// bytes before the segment (window) and the bytes after it. Waves whose
+// packets are not packed run the ordinary phase B after the parse.
+
+// 16 bytes per lane into LDS: lane l's bytes land at LDS byte `lds` + 16 l
+// (wave-uniform destination, per-lane source; tools/probes/lds_dma.hip).
+__device__ __forceinline__ void dma16(uint64_t src, uint32_t lds) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(src), "s"(lds)
+               : "memory");
+}
+// The W-chunk windows of the wave's 64 packets into its slots (slot q at LDS
+// byte `region` + 16 W q, no pad: instruction k writes cells 64 k .. 64 k + 63,
+// cell e = chunk e mod W of packet e / W, the packet's window base and chunk
+// count fetched from its lane). Chunks past a window re-read its last chunk, a
+// packet with none reads the parser's table copy (as load_window).
+template <int W>
+__device__ __forceinline__ void window_dma(const KParams& P, const WinGeo& g, uint32_t region, uint32_t lane) {
+  const uint64_t src = g.nch ? (uint64_t)(uintptr_t)(P.data + g.wb) : (uint64_t)(uintptr_t)P.tab;
+  const uint32_t last = g.nch ? g.nch - 1 : 0u;
+#pragma unroll
+  for (int k = 0; k < W; k++) {
+    const uint32_t e = 64u * k + lane, q = e / W, c = e - q * W;
+    const int qa = (int)(q << 2);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute(qa, (int)(uint32_t)src);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute(qa, (int)(uint32_t)(src >> 32));
+    const uint32_t lq = (uint32_t)__builtin_amdgcn_ds_bpermute(qa, (int)last);
+    dma16(((uint64_t)hi << 32 | lo) + 16u * (c < lq ? c : lq), region + 1024u * k);
+  }
+}
+
 template <bool kCompact, int O>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(O, 8))) void decode_sf_kernel(KParams P) {
-  // O: the register budget (6 blocks per CU by LDS: 80 VGPRs cost nothing); the
-  // phase-B depth and the fallback's specialisation are the 72-VGPR kernel's
-  constexpr int W = 6, OP = GPK_SMALL_WAVES;
-  constexpr int D = GPK_SF_DEPTH;
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(O, 8))) void decode_sb_kernel(KParams P) {
+  constexpr int W = 6, D = GPK_SB_DEPTH;
+  static_assert(kSbStride == 4 * W, "one 16-byte cell per window chunk, no pad");
   const uint32_t tid = threadIdx.x, lane = tid & 63;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const uint32_t slot_dw = tid * kSfStride;
-  const uint32_t bm = (kBlock * kSfStride + wave * kSfBmDw) * 4;  // LDS byte address of this wave's bitmap
-  const uint32_t base = kBlock * kSfStride + kWaves * kSfBmDw;     // table blob (dwords)
+  const uint32_t base = kBlock * kSbStride;  // table blob (dwords)
   if ((uint64_t)blockIdx.x * kBlock >= P.n) return;  // uniform over the block
   const uint64_t i0 = (uint64_t)blockIdx.x * kBlock + tid;
   const bool active = i0 < P.n;
@@ -1220,7 +1232,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(O, 8))) 
 #endif
   const Idx c0 = load_index(P, i0);
   const WinGeo g0 = win_geo<W, 16>(P, c0, active);
-  if (kCompact) {
+  window_dma<W>(P, g0, (uint32_t)(uintptr_t)gpk_smem + wave * (64u * kSbStride * 4u), lane);
+  if (kCompact) {  // the table blob (read after the barrier below)
     static_assert(kCtDwords <= 3 * kBlock, "three blob words per thread");
     const uint32_t last = P.cg.words - 1;
 #pragma unroll
@@ -1228,51 +1241,29 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(O, 8))) 
       const uint32_t j = tid + k * kBlock < last ? tid + k * kBlock : last;
       gpk_smem[base + j] = P.ctab[j];
     }
-    __syncthreads();
   }
 #if GPK_DIAG_TIMES
-  dt[1] = dt[2] = __builtin_amdgcn_s_memrealtime();
+  dt[1] = __builtin_amdgcn_s_memrealtime();  // (diag phases: index | stream | parse | correction)
 #endif
-  // the wave's plan: packed (dense_region over the packet extents), in order,
-  // not overlapping, one start per granule, and the bitmap large enough
+  // the stream over the packets' extents, when packed
   uint64_t R0 = 0;
   uint32_t R = 0;
-  bool ok = dense_region(active, c0.off, c0.off + c0.cl, R0, R);
-  {
-    const uint64_t end = c0.off + c0.cl;
-    const uint32_t pe_lo = (uint32_t)__shfl_up((int)(uint32_t)end, 1), pe_hi = (uint32_t)__shfl_up((int)(uint32_t)(end >> 32), 1);
-    const uint32_t pw_lo = (uint32_t)__shfl_up((int)(uint32_t)g0.wb, 1), pw_hi = (uint32_t)__shfl_up((int)(uint32_t)(g0.wb >> 32), 1);
-    const uint64_t pend = (uint64_t)pe_hi << 32 | pe_lo, pwb = (uint64_t)pw_hi << 32 | pw_lo;
-    const bool bad = active && lane > 0 && (c0.off < pend || g0.wb <= pwb);
-    ok = ok && !__ballot(bad) && R <= (uint32_t)kSfBmDw * 32u * 16u;
-  }
+  const bool ok = dense_region(active, c0.off, c0.off + c0.cl, R0, R);
   uint32_t L = 0;
   int32_t b = -1;
   if (ok) {
-    // start bitmap: granule a of every packet (region-relative)
-    const uint32_t a = active ? (uint32_t)((g0.wb - R0) >> 4) : 0xffffffu;
-    const uint32_t an = active ? (a | g0.nch << 24) : 0xffffffu;
-    const uint32_t np = (R + kPassBytes - 1) / kPassBytes;
-    uint32_t* bmw = gpk_smem + (bm >> 2);
-    const uint32_t nw = 2 * (np > (uint32_t)D ? np : (uint32_t)D);  // the first round's passes too
-    if (lane < nw) bmw[lane] = 0u;
-    if (lane + 64 < nw) bmw[lane + 64] = 0u;
-    if (active) __hip_atomic_fetch_or(bmw + (a >> 5), 1u << (a & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    const int32_t a1 = active ? (int32_t)a - 1 : -1;
+    const int32_t a1 = active ? (int32_t)((g0.wb - R0) >> 4) - 1 : -1;
     b = active ? (int32_t)(((c0.off + c0.cl) - 1 - R0) >> 4) : -1;
     Stream<D> S;
     S.on = true;
-    L = sf_stream<D>(P, S, R0, R, lane, a1, b, an, bm, (wave * 64u * kSfStride) * 4u);
-  } else {
-    WinT<W> w;
-    load_window<W, 16>(P, g0, w);
-    store_window<W, 16>(slot_dw, w);
+    L = sb_stream<D>(P, S, R0, R, lane, a1, b);
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the windows have landed (the stream waited for them too)
+  if (kCompact) __syncthreads();
 #if GPK_DIAG_TIMES
-  dt[3] = __builtin_amdgcn_s_memrealtime();
+  dt[2] = __builtin_amdgcn_s_memrealtime();
 #endif
-  // Only the index entry crosses the stream: everything derived from it is
-  // formed again here (kept live, it was spilled around the stream).
+  // only the index entry crosses the stream: everything derived from it is formed again
   uint32_t off_lo = (uint32_t)c0.off, off_hi = (uint32_t)(c0.off >> 32), ccl = c0.cl;
   asm volatile("" : "+v"(off_lo), "+v"(off_hi), "+v"(ccl));
   const Idx c1{(uint64_t)off_hi << 32 | off_lo, ccl};
@@ -1280,17 +1271,17 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(O, 8))) 
   const uint64_t i1 = (uint64_t)blockIdx.x * kBlock + tid1;
   const WinGeo g1 = win_geo<W, 16>(P, c1, i1 < P.n);
   if (kCompact)
-    decode_packet<true, false, LTab, false, W, OP, 16, kSfStride, 0, true>(P, LTab{P.cg, base}, i1, i1 < P.n, c1.off,
-                                                                          c1.cl, g1, tid1 * kSfStride, tid1 & 63, dt,
-                                                                          SfPkt{L, R0, b, ok});
+    decode_packet<true, false, LTab, false, W, O, 16, kSbStride, 0, true>(P, LTab{P.cg, base}, i1, i1 < P.n, c1.off,
+                                                                         c1.cl, g1, tid1 * kSbStride, tid1 & 63, dt,
+                                                                         SbPkt{L, R0, b, ok});
   else
-    decode_packet<true, false, GTab, false, W, OP, 16, kSfStride, 0, true>(P, GTab{P.tab}, i1, i1 < P.n, c1.off, c1.cl,
-                                                                          g1, tid1 * kSfStride, tid1 & 63, dt,
-                                                                          SfPkt{L, R0, b, ok});
+    decode_packet<true, false, GTab, false, W, O, 16, kSbStride, 0, true>(P, GTab{P.tab}, i1, i1 < P.n, c1.off, c1.cl,
+                                                                         g1, tid1 * kSbStride, tid1 & 63, dt,
+                                                                         SbPkt{L, R0, b, ok});
 #if GPK_DIAG_TIMES
   dt[5] = __builtin_amdgcn_s_memrealtime();
   dt[6] = (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 4) | (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32;
-  dt[7] = ok ? (uint64_t)R | (uint64_t)__builtin_popcountll(__ballot(active)) << 32 : 0;  // the stream-first region
+  dt[7] = ok ? (uint64_t)R | (uint64_t)__builtin_popcountll(__ballot(active)) << 32 : 0;
   if (P.diag && lane < 8) {
     uint64_t v = dt[0];
 #pragma unroll
@@ -1350,15 +1341,15 @@ hipError_t launch(const gpk::KParams* P, hipStream_t stream, int* occ) {
   return hipGetLastError();
 }
 
-template <bool kCompact>
-hipError_t launch_sf(const gpk::KParams* P, hipStream_t stream, int* occ) {
+template <bool kCompact, int O>
+hipError_t launch_sb(const gpk::KParams* P, hipStream_t stream, int* occ) {
   using namespace gpk;
-  constexpr int fixed = kBlock * kSfStride * 4 + kWaves * kSfBmDw * 4;
+  constexpr int fixed = kBlock * kSbStride * 4;
   const int lds = kCompact ? fixed + (int)((P->cg.words + GPK_BLOB_ROUND - 1) & ~(GPK_BLOB_ROUND - 1u)) * 4 : fixed;
-  if (occ) return resident_blocks(decode_sf_kernel<kCompact, GPK_SF_WAVES>, lds, occ);
+  if (occ) return resident_blocks(decode_sb_kernel<kCompact, O>, lds, occ);
   const uint64_t grid = (P->n + kBlock - 1) / kBlock;
   if (grid > 0xffffffffull) return hipErrorInvalidValue;
-  hipLaunchKernelGGL((decode_sf_kernel<kCompact, GPK_SF_WAVES>), dim3((unsigned)grid), dim3(kBlock), lds, stream, *P);
+  hipLaunchKernelGGL((decode_sb_kernel<kCompact, O>), dim3((unsigned)grid), dim3(kBlock), lds, stream, *P);
   return hipGetLastError();
 }
 
@@ -1366,7 +1357,7 @@ hipError_t launch_sf(const gpk::KParams* P, hipStream_t stream, int* occ) {
 struct Sel {
   bool l4, layout, compact, keys;
   int W, O, AL;
-  bool sf;
+  bool sb;
 };
 Sel select(const gpk::KParams* P, int with_l4, int with_layout) {
   Sel s{with_l4 != 0, with_layout != 0, P->ctab != nullptr, P->key_kind != 0, gpk::kWinChunks, GPK_WAVES_PER_EU, 16,
@@ -1377,20 +1368,22 @@ Sel select(const gpk::KParams* P, int with_l4, int with_layout) {
     s.W = 4;
   } else if (!s.layout && !P->big_packets) {
     s.O = GPK_SMALL_WAVES;
-    if (GPK_MID_W5 && !(GPK_SF && GPK_SF_ALL) && (P->mid_headers || GPK_MID_IP6) && P->data_end) {  // a dword-aligned 5-chunk window: 7 blocks per CU (LDS)
+    if (GPK_MID_W5 && (P->mid_headers || GPK_MID_IP6) && P->data_end) {  // a dword-aligned 5-chunk window: 7 blocks per CU (LDS)
       s.W = 5;
       s.AL = 4;
     }
-    // stream-first: the small-packet L4 kernel with the 6-chunk window
-    s.sf = GPK_SF && s.l4 && s.W == gpk::kWinChunks && s.AL == 16;
   }
+  s.sb = GPK_SB && s.l4 && !s.layout && !s.keys && s.W == gpk::kWinChunks && s.AL == 16 &&
+         (GPK_SB_BIG || s.O != GPK_WAVES_PER_EU);
   return s;
 }
 
 template <bool kCompact>
 hipError_t launch_sel(const gpk::KParams* P, const Sel& s, hipStream_t stream, int* occ) {
   constexpr int W = gpk::kWinChunks;
-  if (s.sf) return launch_sf<kCompact>(P, stream, occ);
+  if (s.sb)
+    return s.O == GPK_WAVES_PER_EU ? launch_sb<kCompact, GPK_WAVES_PER_EU>(P, stream, occ)
+                                   : launch_sb<kCompact, GPK_SMALL_WAVES>(P, stream, occ);
   if (s.keys)
     return s.l4 ? launch<true, false, kCompact, true>(P, stream, occ) : launch<false, false, kCompact, true>(P, stream, occ);
   if (s.W == 4) return launch<false, false, kCompact, false, 4>(P, stream, occ);
@@ -1423,7 +1416,7 @@ extern "C" hipError_t gpk_launch_occupancy(const gpk::KParams* P, int with_l4, i
 // Name of the kernel specialisation gpk_launch_decode would launch.
 extern "C" int gpk_launch_describe(const gpk::KParams* P, int with_l4, int with_layout, char* buf, size_t cap) {
   const Sel s = select(P, with_l4, with_layout);
-  if (s.sf) return snprintf(buf, cap, "gpk::decode_sf_kernel<%s,%d>", s.compact ? "true" : "false", s.O);
+  if (s.sb) return snprintf(buf, cap, "gpk::decode_sb_kernel<%s,%d>", s.compact ? "true" : "false", s.O);
   return snprintf(buf, cap, "gpk::decode_kernel<%s,%s,%s,%s,%d,%d,%d>", s.l4 ? "true" : "false",
                   s.layout ? "true" : "false", s.compact ? "true" : "false", s.keys ? "true" : "false", s.W,
                   s.W == 4 ? 6 : s.O, s.AL);

@@ -150,7 +150,7 @@ def main(path):
     text = open(path).read().split("\n")
     funcs, cur, start = {}, None, 0
     for i, l in enumerate(text):
-        m = re.match(r"^(_Z\w*decode_(?:sf_)?kernel\w*):", l)
+        m = re.match(r"^(_Z\w*decode_(?:sb_)?kernel\w*):", l)
         if m:
             cur, start = m.group(1), i
         elif cur and l.startswith(".Lfunc_end"):

@@ -5,7 +5,7 @@ set -o pipefail
 OUT=gpurun_out/$1
 mkdir -p $OUT
 export TMPDIR=/tmp
-P="--kernel-include-regex decode_kernel -f csv"
+P="--kernel-include-regex decode_(sb_|)kernel -f csv"
 for v in $2; do
   for c in $(echo $3 | tr , ' '); do
     A="tools/ab_inproc.py --configs $c --rounds 1 --steps 2 $v"

@@ -30,7 +30,7 @@ def summarise(d, labels):
     rows, meta = load(d)
     by_tag = defaultdict(list)
     for key in sorted(rows):
-        if "decode_kernel" in meta[key][0]:
+        if "decode_kernel" in meta[key][0] or "decode_sb_kernel" in meta[key][0]:
             by_tag[key[0]].append(key)
     out = defaultdict(lambda: defaultdict(list))
     for tag, keys in by_tag.items():

@@ -1,5 +1,5 @@
 // Issue-rate probe: shader cycles per instruction per wave for a stream of
-// independent scalar (s_add_u32), vector (v_add_u32) or mixed (1:1)
+// independent scalar (s_movk_i32), vector (v_add_u32) or mixed (1:1)
 // instructions, at 1..8 waves per SIMD (256-thread blocks, one wave per SIMD,
 // k blocks per CU). Shows whether scalar issue is a per-CU or per-SIMD
 // resource on gfx950, i.e. how much a wave's SALU count costs when the CU is
@@ -29,8 +29,9 @@ __global__ __launch_bounds__(256) void issue_kernel(uint32_t iters, uint64_t* ou
   for (uint32_t k = 0; k < iters; k++) {
     if (MODE == 0 || MODE == 2) {
       asm volatile(
-          "s_add_u32 %0, %0, 1\n\ts_add_u32 %1, %1, 1\n\ts_add_u32 %2, %2, 1\n\ts_add_u32 %3, %3, 1\n\t"
-          "s_add_u32 %4, %4, 1\n\ts_add_u32 %5, %5, 1\n\ts_add_u32 %6, %6, 1\n\ts_add_u32 %7, %7, 1"
+          // s_movk_i32: no SCC write (an s_add here clobbered the loop's branch condition)
+          "s_movk_i32 %0, 0x11\n\ts_movk_i32 %1, 0x12\n\ts_movk_i32 %2, 0x13\n\ts_movk_i32 %3, 0x14\n\t"
+          "s_movk_i32 %4, 0x15\n\ts_movk_i32 %5, 0x16\n\ts_movk_i32 %6, 0x17\n\ts_movk_i32 %7, 0x18"
           : "+s"(s0), "+s"(s1), "+s"(s2), "+s"(s3), "+s"(s4), "+s"(s5), "+s"(s6), "+s"(s7));
     }
     if (MODE == 1 || MODE == 2) {
@@ -77,6 +78,7 @@ int main() {
              "\"instr_per_cycle_per_simd\": %.3f}",
              first ? "" : ",\n", names[mode], k, cyc, k / cyc);
       first = false;
+      fflush(stdout);
     }
   }
   printf("\n]}\n");

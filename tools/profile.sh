@@ -18,7 +18,7 @@ export TMPDIR=/tmp
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -f csv -d $OUT/kt_c3 -o kt -- python3 bench.py --configs c3 --no-cpu-baseline --c5 0 --steps 10 --warmup 2 > $OUT/kt_c3_bench.json || exit 1
 B="bench.py --no-cpu-baseline --no-parity --c5 0 --configs $CFGS"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -f csv -d $OUT/kt -o kt -- python3 $B --steps 5 --warmup 1 > $OUT/kt_bench.json || exit 1
-P="--kernel-include-regex decode_kernel -f csv"
+P="--kernel-include-regex decode_(sb_|)kernel -f csv"
 for c in $(echo $CFGS | tr , ' '); do
   A="tools/ab_inproc.py --configs $c --rounds 1 --steps 2 base"
   timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE $P -d $OUT/$c/fetch -o fetch -- python3 $A > /dev/null || exit 2
