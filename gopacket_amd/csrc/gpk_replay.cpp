@@ -107,6 +107,7 @@ struct Fill {      // one read of a slot's fresh bytes
   uint64_t bytes;  // read
   bool end;        // the stream ended with this read
   double t0, t1;   // read start / end (GPK_REPLAY_TRACE=2)
+  hipEvent_t sent; // recorded after the read's HtoD (device walk), or null
 };
 
 struct Slot {
@@ -121,6 +122,7 @@ struct Slot {
   uint64_t idx_cap = 0;  // entries of d_off / d_cap / d_ci
   hipStream_t stream = nullptr;
   hipEvent_t h2d = nullptr;  // the slot's HtoD finished: host buffer reusable
+  hipEvent_t sent = nullptr; // the read thread's HtoD of the fresh bytes finished (orders the next one)
   hipError_t h2d_err = hipSuccess;  // the read thread's HtoD of the fresh bytes (device walk)
   bool h2d_pending = false;
   std::shared_future<struct Fill> fill;  // async read of the fresh bytes
@@ -195,6 +197,7 @@ struct Pipeline {
       for (void* p : {(void*)s.h_seg.sync, (void*)s.h_seg.end, (void*)s.h_seg.count, (void*)s.h_seg.base})
         if (p) (void)hipHostFree(p);
       if (s.h2d) (void)hipEventDestroy(s.h2d);
+      if (s.sent) (void)hipEventDestroy(s.sent);
       if (s.stream) (void)hipStreamDestroy(s.stream);
     }
     for (auto& B : bats) {
@@ -223,6 +226,7 @@ std::string alloc_slot(Slot& s, uint64_t C, uint64_t R, bool dev_walk, uint64_t 
   ALLOC_OK(hipMalloc((void**)&s.dev, C + R + 16), "hipMalloc slot");
   ALLOC_OK(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking), "hipStreamCreate");
   ALLOC_OK(hipEventCreateWithFlags(&s.h2d, hipEventDisableTiming), "hipEventCreate");
+  ALLOC_OK(hipEventCreateWithFlags(&s.sent, hipEventDisableTiming), "hipEventCreate");
   if (!dev_walk) return "";
   ALLOC_OK(hipMalloc((void**)&s.d_seg.sync, kMaxSeg * 8), "hipMalloc walk");
   ALLOC_OK(hipMalloc((void**)&s.d_seg.end, kMaxSeg * 8), "hipMalloc walk");
@@ -438,17 +442,26 @@ extern "C" int gpk_replay_file(gpk_ctx* ctx, const gpk_parser* parser, const cha
     s.h2d_err = hipSuccess;
     std::shared_future<Fill> prev = last_fill;
     s.fill = std::async(std::launch::async, [&src, &s, C, R, stats, dev, dev_walk, prev] {
-      if (prev.valid()) prev.wait();
+      hipEvent_t before = nullptr;
+      if (prev.valid()) before = prev.get().sent;
       double t = now_s();
       const uint64_t k = src.read(s.host + C, R);
       const bool end = src.at_end;
       const double t1 = now_s();
       stats->read_s += t1 - t;
+      hipEvent_t sent = nullptr;
       if (dev_walk && k) {
+        // the slots' copies go over the link one after another, in stream
+        // order: several in flight at once share the link, and the slot the
+        // walk needs next would land last (A/B r12: 49-52 GB/s against 45-47
+        // with the copies overlapping)
         (void)hipSetDevice(dev);
-        s.h2d_err = hipMemcpyAsync(s.dev + C, s.host + C, k, hipMemcpyHostToDevice, s.stream);
+        s.h2d_err = before ? hipStreamWaitEvent(s.stream, before, 0) : hipSuccess;
+        if (s.h2d_err == hipSuccess) s.h2d_err = hipMemcpyAsync(s.dev + C, s.host + C, k, hipMemcpyHostToDevice, s.stream);
+        if (s.h2d_err == hipSuccess) s.h2d_err = hipEventRecord(s.sent, s.stream);
+        if (s.h2d_err == hipSuccess) sent = s.sent;
       }
-      return Fill{k, end, t, t1};
+      return Fill{k, end, t, t1, sent};
     }).share();
     s.fill_pending = true;
     last_fill = s.fill;
