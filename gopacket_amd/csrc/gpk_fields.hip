@@ -1,0 +1,193 @@
+// gpk_fields.hip — the scalar layer fields of every packet of a decoded batch
+// (include/gpk.h gpk_fields, gpk_extract_fields), for consumers that read
+// layer fields after DecodeLayers.
+//
+// A decoder's fields are a pure function of the slice its last successful
+// DecodeFromBytes was handed, which the decode kernels report per packet as
+// the layout ([start, end) per decoder slot). One lane per packet loads the
+// 16-byte-aligned run of 6 chunks holding the packet's first bytes into its LDS
+// slot, reads each present slice's header words from there (unaligned
+// ds_read_b32; from memory past the run), and the wave writes its 64 records
+// through LDS as eight coalesced 1 KiB stores.
+// Field by field this restates:
+//   Ethernet  layers/ethernet.go:42-55  (EthernetType < 0x0600: Length, LLC)
+//   Dot1Q     layers/dot1q.go:28-41     (the tag control word, Type)
+//   IPv4      layers/ip4.go:178-271     (Length 0 = the slice's length, TSO)
+//   IPv6      layers/ip6.go:221-278
+//   TCP       layers/tcp.go:292-313
+//   UDP       layers/udp.go:30-43
+#include <hip/hip_runtime.h>
+
+#include "../../include/gpk.h"
+
+namespace {
+
+constexpr uint32_t kBlock = 256;
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// 4 bytes at p in memory order (little-endian value), any alignment.
+__device__ __forceinline__ uint32_t ldu32(const uint8_t* p) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+  const uint32_t* q = reinterpret_cast<const uint32_t*>(a & ~static_cast<uintptr_t>(3));
+  return __builtin_amdgcn_alignbyte(q[1], q[0], (uint32_t)(a & 3));
+}
+__device__ __forceinline__ uint32_t be16(const uint8_t* p) {
+  const uint32_t w = ldu32(p);
+  return (w & 0xffu) << 8 | (w >> 8 & 0xffu);
+}
+__device__ __forceinline__ uint32_t be32(const uint8_t* p) { return __builtin_bswap32(ldu32(p)); }
+
+// Header bytes of one packet: the 16-byte-aligned run of kWin chunks holding
+// its first bytes sits in the lane's LDS slot (one round trip of wide loads
+// instead of a dword pair per field); a field past the run (long IPv6
+// extension chains) is read from memory.
+constexpr uint32_t kWin = 6;               // chunks: 81..96 packet bytes
+constexpr uint32_t kSlotDw = 4 * kWin + 1;  // odd stride: lanes at equal offsets on distinct banks
+constexpr uint32_t kWaveDw = 64 * 32;       // LDS per wave: its 64 windows, later its 64 records (8 KiB)
+static_assert(64 * kSlotDw <= kWaveDw, "the windows fit the record staging area");
+extern __shared__ uint32_t fields_smem[];
+typedef uint32_t u32_ua __attribute__((aligned(1)));
+
+struct Hdr {
+  const uint8_t* pk;  // packet byte 0 in memory
+  uint32_t lb;        // byte offset of packet byte 0 in fields_smem
+  uint32_t win;       // packet bytes [0, win) are in LDS
+  __device__ __forceinline__ uint32_t u32(uint32_t p) const {  // 4 bytes at packet byte p, memory order
+    if (p + 4 <= win)  // an unaligned ds_read_b32 (exact at any byte address on gfx950)
+      return *reinterpret_cast<const u32_ua*>(reinterpret_cast<const uint8_t*>(fields_smem) + lb + p);
+    return ldu32(pk + p);
+  }
+  __device__ __forceinline__ uint32_t be16(uint32_t p) const {
+    const uint32_t w = u32(p);
+    return (w & 0xffu) << 8 | (w >> 8 & 0xffu);
+  }
+  __device__ __forceinline__ uint32_t be32(uint32_t p) const { return __builtin_bswap32(u32(p)); }
+};
+
+__global__ __launch_bounds__(kBlock) void fields_kernel(const uint8_t* data, const uint64_t* offsets,
+                                                        const uint32_t* caplens, const gpk_layout* layouts, uint64_t n,
+                                                        gpk_fields* out) {
+  const uint64_t i0 = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  const bool active = i0 < n;
+  const uint64_t i = active ? i0 : n - 1;  // lanes past the batch redo the last packet, store nothing
+  const uint64_t off = offsets[i];
+  const uint32_t cl = caplens[i];
+  const uint4* lp = reinterpret_cast<const uint4*>(layouts + i);
+  const uint4 s0 = lp[0], s1 = lp[1], e0 = lp[2], e1 = lp[3];
+  // the window: chunks past the packet re-read its last one (valid bytes)
+  const uint32_t m = (uint32_t)(off & 15), win = cl < 16 * kWin - m ? cl : 16 * kWin - m;
+  const uint32_t nch = (m + win + 15) >> 4, last = nch ? nch - 1 : 0;
+  const uint8_t* wb = data + (off - m);
+  const uint32_t lane = threadIdx.x & 63, wbase = (threadIdx.x >> 6) * kWaveDw;
+  const uint32_t slot = wbase + lane * kSlotDw;
+  u32x4 c[kWin];
+#pragma unroll
+  for (uint32_t k = 0; k < kWin; k++) c[k] = *reinterpret_cast<const u32x4*>(wb + 16 * (k < last ? k : last));
+#pragma unroll
+  for (uint32_t k = 0; k < kWin; k++) {
+    fields_smem[slot + 4 * k + 0] = c[k].x;
+    fields_smem[slot + 4 * k + 1] = c[k].y;
+    fields_smem[slot + 4 * k + 2] = c[k].z;
+    fields_smem[slot + 4 * k + 3] = c[k].w;
+  }
+  const Hdr h{data + off, slot * 4 + m, nch ? win : 0u};
+  const uint32_t st[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+  const uint32_t en[8] = {e0.x, e0.y, e0.z, e0.w, e1.x, e1.y, e1.z, e1.w};
+  uint32_t w[32];
+#pragma unroll
+  for (int k = 0; k < 32; k++) w[k] = 0;
+#pragma unroll
+  for (int k = 0; k < 8; k++) w[0] |= (st[k] != GPK_LAYOUT_ABSENT ? 1u : 0u) << k;
+  if (st[GPK_DEC_ETHERNET - 1] != GPK_LAYOUT_ABSENT) {  // ethernet.go:46-55
+    const uint32_t d = st[GPK_DEC_ETHERNET - 1];
+    uint32_t et = h.be16(d + 12), len = 0;
+    if (et < 0x0600) {
+      len = et;
+      et = 0;  // EthernetTypeLLC
+    }
+    w[1] = et | len << 16;
+    w[2] = h.u32(d);  // DstMAC, SrcMAC: bytes 8..19 of the record
+    w[3] = h.u32(d + 4);
+    w[4] = h.u32(d + 8);
+  }
+  if (st[GPK_DEC_DOT1Q - 1] != GPK_LAYOUT_ABSENT) {  // dot1q.go:33-37
+    const uint32_t d = st[GPK_DEC_DOT1Q - 1];
+    w[5] = h.be16(d) | h.be16(d + 2) << 16;
+  }
+  if (st[GPK_DEC_IPV4 - 1] != GPK_LAYOUT_ABSENT) {  // ip4.go:183-193, 257-267
+    const uint32_t d = st[GPK_DEC_IPV4 - 1];
+    const uint32_t b0 = h.u32(d);  // bytes 0..3
+    uint32_t length = (b0 >> 16 & 0xffu) << 8 | b0 >> 24;
+    if (length == 0) length = (en[GPK_DEC_IPV4 - 1] - d) & 0xffffu;
+    const uint32_t b4 = h.u32(d + 4), b8 = h.u32(d + 8);  // Id, flags|frag; TTL, Protocol, Checksum
+    w[6] = (b0 & 0xffu) >> 4 | (b0 & 0x0fu) << 8 | (b0 >> 8 & 0xffu) << 16 | (b8 & 0xffu) << 24;
+    w[7] = length | ((b4 & 0xffu) << 8 | (b4 >> 8 & 0xffu)) << 16;
+    w[8] = ((b4 >> 16 & 0xffu) << 8 | b4 >> 24) | (b8 >> 8 & 0xffu) << 16;
+    w[9] = (b8 >> 16 & 0xffu) << 8 | b8 >> 24;
+    w[12] = h.u32(d + 12);
+    w[13] = h.u32(d + 16);
+  }
+  if (st[GPK_DEC_IPV6 - 1] != GPK_LAYOUT_ABSENT) {  // ip6.go:225-234
+    const uint32_t d = st[GPK_DEC_IPV6 - 1];
+    const uint32_t h0 = h.be32(d), b4 = h.u32(d + 4);
+    w[8] |= (h0 >> 28) << 24;                                          // Version
+    w[9] |= (h0 >> 20 & 0xffu) << 16 | (b4 >> 16 & 0xffu) << 24;        // TrafficClass, NextHeader
+    w[10] = h0 & 0x000fffffu;                                          // FlowLabel
+    w[11] = ((b4 & 0xffu) << 8 | (b4 >> 8 & 0xffu)) | (b4 >> 24) << 16;  // Length, HopLimit
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      w[14 + k] = h.u32(d + 8 + 4 * k);
+      w[18 + k] = h.u32(d + 24 + 4 * k);
+    }
+  }
+  if (st[GPK_DEC_TCP - 1] != GPK_LAYOUT_ABSENT) {  // tcp.go:296-313
+    const uint32_t d = st[GPK_DEC_TCP - 1];
+    const uint32_t b0 = h.u32(d), b12 = h.u32(d + 12);  // ports; DataOffset|NS, flags, Window
+    w[11] |= (b12 & 0xffu) >> 4 << 24;
+    w[22] = ((b0 & 0xffu) << 8 | (b0 >> 8 & 0xffu)) | ((b0 >> 16 & 0xffu) << 8 | b0 >> 24) << 16;
+    w[23] = h.be32(d + 4);
+    w[24] = h.be32(d + 8);
+    w[25] = (b12 >> 8 & 0xffu) | (b12 & 1u) << 8 | ((b12 >> 16 & 0xffu) << 8 | b12 >> 24) << 16;
+    w[26] = h.be16(d + 16) | h.be16(d + 18) << 16;
+  }
+  if (st[GPK_DEC_UDP - 1] != GPK_LAYOUT_ABSENT) {  // udp.go:34-41
+    const uint32_t d = st[GPK_DEC_UDP - 1];
+    const uint32_t b0 = h.u32(d), b4 = h.u32(d + 4);
+    w[27] = ((b0 & 0xffu) << 8 | (b0 >> 8 & 0xffu)) | ((b0 >> 16 & 0xffu) << 8 | b0 >> 24) << 16;
+    w[28] = ((b4 & 0xffu) << 8 | (b4 >> 8 & 0xffu)) | ((b4 >> 16 & 0xffu) << 8 | b4 >> 24) << 16;
+  }
+  // Records out through LDS: lane l's 128 bytes go to the wave's staging area
+  // (chunk c at chunk position c ^ (l & 7), spreading the banks), then store
+  // k of the wave writes its 1 KiB of records contiguously (coalesced), lane l
+  // carrying chunk l & 7 of record 8k + l / 8. The wave's window reads above
+  // precede these writes in its LDS instruction order.
+  asm volatile("" ::: "memory");
+#pragma unroll
+  for (uint32_t c = 0; c < 8; c++)
+    *reinterpret_cast<u32x4*>(fields_smem + wbase + lane * 32 + 4 * (c ^ (lane & 7))) =
+        u32x4{w[4 * c], w[4 * c + 1], w[4 * c + 2], w[4 * c + 3]};
+  asm volatile("" ::: "memory");
+  const uint64_t first = (uint64_t)blockIdx.x * kBlock + (threadIdx.x & ~63u);  // the wave's first packet
+  u32x4* o = reinterpret_cast<u32x4*>(out + first);
+#pragma unroll
+  for (uint32_t k = 0; k < 8; k++) {
+    const uint32_t r = 8 * k + (lane >> 3), c = lane & 7;
+    const u32x4 v = *reinterpret_cast<const u32x4*>(fields_smem + wbase + r * 32 + 4 * (c ^ (r & 7)));
+    if (first + r < n) __builtin_nontemporal_store(v, o + 64 * k + lane);
+  }
+}
+
+}  // namespace
+
+static_assert(sizeof(gpk_fields) == 128, "gpk_fields is 128 bytes");
+static_assert(offsetof(gpk_fields, tcp_seq) == 92 && offsetof(gpk_fields, udp_checksum) == 114, "gpk_fields layout");
+
+extern "C" int gpk_extract_fields(const gpk_batch* b, const gpk_layout* layouts, gpk_fields* fields, void* stream) {
+  if (!b || (b->n && (!b->data || !b->offsets || !b->caplens || !layouts || !fields))) return GPK_EINVAL;
+  if (!b->n) return GPK_OK;
+  const uint64_t blocks = (b->n + kBlock - 1) / kBlock;
+  if (blocks > 0xffffffffull) return GPK_EINVAL;
+  hipLaunchKernelGGL(fields_kernel, dim3((unsigned)blocks), dim3(kBlock), (kBlock / 64) * kWaveDw * 4, (hipStream_t)stream,
+                     b->data, b->offsets, b->caplens, layouts, b->n, fields);
+  return hipGetLastError() == hipSuccess ? GPK_OK : GPK_EHIP;
+}

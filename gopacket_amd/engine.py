@@ -112,13 +112,45 @@ class Context:
         r = _lib.Results(records.data_ptr(), err_args.data_ptr() if err_args is not None else None,
                          flows.data_ptr() if flows is not None else None,
                          layouts.data_ptr() if layouts is not None else None)
-        if stream is None:
-            sp = None
-        elif isinstance(stream, int):
-            sp = stream
-        else:
-            sp = stream.cuda_stream
-        check(lib().gpk_decode_batch(self.h, parser.h, ctypes.byref(b), ctypes.byref(r), sp))
+        check(lib().gpk_decode_batch(self.h, parser.h, ctypes.byref(b), ctypes.byref(r), _stream_ptr(stream)))
+
+    def extract_fields(self, data, offsets, caplens, layouts, fields, stream=None):
+        """gpk_extract_fields: the layer fields (include/gpk.h gpk_fields, 128
+        bytes per packet; FIELDS_DTYPE) of a device batch from the layouts a
+        decode_device of it wrote. Device tensors; enqueued on `stream`."""
+        n = offsets.numel()
+        if fields.numel() * fields.element_size() < 128 * n or layouts.numel() * layouts.element_size() < 64 * n:
+            raise ValueError("fields needs 128 bytes and layouts 64 bytes per packet")
+        b = _lib.Batch(data.data_ptr(), offsets.data_ptr(), caplens.data_ptr(), n, data.numel())
+        check(lib().gpk_extract_fields(ctypes.byref(b), layouts.data_ptr(), fields.data_ptr(), _stream_ptr(stream)))
+
+    def decode_host_fields(self, parser, data, offsets, caplens):
+        """decode_host with layouts, plus the layer fields of every packet, both
+        computed on the device (host arrays in and out; torch for the buffers)."""
+        import torch
+        data = np.ascontiguousarray(data, dtype=np.uint8)
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        caplens = np.ascontiguousarray(caplens, dtype=np.uint32)
+        n = len(offsets)
+        if n and np.any(offsets + caplens.astype(np.uint64) > len(data)):
+            raise ValueError("packet range outside the data buffer")
+        dev = torch.device("cuda", self.device)
+        d_data = torch.zeros(len(data) + 32, dtype=torch.uint8, device=dev)  # 16-byte slack after the packets
+        d_data[:len(data)] = torch.from_numpy(data).to(dev)
+        d_off = torch.from_numpy(offsets.view(np.int64)).to(dev)
+        d_cap = torch.from_numpy(caplens.view(np.int32)).to(dev)
+        rec = torch.empty(n * 16, dtype=torch.uint8, device=dev)
+        err = torch.zeros(2 * n, dtype=torch.int32, device=dev)
+        fl = torch.zeros(3 * n, dtype=torch.int64, device=dev)
+        lay = torch.empty(n * 64, dtype=torch.uint8, device=dev)
+        fields = torch.empty(n * 128, dtype=torch.uint8, device=dev)
+        stream = torch.cuda.current_stream(dev)
+        self.decode_device(parser, d_data, d_off, d_cap, rec, err, fl, lay, stream=stream)
+        self.extract_fields(d_data, d_off, d_cap, lay, fields, stream=stream)
+        torch.cuda.synchronize(dev)
+        return (dict(records=rec.cpu().numpy().view(_lib.RECORD_DTYPE), err_args=err.cpu().numpy().view(np.uint32),
+                     flows=fl.cpu().numpy().view(np.uint64), layouts=lay.cpu().numpy().view(_lib.LAYOUT_DTYPE)),
+                fields.cpu().numpy().view(_lib.FIELDS_DTYPE))
 
     def kernel_name(self, parser, data, offsets, caplens, layouts=False):
         """The decode kernel specialisation decode_device launches for this
@@ -191,6 +223,15 @@ class Context:
         pkt = bytes(pkt)
         check(lib().gpk_decoded_list_host(self.h, parser.h, pkt, len(pkt), out, cap, ctypes.byref(n)))
         return [out[i] for i in range(min(n.value, cap))]
+
+
+def _stream_ptr(stream):
+    """A raw hipStream_t from a torch stream, an int handle or None."""
+    if stream is None:
+        return None
+    if isinstance(stream, int):
+        return stream
+    return stream.cuda_stream
 
 
 def format_error(code, a0=0, a1=0):

@@ -308,8 +308,16 @@ class DecodingLayerParser:
         res = self.DecodeBatch(batch, layouts=True)
         return res.Hydrate(0, decoded)
 
-    def DecodeBatch(self, batch, layouts=False, outputs=_lib.OUT_ALL):
+    def DecodeBatch(self, batch, layouts=False, outputs=_lib.OUT_ALL, fields=False):
+        """DecodeLayers for every packet of the batch on the device. fields=True
+        also returns each packet's scalar layer fields computed on the device
+        (gpk_extract_fields; implies layouts): BatchResult.fields, FIELDS_DTYPE."""
         cfg = self._config(outputs)
+        if fields:
+            r, f = self.ctx().decode_host_fields(cfg, batch.data, batch.offsets, batch.caplens)
+            res = BatchResult(self, batch, r)
+            res.fields = f
+            return res
         r = self.ctx().decode_host(cfg, batch.data, batch.offsets, batch.caplens, layouts=layouts)
         return BatchResult(self, batch, r)
 
@@ -325,6 +333,7 @@ class BatchResult:
         self.parser, self.batch = parser, batch
         self.records, self.err_args, self.flows, self.layouts = r["records"], r["err_args"], r["flows"], \
             r["layouts"]
+        self.fields = None  # FIELDS_DTYPE per packet when decoded with fields=True
 
     def __len__(self):
         return len(self.records)

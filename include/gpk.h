@@ -30,6 +30,11 @@
  *                                          layers/udp.go:132)
  *   gpk_decode_batch_host                  the same, starting and ending in host memory
  *                                          (pcap/afpacket sources hand over host buffers)
+ *   gpk_extract_fields                     the scalar fields the six decoders' DecodeFromBytes set
+ *                                          on their structs (layers/ethernet.go:42-55,
+ *                                          dot1q.go:28-41, ip4.go:178-271, ip6.go:221-278,
+ *                                          tcp.go:292-313, udp.go:30-43), from the layouts of a
+ *                                          decode: the fields a consumer reads after DecodeLayers
  *   gpk_format_error                       the error values DecodeLayers returns
  *                                          (UnsupportedLayerType parser.go:321-327, panicToError
  *                                          :329-333, and every fmt.Errorf/errors.New site of
@@ -194,6 +199,59 @@ typedef struct gpk_layout {
 } gpk_layout;
 #define GPK_LAYOUT_ABSENT 0xFFFFFFFFu
 
+/* ---- optional per-packet layer fields (128 B) -----------------------------
+ * The scalar fields the decoders' DecodeFromBytes set on their structs, read
+ * from the bytes of each decoder's last successful slice (the gpk_layout of a
+ * gpk_decode_batch with layouts), so a consumer that reads layer fields after
+ * DecodeLayers gets them from the device instead of decoding headers again.
+ * present: bit k set = layout slot k holds a slice (k = GPK_DEC_* - 1; Payload
+ * and Fragment share slot 7); every field of an absent layer is 0. Integers in
+ * host byte order; MACs and addresses as their bytes. Variable-length parts
+ * (IPv4 / TCP options, HopByHop options, Payload) stay in the packet bytes at
+ * the layout's range.                                                         */
+typedef struct gpk_fields {
+  uint32_t present;          /*   0                                                       */
+  uint16_t eth_type;         /*   4 Ethernet.EthernetType (EthernetTypeLLC = 0 below 0x0600) */
+  uint16_t eth_length;       /*   6 Ethernet.Length (802.3 frames, else 0)               */
+  uint8_t eth_dst[6];        /*   8 Ethernet.DstMAC                                       */
+  uint8_t eth_src[6];        /*  14 Ethernet.SrcMAC                                       */
+  uint16_t d1q_tci;          /*  20 Dot1Q Priority << 13 | DropEligible << 12 | VLANIdentifier */
+  uint16_t d1q_type;         /*  22 Dot1Q.Type                                            */
+  uint8_t ip4_version;       /*  24 IPv4.Version                                          */
+  uint8_t ip4_ihl;           /*  25 IPv4.IHL                                              */
+  uint8_t ip4_tos;           /*  26 IPv4.TOS                                              */
+  uint8_t ip4_ttl;           /*  27 IPv4.TTL                                              */
+  uint16_t ip4_length;       /*  28 IPv4.Length (the slice's length when the field is 0: TSO) */
+  uint16_t ip4_id;           /*  30 IPv4.Id                                               */
+  uint16_t ip4_flags_frag;   /*  32 IPv4.Flags << 13 | IPv4.FragOffset                    */
+  uint8_t ip4_protocol;      /*  34 IPv4.Protocol                                         */
+  uint8_t ip6_version;       /*  35 IPv6.Version                                          */
+  uint16_t ip4_checksum;     /*  36 IPv4.Checksum                                         */
+  uint8_t ip6_traffic_class; /*  38 IPv6.TrafficClass                                     */
+  uint8_t ip6_next_header;   /*  39 IPv6.NextHeader                                       */
+  uint32_t ip6_flow_label;   /*  40 IPv6.FlowLabel                                        */
+  uint16_t ip6_length;       /*  44 IPv6.Length (0 for a jumbogram)                       */
+  uint8_t ip6_hop_limit;     /*  46 IPv6.HopLimit                                         */
+  uint8_t tcp_data_offset;   /*  47 TCP.DataOffset                                        */
+  uint8_t ip4_src[4];        /*  48 IPv4.SrcIP                                            */
+  uint8_t ip4_dst[4];        /*  52 IPv4.DstIP                                            */
+  uint8_t ip6_src[16];       /*  56 IPv6.SrcIP                                            */
+  uint8_t ip6_dst[16];       /*  72 IPv6.DstIP                                            */
+  uint16_t tcp_src_port;     /*  88 TCP.SrcPort                                           */
+  uint16_t tcp_dst_port;     /*  90 TCP.DstPort                                           */
+  uint32_t tcp_seq;          /*  92 TCP.Seq                                               */
+  uint32_t tcp_ack;          /*  96 TCP.Ack                                               */
+  uint16_t tcp_flags;        /* 100 FIN 1 SYN 2 RST 4 PSH 8 ACK 16 URG 32 ECE 64 CWR 128 NS 256 */
+  uint16_t tcp_window;       /* 102 TCP.Window                                            */
+  uint16_t tcp_checksum;     /* 104 TCP.Checksum                                          */
+  uint16_t tcp_urgent;       /* 106 TCP.Urgent                                            */
+  uint16_t udp_src_port;     /* 108 UDP.SrcPort                                           */
+  uint16_t udp_dst_port;     /* 110 UDP.DstPort                                           */
+  uint16_t udp_length;       /* 112 UDP.Length                                            */
+  uint16_t udp_checksum;     /* 114 UDP.Checksum                                          */
+  uint8_t reserved[12];      /* 116 zero                                                  */
+} gpk_fields;
+
 /* ---- outputs -------------------------------------------------------------- */
 #define GPK_OUT_IP4_CSUM 0x1u  /* IPv4.VerifyChecksum for the last IPv4 in decoded        */
 #define GPK_OUT_L4_CSUM 0x2u   /* TCP/UDP.VerifyChecksum, pseudo-header = last network layer */
@@ -276,6 +334,11 @@ typedef struct gpk_results {
  * launch. The parser configuration is uploaded once per (ctx, parser change). */
 int gpk_decode_batch(gpk_ctx* ctx, const gpk_parser* p, const gpk_batch* batch,
                      const gpk_results* out, void* stream);
+
+/* Layer fields of every packet of a device batch from the layouts a
+ * gpk_decode_batch with layouts wrote for it (device memory; fields[n] device
+ * memory), enqueued on `stream`. Asynchronous. The batch is the one decoded. */
+int gpk_extract_fields(const gpk_batch* batch, const gpk_layout* layouts, gpk_fields* fields, void* stream);
 
 /* Diagnostic: the name of the kernel specialisation gpk_decode_batch launches
  * for this parser and batch (with or without layouts), e.g.

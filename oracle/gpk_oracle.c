@@ -786,6 +786,86 @@ static void decode_packet(const oracle_config* c, const uint8_t* pkt, uint32_t c
   }
 }
 
+/* ---- layer fields (gpk_extract_fields) ------------------------------------ */
+/* The field assignments of each DecodeFromBytes, applied to the slice the
+ * layout records for the decoder (the slice of its last successful call). */
+static void fields_of(const uint8_t* pkt, const gpk_layout* lay, gpk_fields* f) {
+  memset(f, 0, sizeof(*f));
+  for (int k = 0; k < 8; k++)
+    if (lay->start[k] != GPK_LAYOUT_ABSENT) f->present |= 1u << k;
+  if (lay->start[GPK_DEC_ETHERNET - 1] != GPK_LAYOUT_ABSENT) { /* ethernet.go:46-55 */
+    const uint8_t* d = pkt + lay->start[GPK_DEC_ETHERNET - 1];
+    memcpy(f->eth_dst, d, 6);
+    memcpy(f->eth_src, d + 6, 6);
+    f->eth_type = be16(d + 12);
+    f->eth_length = 0;
+    if (f->eth_type < 0x0600) {
+      f->eth_length = f->eth_type;
+      f->eth_type = 0; /* EthernetTypeLLC, enums.go:36 */
+    }
+  }
+  if (lay->start[GPK_DEC_DOT1Q - 1] != GPK_LAYOUT_ABSENT) { /* dot1q.go:33-37 */
+    const uint8_t* d = pkt + lay->start[GPK_DEC_DOT1Q - 1];
+    const uint16_t priority = (d[0] & 0xE0) >> 5, de = (d[0] & 0x10) != 0, vid = be16(d) & 0x0FFF;
+    f->d1q_tci = (uint16_t)(priority << 13 | de << 12 | vid);
+    f->d1q_type = be16(d + 2);
+  }
+  if (lay->start[GPK_DEC_IPV4 - 1] != GPK_LAYOUT_ABSENT) { /* ip4.go:183-193, 257-267 */
+    const uint32_t s = lay->start[GPK_DEC_IPV4 - 1];
+    const uint8_t* d = pkt + s;
+    f->ip4_length = be16(d + 2);
+    f->ip4_ihl = d[0] & 0x0F;
+    if (f->ip4_length == 0) f->ip4_length = (uint16_t)(lay->end[GPK_DEC_IPV4 - 1] - s); /* TSO: uint16(len(data)) */
+    const uint16_t flagsfrags = be16(d + 6);
+    f->ip4_version = d[0] >> 4;
+    f->ip4_tos = d[1];
+    f->ip4_id = be16(d + 4);
+    f->ip4_flags_frag = (uint16_t)((flagsfrags >> 13) << 13 | (flagsfrags & 0x1FFF));
+    f->ip4_ttl = d[8];
+    f->ip4_protocol = d[9];
+    f->ip4_checksum = be16(d + 10);
+    memcpy(f->ip4_src, d + 12, 4);
+    memcpy(f->ip4_dst, d + 16, 4);
+  }
+  if (lay->start[GPK_DEC_IPV6 - 1] != GPK_LAYOUT_ABSENT) { /* ip6.go:225-234 */
+    const uint8_t* d = pkt + lay->start[GPK_DEC_IPV6 - 1];
+    f->ip6_version = d[0] >> 4;
+    f->ip6_traffic_class = (uint8_t)((be16(d) >> 4) & 0x00FF);
+    f->ip6_flow_label = be32(d) & 0x000FFFFF;
+    f->ip6_length = be16(d + 4);
+    f->ip6_next_header = d[6];
+    f->ip6_hop_limit = d[7];
+    memcpy(f->ip6_src, d + 8, 16);
+    memcpy(f->ip6_dst, d + 24, 16);
+  }
+  if (lay->start[GPK_DEC_TCP - 1] != GPK_LAYOUT_ABSENT) { /* tcp.go:296-313 */
+    const uint8_t* d = pkt + lay->start[GPK_DEC_TCP - 1];
+    f->tcp_src_port = be16(d);
+    f->tcp_dst_port = be16(d + 2);
+    f->tcp_seq = be32(d + 4);
+    f->tcp_ack = be32(d + 8);
+    f->tcp_data_offset = d[12] >> 4;
+    f->tcp_flags = (uint16_t)((d[13] & 0x01 ? 1 : 0) | (d[13] & 0x02 ? 2 : 0) | (d[13] & 0x04 ? 4 : 0) |
+                              (d[13] & 0x08 ? 8 : 0) | (d[13] & 0x10 ? 16 : 0) | (d[13] & 0x20 ? 32 : 0) |
+                              (d[13] & 0x40 ? 64 : 0) | (d[13] & 0x80 ? 128 : 0) | (d[12] & 0x01 ? 256 : 0));
+    f->tcp_window = be16(d + 14);
+    f->tcp_checksum = be16(d + 16);
+    f->tcp_urgent = be16(d + 18);
+  }
+  if (lay->start[GPK_DEC_UDP - 1] != GPK_LAYOUT_ABSENT) { /* udp.go:34-41 */
+    const uint8_t* d = pkt + lay->start[GPK_DEC_UDP - 1];
+    f->udp_src_port = be16(d);
+    f->udp_dst_port = be16(d + 2);
+    f->udp_length = be16(d + 4);
+    f->udp_checksum = be16(d + 6);
+  }
+}
+
+void oracle_extract_fields(const uint8_t* data, const uint64_t* offsets, const gpk_layout* layouts, uint64_t n,
+                           gpk_fields* out) {
+  for (uint64_t i = 0; i < n; i++) fields_of(data + offsets[i], &layouts[i], &out[i]);
+}
+
 typedef struct {
   const oracle_config* c;
   const uint8_t* data;

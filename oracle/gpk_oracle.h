@@ -53,6 +53,12 @@ void oracle_decode_batch(const oracle_config* c, const uint8_t* data, const uint
                          const uint32_t* caplens, uint64_t n, gpk_record* records,
                          uint32_t* err_args, uint64_t* flows, gpk_layout* layouts, int nthreads);
 
+/* The scalar layer fields (include/gpk.h gpk_fields) of packets [0, n) from
+ * the layouts of a decode: each decoder's DecodeFromBytes field assignments
+ * restated on its slice. */
+void oracle_extract_fields(const uint8_t* data, const uint64_t* offsets, const gpk_layout* layouts, uint64_t n,
+                           gpk_fields* out);
+
 /* Full decoded LayerType list of one packet; returns its length (may exceed cap). */
 uint32_t oracle_decoded_list(const oracle_config* c, const uint8_t* pkt, uint32_t caplen,
                              int64_t* out, uint32_t cap);

@@ -15,6 +15,8 @@ _LIB = None
 RECORD_DTYPE = np.dtype([("layers", "<u8"), ("status", "<u4"), ("ip4_csum", "<u2"), ("l4_csum", "<u2")])
 LAYOUT_DTYPE = np.dtype([("start", "<u4", (8,)), ("end", "<u4", (8,))])
 
+FIELDS_ITEMSIZE = 128  # include/gpk.h gpk_fields
+
 # decoder kinds (include/gpk.h GPK_DEC_*)
 DEC = dict(ETHERNET=1, DOT1Q=2, IPV4=3, IPV6=4, IPV6_EXT=5, TCP=6, UDP=7, PAYLOAD=8, FRAGMENT=9)
 
@@ -157,6 +159,21 @@ def bpf_batch(insns, data, offsets, caplens, wirelens=None):
     L.oracle_bpf_batch(prog.ctypes.data, len(prog), data.ctypes.data, offsets.ctypes.data, caplens.ctypes.data,
                        w.ctypes.data if w is not None else None, len(offsets), ret.ctypes.data)
     return ret
+
+
+def extract_fields(data, offsets, layouts):
+    """oracle_extract_fields: the gpk_fields records (raw bytes, n x 128) of the
+    packets from the layouts of a decode."""
+    L = lib()
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+    layouts = np.ascontiguousarray(layouts)
+    n = len(offsets)
+    out = np.zeros((n, FIELDS_ITEMSIZE), np.uint8)
+    L.oracle_extract_fields.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                                        ctypes.c_void_p]
+    L.oracle_extract_fields(data.ctypes.data, offsets.ctypes.data, layouts.ctypes.data, n, out.ctypes.data)
+    return out
 
 
 def group_batch(kind, data, offsets, records, layouts, flows=None, buckets=8):
