@@ -797,7 +797,6 @@ __device__ __forceinline__ uint32_t segment_sums(const KParams& P, Stream<D>& S,
 // before its packet's first granule and at its last granule; after the parse
 // the segment's sum is that packet sum minus the bytes before s and after e,
 // which lie in the header windows (or come from memory).
-constexpr int kSbStride = 24;  // LDS dwords per lane: 6 whole 16-byte cells (the LDS-DMA layout)
 struct SbPkt {
   uint32_t L;   // L-form sum of the packet's granules [a, b]
   uint64_t R0;  // region base (batch offset, 16-byte aligned)
@@ -859,10 +858,10 @@ __device__ __forceinline__ uint32_t sb_stream(const KParams& P, Stream<D>& S, ui
 // stream-before-parse lane: its own window chunk, the next packet's first chunk, or
 // memory.
 __device__ __forceinline__ u32x4 sb_chunk(const KParams& P, uint64_t ga, uint64_t wb, uint32_t nch, uint32_t slot_dw,
-                                          bool next_here, uint64_t nwb) {
+                                          bool next_here, uint64_t nwb, uint32_t stride) {
   const uint64_t k = (ga - wb) >> 4;
   if (ga >= wb && k < nch) return lds_chunk(slot_dw * 4 + 16u * (uint32_t)k);
-  if (next_here && ga == nwb) return lds_chunk((slot_dw + kSbStride) * 4);
+  if (next_here && ga == nwb) return lds_chunk((slot_dw + stride) * 4);
   return *reinterpret_cast<const u32x4*>(P.data + ga);
 }
 
@@ -1047,7 +1046,7 @@ __device__ __forceinline__ void decode_packet(const KParams& P, const TT& T, uin
         if (!own && !nxt) c = *reinterpret_cast<const u32x4*>(P.data + gj);
         L -= chunk_l(c, 0u) - chunk_l_below(c, (uint32_t)(je & 15), 0u);
         for (uint64_t ga = gj + 16; ga < gend; ga += 16)
-          L -= chunk_l(sb_chunk(P, ga, g.wb, nch, slot_dw, next_here, nwb), 0u);
+          L -= chunk_l(sb_chunk(P, ga, g.wb, nch, slot_dw, next_here, nwb, kSlotStride), 0u);
       }
       const uint32_t sum = l_to_words(L, (uint32_t)js & 1u);
       l4c = fold(jinit + sum - jexist);
@@ -1216,10 +1215,10 @@ __device__ __forceinline__ void window_dma(const KParams& P, const WinGeo& g, ui
   }
 }
 
-template <bool kCompact, int O>
+template <bool kCompact, int O, int W = 6>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(O, 8))) void decode_sb_kernel(KParams P) {
-  constexpr int W = 6, D = GPK_SB_DEPTH;
-  static_assert(kSbStride == 4 * W, "one 16-byte cell per window chunk, no pad");
+  constexpr int D = GPK_SB_DEPTH;
+  constexpr int kSbStride = 4 * W;  // one 16-byte cell per window chunk, no pad
   const uint32_t tid = threadIdx.x, lane = tid & 63;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const uint32_t base = kBlock * kSbStride;  // table blob (dwords)
@@ -1341,15 +1340,15 @@ hipError_t launch(const gpk::KParams* P, hipStream_t stream, int* occ) {
   return hipGetLastError();
 }
 
-template <bool kCompact, int O>
+template <bool kCompact, int O, int W = 6>
 hipError_t launch_sb(const gpk::KParams* P, hipStream_t stream, int* occ) {
   using namespace gpk;
-  constexpr int fixed = kBlock * kSbStride * 4;
+  constexpr int fixed = kBlock * 4 * W * 4;
   const int lds = kCompact ? fixed + (int)((P->cg.words + GPK_BLOB_ROUND - 1) & ~(GPK_BLOB_ROUND - 1u)) * 4 : fixed;
-  if (occ) return resident_blocks(decode_sb_kernel<kCompact, O>, lds, occ);
+  if (occ) return resident_blocks(decode_sb_kernel<kCompact, O, W>, lds, occ);
   const uint64_t grid = (P->n + kBlock - 1) / kBlock;
   if (grid > 0xffffffffull) return hipErrorInvalidValue;
-  hipLaunchKernelGGL((decode_sb_kernel<kCompact, O>), dim3((unsigned)grid), dim3(kBlock), lds, stream, *P);
+  hipLaunchKernelGGL((decode_sb_kernel<kCompact, O, W>), dim3((unsigned)grid), dim3(kBlock), lds, stream, *P);
   return hipGetLastError();
 }
 
