@@ -91,6 +91,9 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 #ifndef GPK_SB_BIG
 #define GPK_SB_BIG 0  // ... for big-packet batches too (C3: +1.2 %, not used)
 #endif
+#ifndef GPK_SB_WAVES
+#define GPK_SB_WAVES GPK_SMALL_WAVES  // ... its register budget (waves per SIMD; LDS allows 6 blocks per CU)
+#endif
 #ifndef GPK_SB_DEPTH
 #define GPK_SB_DEPTH 6  // ... its stream depth (passes in flight; 8 no better)
 #endif
@@ -1382,7 +1385,7 @@ hipError_t launch_sel(const gpk::KParams* P, const Sel& s, hipStream_t stream, i
   constexpr int W = gpk::kWinChunks;
   if (s.sb)
     return s.O == GPK_WAVES_PER_EU ? launch_sb<kCompact, GPK_WAVES_PER_EU>(P, stream, occ)
-                                   : launch_sb<kCompact, GPK_SMALL_WAVES>(P, stream, occ);
+                                   : launch_sb<kCompact, GPK_SB_WAVES>(P, stream, occ);
   if (s.keys)
     return s.l4 ? launch<true, false, kCompact, true>(P, stream, occ) : launch<false, false, kCompact, true>(P, stream, occ);
   if (s.W == 4) return launch<false, false, kCompact, false, 4>(P, stream, occ);
@@ -1415,7 +1418,9 @@ extern "C" hipError_t gpk_launch_occupancy(const gpk::KParams* P, int with_l4, i
 // Name of the kernel specialisation gpk_launch_decode would launch.
 extern "C" int gpk_launch_describe(const gpk::KParams* P, int with_l4, int with_layout, char* buf, size_t cap) {
   const Sel s = select(P, with_l4, with_layout);
-  if (s.sb) return snprintf(buf, cap, "gpk::decode_sb_kernel<%s,%d>", s.compact ? "true" : "false", s.O);
+  if (s.sb)
+    return snprintf(buf, cap, "gpk::decode_sb_kernel<%s,%d>", s.compact ? "true" : "false",
+                    s.O == GPK_WAVES_PER_EU ? s.O : GPK_SB_WAVES);
   return snprintf(buf, cap, "gpk::decode_kernel<%s,%s,%s,%s,%d,%d,%d>", s.l4 ? "true" : "false",
                   s.layout ? "true" : "false", s.compact ? "true" : "false", s.keys ? "true" : "false", s.W,
                   s.W == 4 ? 6 : s.O, s.AL);

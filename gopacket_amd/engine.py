@@ -89,8 +89,6 @@ class Context:
         offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
         caplens = np.ascontiguousarray(caplens, dtype=np.uint32)
         n = len(offsets)
-        if n and int(offsets.max()) + int(caplens.max()) > len(data):
-            pass  # offsets[i]+caplens[i] is checked per packet below
         if n and np.any(offsets.astype(np.uint64) + caplens.astype(np.uint64) > len(data)):
             raise ValueError("packet range outside the data buffer")
         rec = np.zeros(n, _lib.RECORD_DTYPE)
