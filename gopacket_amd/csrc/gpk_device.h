@@ -755,10 +755,19 @@ __device__ __forceinline__ Outcome run_parser(const KParams& P, const TT& T, con
 // TCP options of the straight-line path (tcp.go:336-549 for well-formed
 // option lists without MPTCP): EOL ends the list, NOP, TLVs of length >= 2
 // inside the header. False sends the packet to the general decoder.
+#ifndef GPK_FAST_SYN_OPTS
+#define GPK_FAST_SYN_OPTS 1  // the Linux SYN option block checked as a pattern (no TLV walk; A/B r12: C1 -4..-9 %)
+#endif
 template <class R>
 __device__ __forceinline__ bool tcp_options_ok(const R& rd, uint32_t off, uint32_t ds) {
   if (ds == 20) return true;
   if (ds == 32 && rd32(rd, off + 20) == 0x0101080au) return true;  // NOP, NOP, Timestamps
+#if GPK_FAST_SYN_OPTS
+  // Linux SYN: MSS (4), SACK permitted (2), Timestamps (10), NOP, window scale (3)
+  if (ds == 40 && (rd32(rd, off + 20) & 0xffff0000u) == 0x02040000u && rd32(rd, off + 24) == 0x0402080au &&
+      (rd32(rd, off + 36) & 0xffffff00u) == 0x01030300u)
+    return true;
+#endif
   for (uint32_t p = off + 20, e = off + ds; p < e;) {
     const uint32_t t = rd8(rd, p);
     if (t == 0) break;
