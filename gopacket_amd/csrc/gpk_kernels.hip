@@ -485,16 +485,24 @@ __device__ __forceinline__ int derive_key(const KParams& P, const Rd& r, const P
 // allocator believes the asm wrote the slot at once and could copy or spill
 // it while the load is in flight; every build's device code is therefore
 // checked for that (tools/check_stream_isa.py, run by the Makefile).
+#ifndef GPK_STREAM_NT
+#define GPK_STREAM_NT 1  // phase-B stream loads non-temporal
+#endif
+#if GPK_STREAM_NT
+#define GPK_SPOL " nt"
+#else
+#define GPK_SPOL ""
+#endif
 __device__ __forceinline__ void slot_load(u32x4 (&c)[kGran], __amdgpu_buffer_rsrc_t rs, uint32_t vo,
                                           uint32_t soff) {
-  asm volatile("buffer_load_dwordx4 %0, %1, %2, %3 offen nt" : "+v"(c[0]) : "v"(vo), "s"(rs), "s"(soff) : "memory");
+  asm volatile("buffer_load_dwordx4 %0, %1, %2, %3 offen" GPK_SPOL : "+v"(c[0]) : "v"(vo), "s"(rs), "s"(soff) : "memory");
   if (kGran > 1)
-    asm volatile("buffer_load_dwordx4 %0, %1, %2, %3 offen offset:16 nt"
+    asm volatile("buffer_load_dwordx4 %0, %1, %2, %3 offen offset:16" GPK_SPOL
                  : "+v"(c[kGran > 1 ? 1 : 0]) : "v"(vo), "s"(rs), "s"(soff) : "memory");
   if (kGran > 2) {
-    asm volatile("buffer_load_dwordx4 %0, %1, %2, %3 offen offset:32 nt"
+    asm volatile("buffer_load_dwordx4 %0, %1, %2, %3 offen offset:32" GPK_SPOL
                  : "+v"(c[kGran > 2 ? 2 : 0]) : "v"(vo), "s"(rs), "s"(soff) : "memory");
-    asm volatile("buffer_load_dwordx4 %0, %1, %2, %3 offen offset:48 nt"
+    asm volatile("buffer_load_dwordx4 %0, %1, %2, %3 offen offset:48" GPK_SPOL
                  : "+v"(c[kGran > 3 ? 3 : 0]) : "v"(vo), "s"(rs), "s"(soff) : "memory");
   }
 }

@@ -1,12 +1,14 @@
 // Probe: LDS-DMA (global_load_lds_dwordx4) as the persistent decode kernel uses it.
 // 4 waves; wave w issues 6 instructions k = 0..5 with M0 = its region + 1024 k and a
 // per-lane source address that gathers (packet q, chunk c) = divmod(64 k + lane, 6) of
-// 64 scattered "packets" at arbitrary 16-byte-aligned offsets. Expected: LDS byte
+// 64 scattered "packets" at arbitrary 16-byte-aligned offsets (plus argv[1]
+// bytes: 4, 8, 12 test dword-aligned sources). Expected: LDS byte
 // 96 q + 16 c + b of the wave's region = source byte 16 c + b of packet q, i.e. the
 // destination is M0 + 16 * lane whatever the source.
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdint>
+#include <cstdlib>
 #include <vector>
 
 extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
@@ -37,12 +39,13 @@ __global__ void k(const uint8_t* data, const uint64_t* pk_off, uint32_t* out) {
   for (int i = threadIdx.x; i < 4 * 1536; i += 256) out[i] = smem[i];
 }
 
-int main() {
+int main(int argc, char** argv) {
+  const int shift = argc > 1 ? atoi(argv[1]) : 0;
   const size_t nbytes = 1 << 22;
   std::vector<uint8_t> h(nbytes);
   for (size_t i = 0; i < nbytes; i++) h[i] = (uint8_t)(i * 2654435761u >> 13);
   std::vector<uint64_t> off(256);
-  for (int i = 0; i < 256; i++) off[i] = ((uint64_t)(i * 7919 + 13) * 16) % (nbytes - 256);
+  for (int i = 0; i < 256; i++) off[i] = ((uint64_t)(i * 7919 + 13) * 16) % (nbytes - 256) + shift;
   uint8_t* d;
   uint64_t* doff;
   uint32_t* dout;
@@ -59,6 +62,6 @@ int main() {
     for (int q = 0; q < 64; q++)
       for (int b = 0; b < 96; b++)
         bad += got[w * 6144 + 96 * q + b] != h[off[w * 64 + q] + b];
-  printf("LDS-DMA gather: %zu of %d bytes differ (%s)\n", bad, 4 * 6144, bad ? "FAIL" : "ok");
+  printf("LDS-DMA gather, source shift %d: %zu of %d bytes differ (%s)\n", shift, bad, 4 * 6144, bad ? "FAIL" : "ok");
   return bad != 0;
 }
