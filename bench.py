@@ -489,12 +489,14 @@ def htod_probe(total_bytes, slot_bytes=256 << 20, streams=4, reps=2):
                     streams, slot_bytes >> 20, streams, nslots * slot_bytes / 1e9))
 
 
-def c5_replay(ctx, gib=10.0, reps=2, threads=16, cpu_threads=16):
+def c5_replay(ctx, gib=10.0, reps=2, threads=8, cpu_threads=16):
     """BASELINE config C5: a pcapng of the C4 IMIX mix (~gib GiB, written once
     to $TMPDIR, in the page cache) replayed end to end by gpk_replay_file:
     file -> pinned staging slots -> record walk -> HtoD -> decode -> DtoH ->
     per-launch result callback (which counts valid checksums, as a consumer
-    would touch the results). Sampled packets are checked against the oracle."""
+    would touch the results). Sampled packets are checked against the oracle.
+    8 pread threads per slot (the library's default): on the box's 16-CPU share
+    they beat 12, 16 and 24 in alternating calls (profiles/r14_c5_threads.txt)."""
     from gopacket_amd import _lib, engine, synth
     from oracle import oracle as O
     S = _lib.synth_lib()
