@@ -58,6 +58,11 @@ CONFIGS["c4s"] = dict(CONFIGS["c4"], strong=True,
                       workload="C4 strong: one 64M IMIX batch sharded over the ranks (byte-balanced cuts)")
 
 
+# engine decoder names -> oracle decoder names
+ORACLE_DEC = {"Ethernet": "ETHERNET", "Dot1Q": "DOT1Q", "IPv4": "IPV4", "IPv6": "IPV6",
+              "IPv6ExtensionSkipper": "IPV6_EXT", "TCP": "TCP", "UDP": "UDP", "Payload": "PAYLOAD"}
+
+
 def dist_init(backend="nccl", same_device=False, force=False):
     """One process per GPU (torchrun env). backend "nccl" is RCCL on ROCm;
     "gloo" + same_device=True rehearses N ranks on one GPU (tests only).
@@ -506,7 +511,7 @@ def c5_replay(ctx, gib=10.0, reps=2, threads=8, cpu_threads=16):
     n = int(gib * 2**30 / per)
     path = os.path.join(os.environ.get("TMPDIR", "/tmp"), "gpk_c5_%d.pcapng" % os.getpid())
     t0 = time.perf_counter()
-    size = S.gpk_synth_write_pcapng(path.encode(), 4, 0, n, threads)
+    size = S.gpk_synth_write_pcapng(path.encode(), 4, 0, n, cpu_threads)
     gen_s = time.perf_counter() - t0
     if not size:
         raise RuntimeError("could not write %s" % path)
@@ -522,29 +527,53 @@ def c5_replay(ctx, gib=10.0, reps=2, threads=8, cpu_threads=16):
             j = i - first
             picked[i] = (rec[j].copy(), fl[[j, k + j, 2 * k + j]].copy())
 
-    runs = []
-    cpu = None
-    try:
+    def replay(p):  # reps calls with parser p; the fastest, and what it delivered for the sample
+        rs = []
         for _ in range(reps):
             picked.clear()
             valid[0] = 0
-            _, st = ctx.replay_file(parser, path, collect=False, on_batch=on_batch, read_threads=threads)
-            runs.append(st)
+            _, r = ctx.replay_file(p, path, collect=False, on_batch=on_batch, read_threads=threads)
+            rs.append(r)
+        return rs, dict(picked)
+
+    def check(st, got_pk, decoders, outputs):  # the sample against the oracle with the same parser
+        idx = sorted(got_pk)
+        pk = [synth.packet(4, i) for i in idx]
+        cap = np.array([len(x) for x in pk], np.uint32)
+        off = np.concatenate([[0], np.cumsum(cap[:-1], dtype=np.uint64)]).astype(np.uint64)
+        ref = O.OracleParser(17, decoders, outputs=outputs).decode(
+            np.frombuffer(b"".join(pk) + bytes(16), np.uint8), off, cap, layouts=False)
+        got = np.array([got_pk[i][0] for i in idx], _lib.RECORD_DTYPE)
+        ok = (st["packets"] == n and st["error"] == "EOF" and len(idx) == len(sample)
+              and np.array_equal(got, ref["records"]))
+        if ok and outputs & 4:
+            gfl = np.stack([got_pk[i][1] for i in idx], axis=1).reshape(-1)
+            ok = np.array_equal(gfl, ref["flows"])
+        return "%s (%d sampled packets vs oracle)" % ("bit-exact" if ok else "MISMATCH", len(idx))
+
+    cpu = None
+    c1 = None
+    try:
+        runs, got4 = replay(parser)
+        valid4 = valid[0]
+        # the same file through C1's parser (Ethernet/IPv4/TCP/Payload, IPv4+TCP checksums): the
+        # small-packet dword-aligned kernel on replay batches
+        c1cfg = CONFIGS["c1"]
+        p1 = engine.ParserConfig(17, [engine.DECODER_KINDS[d] for d in c1cfg["decoders"]], outputs=c1cfg["outputs"])
+        runs1, got1 = replay(p1)
         cpu = c5_cpu(path, cpu_threads)
     finally:
         os.unlink(path)
     probe = htod_probe(size)
     st = min(runs, key=lambda x: x["wall_s"])
-    idx = sorted(picked)
-    pk = [synth.packet(4, i) for i in idx]
-    cap = np.array([len(x) for x in pk], np.uint32)
-    off = np.concatenate([[0], np.cumsum(cap[:-1], dtype=np.uint64)]).astype(np.uint64)
-    ref = O.OracleParser(17, ["ETHERNET", "DOT1Q", "IPV4", "IPV6", "IPV6_EXT", "TCP", "UDP", "PAYLOAD"]).decode(
-        np.frombuffer(b"".join(pk) + bytes(16), np.uint8), off, cap, layouts=False)
-    got = np.array([picked[i][0] for i in idx], _lib.RECORD_DTYPE)
-    gfl = np.stack([picked[i][1] for i in idx], axis=1).reshape(-1)
-    ok = (st["packets"] == n and st["error"] == "EOF" and len(idx) == len(sample)
-          and np.array_equal(got, ref["records"]) and np.array_equal(gfl, ref["flows"]))
+    parity = check(st, got4, ["ETHERNET", "DOT1Q", "IPV4", "IPV6", "IPV6_EXT", "TCP", "UDP", "PAYLOAD"], 7)
+    st1 = min(runs1, key=lambda x: x["wall_s"])
+    c1 = dict(parser="Ethernet+IPv4+TCP+Payload, IPv4+TCP checksums (C1's)",
+              value=round(st1["packets"] / st1["wall_s"] / 1e6, 2), unit="Mpkts/s",
+              GBps=round(st1["file_bytes"] / st1["wall_s"] / 1e9, 2), wall_s=round(st1["wall_s"], 4),
+              runs_wall_s=[round(r["wall_s"], 4) for r in runs1], kernel=st1["kernel"],
+              kernel_s=round(st1["kernel_s"], 4),
+              parity=check(st1, got1, ["ETHERNET", "IPV4", "TCP", "PAYLOAD"], c1cfg["outputs"]))
     w = st["wall_s"]
     w0 = runs[0]["wall_s"]
     return dict(workload="C5: pcapng replay of the C4 IMIX mix, end to end incl. HtoD/DtoH",
@@ -557,25 +586,26 @@ def c5_replay(ctx, gib=10.0, reps=2, threads=8, cpu_threads=16):
                 breakdown_s=dict(read=round(st["read_s"], 4), index=round(st["index_s"], 4),
                                  gpu_copy_decode=round(st["gpu_s"], 4), kernel=round(st["kernel_s"], 4),
                                  deliver=round(st["deliver_s"], 4)),
-                batches=st["batches"], slots=st["slots"], l4_valid=valid[0], write_s=round(gen_s, 2),
+                batches=st["batches"], slots=st["slots"], l4_valid=valid4, write_s=round(gen_s, 2),
                 kernel=st["kernel"], **probe,
                 frac_of_htod_probe=round(st["file_bytes"] / w / 1e9 / probe["htod_probe_GBps"], 4),
-                parity="%s (%d sampled packets vs oracle)" % ("bit-exact" if ok else "MISMATCH", len(idx)),
+                parity=parity, c1_parser=c1,
                 source="page-cached file in %s" % os.path.dirname(path), cpu_baseline=cpu)
 
 
-def afpacket_pump(ctx, packets=16 * 2**20, block_mib=4, blocks=64, reps=2, batch=1 << 18):
+def afpacket_pump(ctx, packets=16 * 2**20, block_mib=4, blocks=64, reps=2, batch=1 << 18, cfg_name="c4"):
     """Row (f)2: a TPACKET_V3 ring (blocks x block_mib MiB, laid out as the
     kernel fills it, C4 IMIX packets) drained by gpk_tpacket_pump: ring walk ->
     HtoD of each retired block into the HBM mirror -> decode -> DtoH, blocks
     handed back once on the device. The kernel side is emulated by a thread
     that re-arms every released block at once (a producer that never makes the
     consumer wait), so the figure is the consumer's ceiling. Sampled packets
-    are checked against the oracle."""
+    are checked against the oracle. cfg_name picks the parser (C4's by
+    default; "c1" for C1's Ethernet/IPv4/TCP parser on the same ring)."""
     from gopacket_amd import _lib, afpacket, engine, synth
     from oracle import oracle as O
     S = _lib.synth_lib()
-    cfg = CONFIGS["c4"]
+    cfg = CONFIGS[cfg_name]
     parser = engine.ParserConfig(17, [engine.DECODER_KINDS[d] for d in cfg["decoders"]], outputs=cfg["outputs"])
     bs = block_mib << 20
     ring = np.zeros(bs * blocks, np.uint8)
@@ -612,14 +642,15 @@ def afpacket_pump(ctx, packets=16 * 2**20, block_mib=4, blocks=64, reps=2, batch
     pk = [synth.packet(4, i % n_ring) for i in idx]
     cap = np.array([len(x) for x in pk], np.uint32)
     off = np.concatenate([[0], np.cumsum(cap[:-1], dtype=np.uint64)]).astype(np.uint64)
-    ref = O.OracleParser(17, ["ETHERNET", "DOT1Q", "IPV4", "IPV6", "IPV6_EXT", "TCP", "UDP", "PAYLOAD"]).decode(
+    ref = O.OracleParser(17, [ORACLE_DEC[d] for d in cfg["decoders"]], outputs=cfg["outputs"]).decode(
         np.frombuffer(b"".join(pk) + bytes(16), np.uint8), off, cap, layouts=False)
     got = np.array([picked[i][0] for i in idx], _lib.RECORD_DTYPE)
     gfl = np.stack([picked[i][1] for i in idx], axis=1).reshape(-1)
     ok = (st["packets"] == packets and len(idx) == len(sample) and np.array_equal(got, ref["records"])
-          and np.array_equal(gfl, ref["flows"]))
+          and (not cfg["outputs"] & 4 or np.array_equal(gfl, ref["flows"])))
     w = st["wall_s"]
     return dict(workload="(f)2: AF_PACKET TPACKET_V3 ring -> HBM -> decode (C4 IMIX mix), emulated kernel producer",
+                parser=" ".join(cfg["decoders"]), kernel=st.get("kernel"),
                 ring="%d x %d MiB blocks, %d packets per lap" % (blocks, block_mib, n_ring),
                 packets=st["packets"], value=round(st["packets"] / w / 1e6, 2), unit="Mpkts/s",
                 packet_GBps=round(st["packet_bytes"] / w / 1e9, 2),
@@ -906,6 +937,7 @@ def main():
             out["flows"] = flow_grouping(ctx)
         if args.afpacket > 0 and world == 1:
             out["afpacket"] = afpacket_pump(ctx, packets=args.afpacket * 2**20)
+            out["afpacket"]["c1_parser"] = afpacket_pump(ctx, packets=args.afpacket * 2**20, cfg_name="c1")
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(head, names, seconds=args.cpu_seconds)
         else:
