@@ -19,6 +19,9 @@ def main():
     ap.add_argument("--gib", type=float, default=10.0)
     ap.add_argument("--threads", default="8,12,16,24")
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--affinity", default="all", help="comma list of 'all' (inherited CPU set) and 'local' "
+                    "(the CPUs of the GPU's NUMA node, from sysfs): the calling thread's set, which the "
+                    "replay's reader threads inherit")
     a = ap.parse_args()
     import torch  # noqa: F401
     from gopacket_amd import _lib, engine
@@ -32,17 +35,36 @@ def main():
     S.gpk_synth_write_pcapng(path.encode(), 4, 0, n, 16)
     counts = [int(x) for x in a.threads.split(",")]
     ctx = engine.Context(0)
+    all_cpus = os.sched_getaffinity(0)
+    sets = {"all": all_cpus}
+    if "local" in a.affinity:
+        pr = torch.cuda.get_device_properties(0)
+        bdf = "%04x:%02x:%02x.0" % (pr.pci_domain_id, pr.pci_bus_id, pr.pci_device_id)
+        dev = "/sys/bus/pci/devices/" + bdf
+        cl = open(dev + "/local_cpulist").read().strip()
+        node = open(dev + "/numa_node").read().strip()
+        cpus = set()
+        for part in cl.split(","):
+            lo, _, hi = part.partition("-")
+            cpus.update(range(int(lo), int(hi or lo) + 1))
+        sets["local"] = cpus & all_cpus or cpus
+        print("GPU %s: NUMA node %s, local CPUs %s (%d of the %d inherited)" % (
+            bdf, node, cl, len(sets["local"]), len(all_cpus)), flush=True)
+    modes = a.affinity.split(",")
     best = {}
     try:
         ctx.replay_file(parser, path, collect=False, on_batch=lambda *x: None)  # allocate + pin the slots
         for r in range(a.rounds):
-            for t in counts:
-                _, st = ctx.replay_file(parser, path, collect=False, on_batch=lambda *x: None, read_threads=t)
-                gbs = st["file_bytes"] / st["wall_s"] / 1e9
-                best[t] = max(best.get(t, 0.0), gbs)
-                print("round %d threads %2d: %.4f s, %.2f GB/s, read %.3f index %.3f gpu %.3f" % (
-                    r, t, st["wall_s"], gbs, st["read_s"], st["index_s"], st["gpu_s"]), flush=True)
-        print("best GB/s: " + ", ".join("%d: %.2f" % (t, best[t]) for t in counts), flush=True)
+            for m in modes:
+                os.sched_setaffinity(0, sets[m])
+                for t in counts:
+                    _, st = ctx.replay_file(parser, path, collect=False, on_batch=lambda *x: None, read_threads=t)
+                    gbs = st["file_bytes"] / st["wall_s"] / 1e9
+                    best[m, t] = max(best.get((m, t), 0.0), gbs)
+                    print("round %d %s threads %2d: %.4f s, %.2f GB/s, read %.3f index %.3f gpu %.3f" % (
+                        r, m, t, st["wall_s"], gbs, st["read_s"], st["index_s"], st["gpu_s"]), flush=True)
+            os.sched_setaffinity(0, all_cpus)
+        print("best GB/s: " + ", ".join("%s/%d: %.2f" % (m, t, best[m, t]) for m in modes for t in counts), flush=True)
     finally:
         os.unlink(path)
 
