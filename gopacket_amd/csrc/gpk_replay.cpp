@@ -28,11 +28,15 @@
 // Results are delivered in packet order through the callback.
 #include <hip/hip_runtime.h>
 #include <fcntl.h>
+#include <pthread.h>
+#include <sched.h>
 #include <sys/stat.h>
 #include <unistd.h>
 #include <zlib.h>
 
 #include <algorithm>
+#include <cctype>
+#include <cstdlib>
 #include <chrono>
 #include <cstdio>
 #include <cstring>
@@ -54,12 +58,59 @@ double now_s() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
+// The CPUs of the device's NUMA node (sysfs local_cpulist of its PCI
+// function) that this thread may run on; false when unknown or empty. The
+// reader threads copy the file into pinned staging memory that the device's
+// DMA then reads, and the calling thread walks and launches: on the device's
+// node (profiles/r14_c5_numa.txt). GPK_REPLAY_NUMA: 0 leaves every thread
+// where it is, 1 pins the reader threads, 2 (default) also the calling thread
+// for the duration of the call.
+int numa_level() {
+  const char* env = getenv("GPK_REPLAY_NUMA");
+  return env && env[0] >= '0' && env[0] <= '2' ? env[0] - '0' : 2;
+}
+bool device_local_cpus(int dev, cpu_set_t& out) {
+  if (numa_level() == 0) return false;
+  char bdf[64] = {0};
+  if (hipDeviceGetPCIBusId(bdf, (int)sizeof(bdf) - 1, dev) != hipSuccess) return false;
+  for (char* p = bdf; *p; p++) *p = (char)tolower((unsigned char)*p);
+  char path[160];
+  snprintf(path, sizeof(path), "/sys/bus/pci/devices/%s/local_cpulist", bdf);
+  FILE* f = fopen(path, "r");
+  if (!f) return false;
+  char buf[4096] = {0};
+  const size_t k = fread(buf, 1, sizeof(buf) - 1, f);
+  fclose(f);
+  buf[k] = 0;
+  cpu_set_t allowed;
+  CPU_ZERO(&allowed);
+  if (sched_getaffinity(0, sizeof(allowed), &allowed) != 0) return false;
+  CPU_ZERO(&out);
+  for (char* p = buf; *p;) {  // "a-b,c,d-e\n"
+    char* e = nullptr;
+    const long lo = strtol(p, &e, 10);
+    if (e == p) break;
+    long hi = lo;
+    p = e;
+    if (*p == '-') {
+      hi = strtol(p + 1, &e, 10);
+      p = e;
+    }
+    for (long c = lo; c <= hi && c < CPU_SETSIZE; c++)
+      if (c >= 0 && CPU_ISSET(c, &allowed)) CPU_SET(c, &out);
+    while (*p == ',' || *p == '\n' || *p == ' ') p++;
+  }
+  return CPU_COUNT(&out) > 0;
+}
+
 struct Src {  // the capture byte stream: plain file (parallel pread) or gzip (zlib)
   int fd = -1;
   gzFile gz = nullptr;
   uint64_t size = 0, pos = 0;
   bool at_end = false;
   int threads = 8;
+  bool pin = false;  // run the reader threads on `cpus` (the device's NUMA node)
+  cpu_set_t cpus;
 
   // Fill dst with up to cap bytes of the stream; returns the count.
   uint64_t read(uint8_t* dst, uint64_t cap) {
@@ -85,6 +136,7 @@ struct Src {  // the capture byte stream: plain file (parallel pread) or gzip (z
     const uint64_t per = (want + T - 1) / T;
     for (int t = 0; t < T; t++) {
       th.emplace_back([&, t] {
+        if (pin) (void)pthread_setaffinity_np(pthread_self(), sizeof(cpus), &cpus);
         uint64_t a = (uint64_t)t * per, e = std::min<uint64_t>(want, a + per);
         while (a < e) {
           ssize_t k = pread(fd, dst + a, e - a, (off_t)(base + a));
@@ -329,6 +381,22 @@ extern "C" int gpk_replay_file(gpk_ctx* ctx, const gpk_parser* parser, const cha
   // ---- the stream ------------------------------------------------------------
   Src src;
   src.threads = opt.read_threads;
+  cpu_set_t caller_cpus;  // restored on every return (the calling thread pinned at level 2)
+  bool caller_pinned = false;
+  {
+    int d = 0;
+    (void)hipGetDevice(&d);
+    src.pin = device_local_cpus(d, src.cpus);
+    if (src.pin && numa_level() == 2 && pthread_getaffinity_np(pthread_self(), sizeof(caller_cpus), &caller_cpus) == 0)
+      caller_pinned = pthread_setaffinity_np(pthread_self(), sizeof(src.cpus), &src.cpus) == 0;
+  }
+  struct Restore {
+    bool on;
+    cpu_set_t* set;
+    ~Restore() {
+      if (on) (void)pthread_setaffinity_np(pthread_self(), sizeof(*set), set);
+    }
+  } restore{caller_pinned, &caller_cpus};
   src.fd = open(path, O_RDONLY);
   if (src.fd < 0) {
     snprintf(stats->error, sizeof(stats->error), "open %s failed", path);
@@ -442,6 +510,7 @@ extern "C" int gpk_replay_file(gpk_ctx* ctx, const gpk_parser* parser, const cha
     s.h2d_err = hipSuccess;
     std::shared_future<Fill> prev = last_fill;
     s.fill = std::async(std::launch::async, [&src, &s, C, R, stats, dev, dev_walk, prev] {
+      if (src.pin) (void)pthread_setaffinity_np(pthread_self(), sizeof(src.cpus), &src.cpus);
       hipEvent_t before = nullptr;
       if (prev.valid()) before = prev.get().sent;
       double t = now_s();

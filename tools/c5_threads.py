@@ -19,9 +19,10 @@ def main():
     ap.add_argument("--gib", type=float, default=10.0)
     ap.add_argument("--threads", default="8,12,16,24")
     ap.add_argument("--rounds", type=int, default=3)
-    ap.add_argument("--affinity", default="all", help="comma list of 'all' (inherited CPU set) and 'local' "
-                    "(the CPUs of the GPU's NUMA node, from sysfs): the calling thread's set, which the "
-                    "replay's reader threads inherit")
+    ap.add_argument("--affinity", default="lib", help="comma list of 'lib' (the library pins its reader "
+                    "threads and the calling thread to the GPU's NUMA node), 'lib1' (the reader threads only), 'all' (GPK_REPLAY_NUMA=0: the inherited CPU set) and "
+                    "'local' (GPK_REPLAY_NUMA=0, the calling thread on the GPU's node: the reader threads "
+                    "inherit it)")
     a = ap.parse_args()
     import torch  # noqa: F401
     from gopacket_amd import _lib, engine
@@ -36,7 +37,7 @@ def main():
     counts = [int(x) for x in a.threads.split(",")]
     ctx = engine.Context(0)
     all_cpus = os.sched_getaffinity(0)
-    sets = {"all": all_cpus}
+    sets = {"all": all_cpus, "lib": all_cpus, "lib1": all_cpus}
     if "local" in a.affinity:
         pr = torch.cuda.get_device_properties(0)
         bdf = "%04x:%02x:%02x.0" % (pr.pci_domain_id, pr.pci_bus_id, pr.pci_device_id)
@@ -57,6 +58,7 @@ def main():
         for r in range(a.rounds):
             for m in modes:
                 os.sched_setaffinity(0, sets[m])
+                os.environ["GPK_REPLAY_NUMA"] = {"lib": "2", "lib1": "1"}.get(m, "0")
                 for t in counts:
                     _, st = ctx.replay_file(parser, path, collect=False, on_batch=lambda *x: None, read_threads=t)
                     gbs = st["file_bytes"] / st["wall_s"] / 1e9
