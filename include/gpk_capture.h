@@ -177,7 +177,11 @@ typedef void (*gpk_replay_cb)(void* user, uint64_t first_packet, uint64_t n, con
  * Enhanced Packet Blocks; the host reader takes every other block, same
  * results either way; GPK_REPLAY_HOST_WALK=1 in the environment keeps it on
  * the host). The pinned staging slots and device buffers stay with ctx for
- * the next call with the same sizes (gpk_ctx_destroy frees them). */
+ * the next call with the same sizes (gpk_ctx_destroy frees them).
+ * The reader threads, and the calling thread for the duration of the call,
+ * run on the CPUs of the current device's NUMA node that the caller may use
+ * (its affinity is restored on return); environment GPK_REPLAY_NUMA=0 turns
+ * this off, =1 pins the reader threads only. */
 int gpk_replay_file(gpk_ctx* ctx, const gpk_parser* p, const char* path, const gpk_replay_opts* opts,
                     gpk_replay_cb cb, void* user, gpk_replay_stats* stats);
 
