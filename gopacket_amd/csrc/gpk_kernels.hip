@@ -62,7 +62,10 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 #define GPK_PB_DEPTH 8  // dense phase B: passes in flight (80-VGPR kernels; A/B r04b: 8 vs 6 -0.4 % C3, 10 no better)
 #endif
 #ifndef GPK_PB_DEPTH7
-#define GPK_PB_DEPTH7 6  // ... in the 72-VGPR kernels (7 waves per SIMD; A/B r04b: 6 vs 4 -0.9 % C4, -2.8 % C1)
+#define GPK_PB_DEPTH7 6  // ... in the 72-VGPR kernels (7 waves per SIMD; A/B r04b: 6 vs 4 -0.9 % C4, -2.8 % C1; r14: 8 vs 6 C1 -3.9 % in one A/B, parity not yet run on the GPU; 10 spills)
+#endif
+#ifndef GPK_PB_DEPTH7SB
+#define GPK_PB_DEPTH7SB 6  // ... in the stream-before-parse kernel's phase B after the parse (8: 40 B of scratch, not 20)
 #endif
 #ifndef GPK_PB_IDPERM
 #define GPK_PB_IDPERM 1  // dense phase B: lanes outside their target pass pull their own prefix (no LDS bank conflicts)
@@ -886,7 +889,7 @@ __device__ __forceinline__ void decode_packet(const KParams& P, const TT& T, uin
 
   // Phase B's stream over the wave's packets starts now when they are packed:
   // its first D KiB load while the headers are parsed.
-  constexpr int D = kLayout ? 4 : (O > 6 ? GPK_PB_DEPTH7 : GPK_PB_DEPTH);  // layouts: fewer registers left
+  constexpr int D = kLayout ? 4 : (O > 6 ? (kSB ? GPK_PB_DEPTH7SB : GPK_PB_DEPTH7) : GPK_PB_DEPTH);  // layouts: fewer registers left
   // early passes: as many as the kernel's register budget carries through
   // DecodeLayers untouched (tools/check_stream_isa.py)
   constexpr int E = kEarly >= 0 ? kEarly : ((kLayout || kKeys) ? 0 : (O > 6 ? GPK_PB_EARLY7 : GPK_PB_EARLY));
