@@ -25,17 +25,14 @@ namespace {
 constexpr uint32_t kBlock = 256;
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-// 4 bytes at p in memory order (little-endian value), any alignment.
-__device__ __forceinline__ uint32_t ldu32(const uint8_t* p) {
-  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
-  const uint32_t* q = reinterpret_cast<const uint32_t*>(a & ~static_cast<uintptr_t>(3));
-  return __builtin_amdgcn_alignbyte(q[1], q[0], (uint32_t)(a & 3));
+// n bytes at p in memory order (little-endian value), byte loads: exactly the
+// field's bytes, never a byte past them (a field can end at the batch's last
+// byte).
+__device__ __forceinline__ uint32_t ldbytes(const uint8_t* p, int n) {
+  uint32_t v = 0;
+  for (int k = 0; k < n; k++) v |= (uint32_t)p[k] << (8 * k);
+  return v;
 }
-__device__ __forceinline__ uint32_t be16(const uint8_t* p) {
-  const uint32_t w = ldu32(p);
-  return (w & 0xffu) << 8 | (w >> 8 & 0xffu);
-}
-__device__ __forceinline__ uint32_t be32(const uint8_t* p) { return __builtin_bswap32(ldu32(p)); }
 
 // Header bytes of one packet: the 16-byte-aligned run of kWin chunks holding
 // its first bytes sits in the lane's LDS slot (one round trip of wide loads
@@ -55,11 +52,22 @@ struct Hdr {
   __device__ __forceinline__ uint32_t u32(uint32_t p) const {  // 4 bytes at packet byte p, memory order
     if (p + 4 <= win)  // an unaligned ds_read_b32 (exact at any byte address on gfx950)
       return *reinterpret_cast<const u32_ua*>(reinterpret_cast<const uint8_t*>(fields_smem) + lb + p);
-    return ldu32(pk + p);
+    return ldbytes(pk + p, 4);
   }
+  // a 16-bit field reads its own 2 bytes only: from LDS as two byte reads when
+  // it ends inside the window (a dword there could pass the window), else from
+  // memory (the dword form read up to 7 bytes past the field)
   __device__ __forceinline__ uint32_t be16(uint32_t p) const {
-    const uint32_t w = u32(p);
-    return (w & 0xffu) << 8 | (w >> 8 & 0xffu);
+    if (p + 4 <= win) {
+      const uint32_t w = u32(p);
+      return (w & 0xffu) << 8 | (w >> 8 & 0xffu);
+    }
+    if (p + 2 <= win) {
+      const uint8_t* b = reinterpret_cast<const uint8_t*>(fields_smem) + lb + p;
+      return (uint32_t)b[0] << 8 | b[1];
+    }
+    const uint32_t w = ldbytes(pk + p, 2);
+    return (w & 0xffu) << 8 | w >> 8;
   }
   __device__ __forceinline__ uint32_t be32(uint32_t p) const { return __builtin_bswap32(u32(p)); }
 };

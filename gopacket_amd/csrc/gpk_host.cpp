@@ -73,11 +73,12 @@ struct TabSlot {
   uint64_t version = 0;       // parser table version held, 0 = empty
   uint64_t last_use = 0;      // LRU tick
   uint8_t* staging = nullptr; // pinned: DevTables, then the compact blob; the last upload's source
-  // Both events are recorded on the context's aggregation stream (agg), which
-  // waits for the stream concerned first, so they never refer to a caller's
-  // stream that may be destroyed meanwhile.
+  // Both events are recorded on an aggregation stream of the context (one per
+  // caller stream, Agg), which waits for the caller's stream first, so they
+  // never refer to a caller's stream that may be destroyed meanwhile.
   hipEvent_t ready = nullptr;  // the slot's last upload has landed
-  hipEvent_t done = nullptr;   // every launch so far that read the slot has completed
+  hipEvent_t done = nullptr;   // every launch so far that read the slot has completed (cumulative:
+                               // each record first waits for the previous one)
   bool uploaded = false, read = false;
   bool ready_seen = false;     // ready has been observed complete (no wait needed)
 };
@@ -92,11 +93,18 @@ struct gpk_ctx {
   void* dbuf = nullptr;
   size_t dbuf_bytes = 0;
   hipStream_t stream = nullptr;
-  // carries only waits and event records: the completion marks of launches and
-  // uploads on callers' streams (note_launch), so no caller stream is coupled to
-  // another and no event outlives the stream it was recorded on
-  hipStream_t agg = nullptr;
-  std::unordered_map<hipStream_t, hipEvent_t> stream_ev;  // one reusable event per caller stream
+  // Aggregation streams, one per caller stream (the most recently used
+  // kAggStreams callers): each carries only waits and event records, the
+  // completion marks of launches and uploads on its caller's stream
+  // (note_launch, upload), so a mark waits for its own caller's work only and
+  // no event outlives the stream it was recorded on. ev: a reusable event
+  // recorded on the caller's stream.
+  struct Agg {
+    hipStream_t agg = nullptr;
+    hipEvent_t ev = nullptr;
+    uint64_t last_use = 0;
+  };
+  std::unordered_map<hipStream_t, Agg> aggs;
   std::mutex mu;
   // gpk_replay_file's staging buffers, kept for the next call (gpk_walk.h)
   void* replay_cache = nullptr;
@@ -257,8 +265,12 @@ static void free_slots(gpk_ctx* c) {
     t.dctab = nullptr;
     t.staging = nullptr;
   }
-  for (auto& kv : c->stream_ev) (void)hipEventDestroy(kv.second);
-  c->stream_ev.clear();
+  for (auto& kv : c->aggs) {
+    (void)hipStreamSynchronize(kv.second.agg);
+    (void)hipStreamDestroy(kv.second.agg);
+    (void)hipEventDestroy(kv.second.ev);
+  }
+  c->aggs.clear();
 }
 
 int gpk_ctx_create(gpk_ctx** out, int device) {
@@ -273,11 +285,6 @@ int gpk_ctx_create(gpk_ctx** out, int device) {
     delete c;
     return GPK_EHIP;
   }
-  if (hipStreamCreateWithFlags(&c->agg, hipStreamNonBlocking) != hipSuccess) {
-    (void)hipStreamDestroy(c->stream);
-    delete c;
-    return GPK_EHIP;
-  }
   *out = c;
   return GPK_OK;
 }
@@ -287,7 +294,6 @@ int gpk_ctx_destroy(gpk_ctx* c) {
   (void)hipSetDevice(c->device);
   (void)hipDeviceSynchronize();  // launches still reading the table copies
   if (c->stream) (void)hipStreamDestroy(c->stream);
-  if (c->agg) (void)hipStreamDestroy(c->agg);
   free_slots(c);
   if (c->dbuf) (void)hipFree(c->dbuf);
   if (c->replay_cache && c->replay_cache_free) c->replay_cache_free(c->replay_cache);
@@ -402,28 +408,48 @@ static uint32_t fast_flags(const gpk_parser* p) {
   return f;
 }
 
-// The context's reusable event for caller stream s.
-static int stream_event(gpk_ctx* c, hipStream_t s, hipEvent_t* ev) {
-  auto it = c->stream_ev.find(s);
-  if (it == c->stream_ev.end()) {
-    hipEvent_t e = nullptr;
-    HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    it = c->stream_ev.emplace(s, e).first;
+constexpr size_t kAggStreams = 8;
+
+// The aggregation stream and reusable event of caller stream s (created on
+// first use; beyond kAggStreams callers the least recently used one is
+// drained and retired: the marks recorded on it have completed by then, and
+// a completed event stays complete).
+static int agg_of(gpk_ctx* c, hipStream_t s, gpk_ctx::Agg** out) {
+  auto it = c->aggs.find(s);
+  if (it == c->aggs.end()) {
+    if (c->aggs.size() >= kAggStreams) {
+      auto lru = c->aggs.begin();
+      for (auto j = c->aggs.begin(); j != c->aggs.end(); ++j)
+        if (j->second.last_use < lru->second.last_use) lru = j;
+      HIPCHK(hipStreamSynchronize(lru->second.agg));
+      HIPCHK(hipStreamDestroy(lru->second.agg));
+      HIPCHK(hipEventDestroy(lru->second.ev));
+      c->aggs.erase(lru);
+    }
+    gpk_ctx::Agg a;
+    HIPCHK(hipStreamCreateWithFlags(&a.agg, hipStreamNonBlocking));
+    if (hipEventCreateWithFlags(&a.ev, hipEventDisableTiming) != hipSuccess) {
+      (void)hipStreamDestroy(a.agg);
+      return hip_fail(hipErrorOutOfMemory, "hipEventCreateWithFlags");
+    }
+    it = c->aggs.emplace(s, a).first;
   }
-  *ev = it->second;
+  it->second.last_use = ++c->tick;
+  *out = &it->second;
   return GPK_OK;
 }
 
-// Record on the aggregation stream, as mark, the point stream s has reached.
-static int mark_after(gpk_ctx* c, hipStream_t s, hipEvent_t mark) {
-  if (s != c->agg) {
-    hipEvent_t ev = nullptr;
-    int rc = stream_event(c, s, &ev);
-    if (rc) return rc;
-    HIPCHK(hipEventRecord(ev, s));
-    HIPCHK(hipStreamWaitEvent(c->agg, ev, 0));
-  }
-  HIPCHK(hipEventRecord(mark, c->agg));
+// Record, as mark, the point stream s has reached (on s's aggregation
+// stream). cumulative: the mark also stays behind its own previous record
+// (a slot's done covers every launch that read it, on any stream).
+static int mark_after(gpk_ctx* c, hipStream_t s, hipEvent_t mark, bool cumulative) {
+  gpk_ctx::Agg* a = nullptr;
+  int rc = agg_of(c, s, &a);
+  if (rc) return rc;
+  HIPCHK(hipEventRecord(a->ev, s));
+  HIPCHK(hipStreamWaitEvent(a->agg, a->ev, 0));
+  if (cumulative) HIPCHK(hipStreamWaitEvent(a->agg, mark, 0));
+  HIPCHK(hipEventRecord(mark, a->agg));
   return GPK_OK;
 }
 
@@ -457,7 +483,7 @@ static int upload(gpk_ctx* c, const gpk_parser* p, gpk::KParams& P, int* slot, h
     t.compact = !c->force_global && build_compact(p->tab, p->first, blob, t.cg);
     HIPCHK(hipMemcpyAsync(t.dtab, t.staging, sizeof(gpk::DevTables), hipMemcpyHostToDevice, s));
     if (t.compact) HIPCHK(hipMemcpyAsync(t.dctab, blob, gpk::kCtDwords * 4, hipMemcpyHostToDevice, s));
-    int rc = mark_after(c, s, t.ready);
+    int rc = mark_after(c, s, t.ready, false);
     if (rc) return rc;
     t.uploaded = true;
     t.ready_seen = false;
@@ -503,7 +529,7 @@ static int upload(gpk_ctx* c, const gpk_parser* p, gpk::KParams& P, int* slot, h
 // caller stream), so the slot is rewritten only after it completes.
 static int note_launch(gpk_ctx* c, int k, hipStream_t s) {
   TabSlot& t = c->slots[k];
-  int rc = mark_after(c, s, t.done);
+  int rc = mark_after(c, s, t.done, t.read);
   if (rc) return rc;
   t.read = true;
   return GPK_OK;

@@ -62,10 +62,11 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 #define GPK_PB_DEPTH 8  // dense phase B: passes in flight (80-VGPR kernels; A/B r04b: 8 vs 6 -0.4 % C3, 10 no better)
 #endif
 #ifndef GPK_PB_DEPTH7
-#define GPK_PB_DEPTH7 6  // ... in the 72-VGPR kernels (7 waves per SIMD; A/B r04b: 6 vs 4 -0.9 % C4, -2.8 % C1; r14: 8 vs 6 C1 -3.9 % in one A/B, parity not yet run on the GPU; 10 spills)
+#define GPK_PB_DEPTH7 8  // ... in the 72-VGPR kernels (7 waves per SIMD; A/B r04b: 6 vs 4 -0.9 % C4, -2.8 % C1; r14: 8 vs 6 C1 -3.9 %; 10 spills)
 #endif
 #ifndef GPK_PB_DEPTH7SB
-#define GPK_PB_DEPTH7SB 6  // ... in the stream-before-parse kernel's phase B after the parse (8: 40 B of scratch, not 20)
+#define GPK_PB_DEPTH7SB 5  // ... in the stream-before-parse kernel's phase B after the parse (the fallback of waves whose
+                           // packets are not packed; 6: 20 B of scratch, 8: 40 B; 5 and below: none)
 #endif
 #ifndef GPK_PB_IDPERM
 #define GPK_PB_IDPERM 1  // dense phase B: lanes outside their target pass pull their own prefix (no LDS bank conflicts)
@@ -1394,9 +1395,12 @@ Sel select(const gpk::KParams* P, int with_l4, int with_layout) {
 template <bool kCompact>
 hipError_t launch_sel(const gpk::KParams* P, const Sel& s, hipStream_t stream, int* occ) {
   constexpr int W = gpk::kWinChunks;
-  if (s.sb)
-    return s.O == GPK_WAVES_PER_EU ? launch_sb<kCompact, GPK_WAVES_PER_EU>(P, stream, occ)
-                                   : launch_sb<kCompact, GPK_SB_WAVES>(P, stream, occ);
+  if (s.sb) {
+#if GPK_SB_BIG
+    if (s.O == GPK_WAVES_PER_EU) return launch_sb<kCompact, GPK_WAVES_PER_EU>(P, stream, occ);
+#endif
+    return launch_sb<kCompact, GPK_SB_WAVES>(P, stream, occ);
+  }
   if (s.keys)
     return s.l4 ? launch<true, false, kCompact, true>(P, stream, occ) : launch<false, false, kCompact, true>(P, stream, occ);
   if (s.W == 4) return launch<false, false, kCompact, false, 4>(P, stream, occ);
@@ -1430,8 +1434,8 @@ extern "C" hipError_t gpk_launch_occupancy(const gpk::KParams* P, int with_l4, i
 extern "C" int gpk_launch_describe(const gpk::KParams* P, int with_l4, int with_layout, char* buf, size_t cap) {
   const Sel s = select(P, with_l4, with_layout);
   if (s.sb)
-    return snprintf(buf, cap, "gpk::decode_sb_kernel<%s,%d>", s.compact ? "true" : "false",
-                    s.O == GPK_WAVES_PER_EU ? s.O : GPK_SB_WAVES);
+    return snprintf(buf, cap, "gpk::decode_sb_kernel<%s,%d,%d>", s.compact ? "true" : "false",
+                    s.O == GPK_WAVES_PER_EU ? s.O : GPK_SB_WAVES, gpk::kWinChunks);
   return snprintf(buf, cap, "gpk::decode_kernel<%s,%s,%s,%s,%d,%d,%d>", s.l4 ? "true" : "false",
                   s.layout ? "true" : "false", s.compact ? "true" : "false", s.keys ? "true" : "false", s.W,
                   s.W == 4 ? 6 : s.O, s.AL);

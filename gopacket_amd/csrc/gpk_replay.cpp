@@ -509,10 +509,13 @@ extern "C" int gpk_replay_file(gpk_ctx* ctx, const gpk_parser* parser, const cha
   auto start_fill = [&](Slot& s) {
     s.h2d_err = hipSuccess;
     std::shared_future<Fill> prev = last_fill;
-    s.fill = std::async(std::launch::async, [&src, &s, C, R, stats, dev, dev_walk, prev] {
+    // (mutable: the previous fill's future is dropped as soon as it has been
+    // read, so the async states do not chain every fill of the call together)
+    s.fill = std::async(std::launch::async, [&src, &s, C, R, stats, dev, dev_walk, prev]() mutable {
       if (src.pin) (void)pthread_setaffinity_np(pthread_self(), sizeof(src.cpus), &src.cpus);
       hipEvent_t before = nullptr;
       if (prev.valid()) before = prev.get().sent;
+      prev = std::shared_future<Fill>();
       double t = now_s();
       const uint64_t k = src.read(s.host + C, R);
       const bool end = src.at_end;

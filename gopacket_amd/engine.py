@@ -152,9 +152,10 @@ class Context:
                 fields.cpu().numpy().view(_lib.FIELDS_DTYPE))
 
     def kernel_name(self, parser, data, offsets, caplens, layouts=False):
-        """The decode kernel specialisation decode_device launches for this
-        parser and batch (gpk_decode_kernel_name): the name rocprofv3 lists."""
-        b = _lib.Batch(data.data_ptr(), offsets.data_ptr(), caplens.data_ptr(), offsets.numel(), data.numel())
+        """The decode kernel specialisation decode_device (torch tensors) or
+        decode_host (numpy arrays) launches for this parser and batch
+        (gpk_decode_kernel_name): the name rocprofv3 lists."""
+        b = _batch_of(data, offsets, caplens)
         buf = ctypes.create_string_buffer(256)
         n = lib().gpk_decode_kernel_name(self.h, parser.h, ctypes.byref(b), int(layouts), buf, 256)
         if n < 0:
@@ -164,7 +165,7 @@ class Context:
     def occupancy(self, parser, data, offsets, caplens, layouts=False):
         """Blocks of that kernel resident per CU with this parser's LDS table
         blob (gpk_decode_occupancy)."""
-        b = _lib.Batch(data.data_ptr(), offsets.data_ptr(), caplens.data_ptr(), offsets.numel(), data.numel())
+        b = _batch_of(data, offsets, caplens)
         out = ctypes.c_int()
         check(lib().gpk_decode_occupancy(self.h, parser.h, ctypes.byref(b), int(layouts), ctypes.byref(out)))
         return out.value
@@ -222,6 +223,14 @@ class Context:
         pkt = bytes(pkt)
         check(lib().gpk_decoded_list_host(self.h, parser.h, pkt, len(pkt), out, cap, ctypes.byref(n)))
         return [out[i] for i in range(min(n.value, cap))]
+
+
+def _batch_of(data, offsets, caplens):
+    """gpk_batch over torch tensors or numpy arrays (the pointers are only
+    described, never dereferenced, by the name / occupancy queries)."""
+    if isinstance(data, np.ndarray):
+        return _lib.Batch(data.ctypes.data, offsets.ctypes.data, caplens.ctypes.data, len(offsets), data.nbytes)
+    return _lib.Batch(data.data_ptr(), offsets.data_ptr(), caplens.data_ptr(), offsets.numel(), data.numel())
 
 
 def _stream_ptr(stream):

@@ -55,6 +55,30 @@ def pack(packets, align=1, pad=0):
     return data, np.array(offs, np.uint64), np.array([len(p) for p in packets], np.uint32)
 
 
+def ipv6_udp_jumbogram(checksum=0, hbh16=False):
+    """The packet layers/tcpip_test.go:138-186 (TestIPv6JumbogramUDPChecksum)
+    serializes, rebuilt from the test's code: IPv6 2001:db8::1 -> 2001:db8::2,
+    HopLimit 64, Length 0 (ip6.go:202-208, jumbo); the HopByHop header
+    addIPv6JumboOption adds (ip6.go:80-102: NextHeader UDP, HdrExtLen 0, the
+    Jumbo TLV 0xC2/4 at offset 2, no padding: serializeIPv6HeaderTLVOptions
+    ip6.go:368-408) holding the payload length from the HopByHop header on
+    (setIPv6PayloadJumboLength ip6.go:105-134: 8 + 8 + 65536); UDP 12345 ->
+    9999 with Length 0 (udp.go:65-81, jumbo) and 65536 bytes of 0xfe.
+    hbh16: a jumbogram whose IPv6 Payload is the UDP segment as DecodeLayers
+    slices it: a 16-byte HopByHop header (PadN, the Jumbo TLV at 4n+2, PadN)
+    whose bytes 4-5 are 0, so the UDP decoder reads them as a jumbo Length 0
+    (udp.go:49-50) and sums the whole rest of the packet."""
+    src = bytes.fromhex("20010db8000000000000000000000001")
+    dst = bytes.fromhex("20010db8000000000000000000000002")
+    payload = b"\xfe" * 65536
+    hbh = bytes([17, 0, 0xC2, 4]) + struct.pack(">I", 8 + 8 + len(payload))
+    if hbh16:
+        hbh = bytes([17, 1, 1, 2, 0, 0, 0xC2, 4]) + struct.pack(">I", 16 + 8 + len(payload)) + bytes([1, 2, 0, 0])
+    udp = struct.pack(">HHHH", 12345, 9999, 0, checksum)
+    ip6 = struct.pack(">IHBB16s16s", 0x60000000, 0, 0, 64, src, dst)
+    return ip6 + hbh + udp + payload
+
+
 # ---------------------------------------------------------------------------
 # structure-aware fuzzer
 

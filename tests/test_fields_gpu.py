@@ -96,3 +96,45 @@ def test_decode_batch_fields_api(gpu_ctx):
         if layers.LayerTypeIPv4 in decoded:
             assert (int(f["ip4_ttl"]), bytes(f["ip4_dst"])) == (ip4.TTL, bytes(ip4.DstIP))
     assert n > 100
+
+
+def test_fields_header_ends_at_buffer_end(gpu_ctx):
+    """A pure ACK whose TCP header ends past the 6-chunk LDS window and exactly
+    at the end of the batch buffer (data_bytes = its last byte + 1): the 16-bit
+    fields at the header's end (Checksum, Urgent) come from memory and read
+    their own 2 bytes only (ADVICE r3, gpk_fields.hip Hdr::be16)."""
+    import struct
+    cfg = CONFIGS["statsassembly"]
+    src, dst = bytes(range(16)), bytes(range(16, 32))
+    hbh = bytes([6, 0, 1, 4, 0, 0, 0, 0])
+    tcp = struct.pack(">HHIIBBHHH", 443, 51000, 7, 9, 0x50, 0x10, 512, 0x1234, 0xBEEF)
+    ip6 = struct.pack(">IHBB16s16s", 0x60000000, len(hbh) + len(tcp), 0, 64, src, dst)
+    ack = b"\x02" * 12 + b"\x86\xdd" + ip6 + hbh + tcp  # 82 bytes: Ethernet + IPv6 + HopByHop + TCP
+    lead = pktutil.fuzz_packets(31, 300)
+    data, off, cap = pktutil.pack(lead)
+    last = (len(data) + 15) // 16 * 16 + 15  # packet byte 0 at window byte 15: window = 81 bytes
+    buf = np.zeros(last + len(ack), np.uint8)
+    buf[:len(data)] = data
+    buf[last:] = np.frombuffer(ack, np.uint8)
+    off = np.append(off, np.uint64(last))
+    cap = np.append(cap, np.uint32(len(ack)))
+    n = len(off)
+    d_data = torch.from_numpy(buf).cuda()
+    d_off = torch.from_numpy(off.view(np.int64)).cuda()
+    d_cap = torch.from_numpy(cap.view(np.int32)).cuda()
+    rec = torch.zeros(n * 16, dtype=torch.uint8, device="cuda")
+    err = torch.zeros(2 * n, dtype=torch.int32, device="cuda")
+    fl = torch.zeros(3 * n, dtype=torch.int64, device="cuda")
+    lay = torch.zeros(n * 64, dtype=torch.uint8, device="cuda")
+    fields = torch.zeros(n * 128, dtype=torch.uint8, device="cuda")
+    s = torch.cuda.current_stream()
+    gpu_ctx.decode_device(device_parser(cfg), d_data, d_off, d_cap, rec, err, fl, lay, stream=s)
+    gpu_ctx.extract_fields(d_data, d_off, d_cap, lay, fields, stream=s)
+    torch.cuda.synchronize()
+    ref = oracle_parser(cfg).decode(buf, off, cap, layouts=True)
+    assert np.array_equal(lay.cpu().numpy().view(_lib.LAYOUT_DTYPE).view(np.uint8), ref["layouts"].view(np.uint8))
+    want = O.extract_fields(buf, off, ref["layouts"])
+    got = fields.cpu().numpy().reshape(-1, 128)
+    assert np.array_equal(got, want)
+    f = got[-1:].view(_lib.FIELDS_DTYPE)[0]
+    assert (int(f["tcp_checksum"]), int(f["tcp_urgent"]), int(f["tcp_window"])) == (0x1234, 0xBEEF, 512)

@@ -74,7 +74,11 @@ def test_edge_sizes(gpu_ctx):
     jumbo[16:18] = b"\x00\x00"
     big = bytearray(base) + bytes(262144 - len(base))
     big[16:18] = b"\x00\x00"
-    packets = [b"", b"\x00", base[:13], base[:14], base, bytes(jumbo), bytes(big), base[:60]] * 3
+    # the IPv6 UDP jumbogram of tcpip_test.go:138-186 (its UDP decode fails under
+    # DecodeLayers) and the variant whose UDP segment of 65 560 bytes is
+    # summed, with the pseudo-header's length>>16 term (raw_ip6 config)
+    j6 = [pktutil.ipv6_udp_jumbogram(0xcda8), pktutil.ipv6_udp_jumbogram(hbh16=True)]
+    packets = [b"", b"\x00", base[:13], base[:14], base, bytes(jumbo), bytes(big), base[:60]] * 3 + j6
     for name in sorted(CONFIGS):
         dev, ref = run_both(gpu_ctx, CONFIGS[name], packets, align=1, pad=3)
         assert_same(dev, ref, name)
@@ -240,25 +244,83 @@ def test_port_traffic_hits_table_entries(gpu_ctx):
     assert_same(dev, ref, "many_ports keys")
 
 
-@pytest.mark.parametrize("layout", ["sparse4k", "shuffled", "reversed"])
-def test_phase_b_layouts(gpu_ctx, layout):
-    """The L4 segment sums take the dense prefix stream when a wave's segments
-    share a compact region and the per-segment stream otherwise: packets 4 KiB
-    apart (sparse), packets in shuffled or reversed order inside one packed
-    buffer (dense, unordered) must all give the oracle's results."""
-    packets = pktutil.fuzz_packets(4242, 12000) + golden_packets()
+def phase_b_layout(packets, layout):
+    """The packets of `packets` placed in one buffer as `layout` says:
+    sparse4k   every packet at a multiple of 4 KiB (sparse waves)
+    sparse_mix packed, but every 8th packet moved to a 4 KiB-aligned place past
+               the packed ones (mean packet still under 1 KiB: the small-packet
+               kernels, whose waves are then not packed)
+    gapped     in order, 1-40 random bytes between packets (the tail granule of
+               a segment is never the next packet's first bytes)
+    shuffled / reversed            the packed buffer's index permuted / reversed
+    wave_shuffled                  permuted inside each group of 64 (a wave's
+                                   region is compact, its packets out of order)"""
+    rng = np.random.default_rng(9)
     if layout == "sparse4k":
-        data, off, cap = pktutil.pack(packets, align=4096)
-    else:
+        return pktutil.pack(packets, align=4096)
+    if layout == "gapped":
+        offs, o = [], 0
+        for p in packets:
+            o += int(rng.integers(1, 41))
+            offs.append(o)
+            o += len(p)
+        data = np.zeros(o + 64, np.uint8)
+        for q, p in zip(offs, packets):
+            data[q:q + len(p)] = np.frombuffer(p, np.uint8) if len(p) else []
+        return data, np.array(offs, np.uint64), np.array([len(p) for p in packets], np.uint32)
+    if layout == "sparse_mix":
         data, off, cap = pktutil.pack(packets)
-        order = np.arange(len(packets))
-        if layout == "shuffled":
-            order = np.random.default_rng(9).permutation(len(packets))
-        else:
-            order = order[::-1].copy()
-        off, cap = off[order], cap[order]
+        far = np.arange(len(packets)) % 8 == 5
+        end = (len(data) + 4095) // 4096 * 4096
+        new_off = off.copy()
+        new_off[far] = end + 4096 * np.arange(far.sum(), dtype=np.uint64) + np.uint64(3)
+        big = np.zeros(int(new_off[far][-1]) + 4096 + 64, np.uint8)
+        big[:len(data)] = data
+        for q, o, c in zip(new_off[far], off[far], cap[far]):
+            big[int(q):int(q) + int(c)] = data[int(o):int(o) + int(c)]
+        return big, new_off, cap
+    data, off, cap = pktutil.pack(packets)
+    order = np.arange(len(packets))
+    if layout == "shuffled":
+        order = rng.permutation(len(packets))
+    elif layout == "reversed":
+        order = order[::-1].copy()
+    elif layout == "wave_shuffled":
+        for k in range(0, len(order), 64):
+            order[k:k + 64] = rng.permutation(order[k:k + 64])
+    return data, off[order], cap[order]
+
+
+# the kernels the no-layout runs must take (gpk_decode_kernel_name): the
+# stream-before-parse kernel for parsers with IPv6, the dword-aligned 5-chunk
+# kernel for parsers without; batches with a mean packet of 1 KiB or more take
+# the 80-VGPR 6-chunk kernel
+PHASE_B_KERNELS = {
+    "statsassembly": "gpk::decode_sb_kernel<true,7,6>",
+    "raw_ip6": "gpk::decode_sb_kernel<true,7,6>",
+    "eth_ip4_tcp_payload": "gpk::decode_kernel<true,false,true,false,5,7,4>",
+}
+
+
+@pytest.mark.parametrize("layouts", [True, False])
+@pytest.mark.parametrize("layout", ["sparse4k", "sparse_mix", "gapped", "shuffled", "reversed", "wave_shuffled"])
+def test_phase_b_layouts(gpu_ctx, layout, layouts):
+    """The L4 segment sums take the dense prefix stream when a wave's segments
+    share a compact region and the per-segment stream otherwise: sparse,
+    gapped, shuffled and reversed layouts must all give the oracle's results
+    (layers_decoder.go:60-79 and tcpip.go:54-69 on packets at arbitrary
+    offsets, include/gpk.h gpk_batch), through the layout kernel and through
+    the default small-packet kernels (their next-lane tail rules and their
+    fallbacks when a wave's packets are not packed)."""
+    packets = pktutil.fuzz_packets(4242, 12000) + golden_packets()
+    data, off, cap = phase_b_layout(packets, layout)
     for name in ("statsassembly", "eth_ip4_tcp_payload", "raw_ip6"):
         cfg = CONFIGS[name]
-        dev = gpu_ctx.decode_host(device_parser(cfg), data, off, cap, layouts=True)
-        ref = oracle_parser(cfg).decode(data, off, cap, nthreads=8, layouts=True)
-        assert_same(dev, ref, "%s/%s" % (layout, name))
+        dp = device_parser(cfg)
+        if not layouts:
+            want = ("gpk::decode_kernel<true,false,true,false,6,6,16>" if layout == "sparse4k"
+                    else PHASE_B_KERNELS[name])
+            assert gpu_ctx.kernel_name(dp, data, off, cap, layouts=False) == want, (layout, name)
+        dev = gpu_ctx.decode_host(dp, data, off, cap, layouts=layouts)
+        ref = oracle_parser(cfg).decode(data, off, cap, nthreads=8, layouts=layouts)
+        assert_same(dev, ref, "%s/%s/layouts=%s" % (layout, name, layouts))

@@ -222,6 +222,37 @@ def test_ipv6_jumbogram():
     assert ip6.HopByHop.Options[0].OptionType == 0xC2 and ip6.HopByHop.Options[0].OptionData == bytes([0, 1, 0, 8])
 
 
+# layers/tcpip_test.go:138-186 TestIPv6JumbogramUDPChecksum: ipv6UDPChecksumJumbogram
+# = 0xcda8 (tcpip_test.go:19), the reference's one vector for a segment over 64 KiB
+# and for the pseudo-header's length>>16 term (tcpip.go:54-69: 65544 bytes)
+def test_ipv6_jumbogram_udp_checksum():
+    pkt = pktutil.ipv6_udp_jumbogram()
+    seg, src, dst = pkt[48:], pkt[8:24], pkt[24:40]
+    assert len(seg) == 65544
+    # computeChecksum (tcpip.go:54-69) as the oracle restates it: pseudo-header
+    # addresses + protocol + length & 0xffff + length >> 16, then ComputeChecksum
+    # over the segment mod 2^32 (checksum.go:35-50) and FoldChecksum
+    csum = O.compute_checksum(src + dst) + 17 + (len(seg) & 0xFFFF) + (len(seg) >> 16)
+    assert O.fold_checksum(O.compute_checksum(seg, csum)) == 0xcda8
+    # the same through the oracle's decode: gopacket's test reads the layers of
+    # NewPacket, where the HopByHop layer's payload feeds UDP; DecodingLayerParser
+    # hands UDP the IPv6 Payload, which keeps the HopByHop header (ip6.go:249-256,
+    # SURVEY P4): the UDP decoder sees Length 1 there and fails (udp.go:52-53)
+    r = decode_one(21, [IP6, EXT, UDP, PAY], pkt)
+    assert r["decoded"] == [21] and r["err"] == 61 and r["args"][0] == 1
+    # a jumbogram whose IPv6 Payload is the UDP segment as DecodeLayers slices it:
+    # a 16-byte HopByHop header (PadN, the Jumbo TLV at 4n+2, PadN) whose bytes 4-5
+    # are 0, so the UDP decoder reads them as a jumbo Length 0 (udp.go:49-50)
+    # and sums the whole rest of the packet, with length>>16 = 1
+    pkt2 = pktutil.ipv6_udp_jumbogram(hbh16=True)
+    r = decode_one(21, [IP6, EXT, UDP, PAY], pkt2)
+    assert r["decoded"] == [21, 45, 2] and r["err"] == 0 and r["st"] & (1 << 22)
+    seg2 = pkt2[40:]
+    csum2 = O.compute_checksum(src + dst) + 17 + (len(seg2) & 0xFFFF) + (len(seg2) >> 16)
+    existing = struct.unpack(">H", seg2[6:8])[0]
+    assert r["rec"]["l4_csum"] == O.fold_checksum(O.compute_checksum(seg2, csum2) - existing)
+
+
 # pcap/pcap_test.go:50-117: test_ethernet.pcap is 10 Eth/IPv4/TCP packets
 def test_pcap_ethernet_fixture():
     link, pkts = pktutil.read_pcap(pktutil.GOLDEN + "/test_ethernet.pcap")
