@@ -824,6 +824,84 @@ def bpf_filter_bench(ctx, n=64 * 2**20, reps=10):
                          "packets in HBM", packets=n, programs=out)
 
 
+def fields_bench(ctx, name="c4", n=64 * 2**20, reps=5, check_packets=4 << 20):
+    """Layer fields with the decode (gpk_decode_batch_fields, no layouts: ONE
+    launch that also writes each packet's 128-byte gpk_fields record) against
+    the two-launch form (decode with layouts, then gpk_extract_fields), on the
+    64M C4 batch in HBM; HIP events on the launch stream, median of reps.
+    frac counts the algorithmic read bytes (caplen + 12) like the decode rows;
+    written bytes per packet are reported beside it. The first check_packets
+    packets of the fused run are compared with the oracle (records, error
+    arguments, flows, fields)."""
+    import torch
+    from gopacket_amd import _lib, engine, synth
+    from oracle import oracle as O
+    cfg = CONFIGS[name]
+    parser = engine.ParserConfig(17, [engine.DECODER_KINDS[d] for d in cfg["decoders"]], outputs=cfg["outputs"])
+    stream = torch.cuda.current_stream()
+    data, off, cap = synth.device_batch(cfg["synth"], 0, n, stream=stream)
+    rec = torch.empty(n * 16, dtype=torch.uint8, device="cuda")
+    err = torch.zeros(2 * n, dtype=torch.int32, device="cuda")
+    fl = torch.empty(3 * n, dtype=torch.int64, device="cuda")
+    fields = torch.empty(n * 128, dtype=torch.uint8, device="cuda")
+    lay = torch.empty(n * 64, dtype=torch.uint8, device="cuda")
+    payload = int(cap.sum(dtype=torch.int64).item())
+    algo = payload + INDEX_BYTES * n
+
+    def timed(fn):
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        ts = []
+        for k in range(reps + 2):
+            ev[0].record(stream)
+            fn()
+            ev[1].record(stream)
+            torch.cuda.synchronize()
+            if k >= 2:
+                ts.append(ev[0].elapsed_time(ev[1]))
+        return sorted(ts)[len(ts) // 2]
+
+    two = timed(lambda: (ctx.decode_device(parser, data, off, cap, rec, err, fl, lay, stream=stream),
+                         ctx.extract_fields(data, off, cap, lay, fields, stream=stream)))
+    fused = timed(lambda: ctx.decode_device_fields(parser, data, off, cap, rec, err, fl, fields, stream=stream))
+    # parity of the fused run (the last launch wrote every output)
+    dec = [ORACLE_DEC[d] for d in cfg["decoders"]]
+    p = O.OracleParser(17, dec, outputs=cfg["outputs"])
+    bad = 0
+    chunk = 1 << 20
+    for a in range(0, min(n, check_packets), chunk):
+        b = min(n, a + chunk)
+        o = off[a:b].cpu().numpy().astype(np.uint64)
+        c = cap[a:b].cpu().numpy().astype(np.uint32)
+        lo, hi = int(o.min()), int((o + c).max())
+        host = np.zeros(hi - lo + 16, np.uint8)
+        host[:hi - lo] = data[lo:hi].cpu().numpy()
+        ref = p.decode(host, o - np.uint64(lo), c, nthreads=host_cores()[0], layouts=True)
+        ok = rec[a * 16:b * 16].cpu().numpy().view(_lib.RECORD_DTYPE) == ref["records"]
+        ok &= (err[2 * a:2 * b].cpu().numpy().view(np.uint32).reshape(-1, 2) == ref["err_args"].reshape(-1, 2)).all(1)
+        rf = ref["flows"].reshape(3, -1)
+        for k in range(3):
+            ok &= fl[k * n + a:k * n + b].cpu().numpy().view(np.uint64) == rf[k]
+        want = O.extract_fields(host, o - np.uint64(lo), ref["layouts"])
+        ok &= (fields[a * 128:b * 128].cpu().numpy().reshape(-1, 128) == want).all(1)
+        bad += int((~ok).sum())
+    written = 16 + 24 + 128  # record, three flow hashes, fields (+8 on error)
+    ach = algo / (fused * 1e-3) / 1e9
+    res = dict(workload=CONFIGS[name]["workload"] + " + layer fields (gpk_decode_batch_fields)",
+               kernel=ctx.kernel_name(parser, data, off, cap, layouts=_lib.NAME_FIELDS),
+               blocks_per_cu=ctx.occupancy(parser, data, off, cap, layouts=_lib.NAME_FIELDS),
+               kernel_ms=round(fused, 4), value=round(n / fused / 1e3, 2), unit="Mpkts/s",
+               achieved_GBps=round(ach, 1), frac=round(ach / HBM_PEAK_GBS, 4),
+               written_bytes_per_packet=written,
+               read_plus_written_GBps=round((algo + written * n) / (fused * 1e-3) / 1e9, 1),
+               two_launch_ms=round(two, 4), two_launch_kernels=[ctx.kernel_name(parser, data, off, cap, layouts=True),
+                                                                "fields_kernel"],
+               parity=("bit-exact" if not bad else "MISMATCH (%d packets)" % bad) +
+               " (first %d packets vs oracle: records, error arguments, flows, fields)" % min(n, check_packets))
+    del data, off, cap, rec, err, fl, fields, lay
+    torch.cuda.empty_cache()
+    return res
+
+
 def load_traffic(name, n):
     """HBM bytes per launch of the decode kernel from the committed PMC
     profile (profiles/hbm_traffic.json, tools/make_profiles.py): measured
@@ -860,6 +938,8 @@ def main():
     ap.add_argument("--flows", action="store_true",
                     help="also time row (f)3: flow-keyed grouping of 64M C6 packets (gpk_group_batch)")
     ap.add_argument("--bpf", action="store_true", help="also time row (f)4: classic BPF over 64M C4 packets")
+    ap.add_argument("--no-fields", action="store_true",
+                    help="skip the layer-fields row (64M C4 decode + fields in one launch vs two)")
     ap.add_argument("--tables", default="auto", choices=["auto", "global"],
                     help="next-layer tables: compact LDS copy (auto) or device-memory tables (global)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
@@ -928,6 +1008,8 @@ def main():
             out["configs"][name] = row
         if args.pcie and world == 1:
             out["pcie_inclusive"] = pcie_inclusive(head, ctx)
+        if world == 1 and not args.no_fields:
+            out["fields"] = fields_bench(ctx, n=args.packets)
         threads = host_cores()[0]
         if args.c5 > 0 and world == 1:
             out["c5"] = c5_replay(ctx, gib=args.c5, cpu_threads=threads)

@@ -51,14 +51,16 @@ FIELDS_DTYPE = np.dtype({
               "ip6_version", "ip4_checksum", "ip6_traffic_class", "ip6_next_header", "ip6_flow_label", "ip6_length",
               "ip6_hop_limit", "tcp_data_offset", "ip4_src", "ip4_dst", "ip6_src", "ip6_dst", "tcp_src_port",
               "tcp_dst_port", "tcp_seq", "tcp_ack", "tcp_flags", "tcp_window", "tcp_checksum", "tcp_urgent",
-              "udp_src_port", "udp_dst_port", "udp_length", "udp_checksum", "reserved"],
+              "udp_src_port", "udp_dst_port", "udp_length", "udp_checksum", "ip4_start", "tcp_start",
+              "ip4_opt_map", "tcp_opt_map"],
     "formats": ["<u4", "<u2", "<u2", ("u1", (6,)), ("u1", (6,)), "<u2", "<u2", "u1", "u1", "u1", "u1", "<u2", "<u2",
                 "<u2", "u1", "u1", "<u2", "u1", "u1", "<u4", "<u2", "u1", "u1", ("u1", (4,)), ("u1", (4,)),
                 ("u1", (16,)), ("u1", (16,)), "<u2", "<u2", "<u4", "<u4", "<u2", "<u2", "<u2", "<u2", "<u2", "<u2",
-                "<u2", "<u2", ("u1", (12,))],
+                "<u2", "<u2", "u1", "u1", ("u1", (5,)), ("u1", (5,))],
     "offsets": [0, 4, 6, 8, 14, 20, 22, 24, 25, 26, 27, 28, 30, 32, 34, 35, 36, 38, 39, 40, 44, 46, 47, 48, 52, 56, 72,
-                88, 90, 92, 96, 100, 102, 104, 106, 108, 110, 112, 114, 116],
+                88, 90, 92, 96, 100, 102, 104, 106, 108, 110, 112, 114, 116, 117, 118, 123],
     "itemsize": 128})
+NAME_FIELDS = 2  # gpk_decode_kernel_name / gpk_decode_occupancy: the fused fields launch
 TCP_FLAG_BITS = dict(FIN=1, SYN=2, RST=4, PSH=8, ACK=16, URG=32, ECE=64, CWR=128, NS=256)
 # gpk_layout slot -> decoder kind (slot 7: Payload or Fragment)
 LAYOUT_SLOTS = (DEC_ETHERNET, DEC_DOT1Q, DEC_IPV4, DEC_IPV6, DEC_IPV6_EXT, DEC_TCP, DEC_UDP, DEC_PAYLOAD)
@@ -68,7 +70,8 @@ EXPORTS = (
     "gpk_parser_create", "gpk_parser_destroy", "gpk_parser_add_decoder", "gpk_parser_set_options",
     "gpk_parser_set_outputs", "gpk_parser_decoder_for", "gpk_parser_set_ethertype",
     "gpk_parser_set_ipprotocol", "gpk_parser_set_tcp_port", "gpk_parser_set_udp_port", "gpk_ctx_create",
-    "gpk_ctx_destroy", "gpk_ctx_set_table_mode", "gpk_decode_batch", "gpk_extract_fields", "gpk_decode_kernel_name", "gpk_decode_occupancy", "gpk_diag_set_buffer", "gpk_decode_batch_host",
+    "gpk_ctx_destroy", "gpk_ctx_set_table_mode", "gpk_decode_batch", "gpk_decode_batch_fields", "gpk_extract_fields",
+    "gpk_decode_kernel_name", "gpk_decode_occupancy", "gpk_diag_set_buffer", "gpk_decode_batch_host",
     "gpk_decoded_list",
     "gpk_decoded_list_host", "gpk_host_alloc", "gpk_host_free", "gpk_format_error", "gpk_layer_type_name", "gpk_code_layer_type", "gpk_strerror",
     "gpk_last_hip_error", "gpk_abi_version",
@@ -228,6 +231,7 @@ def lib():
         "gpk_decode_batch": ([vp, vp, P(Batch), P(Results), vp], c_int),
         "gpk_decode_batch_host": ([vp, vp, P(Batch), P(Results)], c_int),
         "gpk_extract_fields": ([P(Batch), vp, vp, vp], c_int),
+        "gpk_decode_batch_fields": ([vp, vp, P(Batch), P(Results), vp, vp], c_int),
         "gpk_decode_kernel_name": ([vp, vp, P(Batch), c_int, ctypes.c_char_p, ctypes.c_size_t], c_int),
         "gpk_decode_occupancy": ([vp, vp, P(Batch), c_int, P(c_int)], c_int),
         "gpk_diag_set_buffer": ([vp], c_int),

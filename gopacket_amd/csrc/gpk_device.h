@@ -73,6 +73,7 @@ struct KParams {
   uint64_t* khash;
   int32_t* kcode;
   uint64_t* diag;           // GPK_DIAG_TIMES builds only: 8 u64 per wave (gpk_diag_set_buffer)
+  gpk_fields* fields;       // fused layer fields (gpk_decode_batch_fields), the fields kernels only
 };
 
 // Straight-line common-case parse (fast_parser below). Each bit says the

@@ -9,16 +9,12 @@
 // slot, reads each present slice's header words from there (unaligned
 // ds_read_b32; from memory past the run), and the wave writes its 64 records
 // through LDS as eight coalesced 1 KiB stores.
-// Field by field this restates:
-//   Ethernet  layers/ethernet.go:42-55  (EthernetType < 0x0600: Length, LLC)
-//   Dot1Q     layers/dot1q.go:28-41     (the tag control word, Type)
-//   IPv4      layers/ip4.go:178-271     (Length 0 = the slice's length, TSO)
-//   IPv6      layers/ip6.go:221-278
-//   TCP       layers/tcp.go:292-313
-//   UDP       layers/udp.go:30-43
+// The field assignments are gpk_fields.h (shared with the decode kernel's
+// fused-fields variant).
 #include <hip/hip_runtime.h>
 
 #include "../../include/gpk.h"
+#include "gpk_fields.h"
 
 namespace {
 
@@ -69,7 +65,9 @@ struct Hdr {
     const uint32_t w = ldbytes(pk + p, 2);
     return (w & 0xffu) << 8 | w >> 8;
   }
-  __device__ __forceinline__ uint32_t be32(uint32_t p) const { return __builtin_bswap32(u32(p)); }
+  __device__ __forceinline__ uint32_t u8(uint32_t p) const {
+    return p < win ? (uint32_t)reinterpret_cast<const uint8_t*>(fields_smem)[lb + p] : (uint32_t)pk[p];
+  }
 };
 
 __global__ __launch_bounds__(kBlock) void fields_kernel(const uint8_t* data, const uint64_t* offsets,
@@ -102,68 +100,10 @@ __global__ __launch_bounds__(kBlock) void fields_kernel(const uint8_t* data, con
   const uint32_t st[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
   const uint32_t en[8] = {e0.x, e0.y, e0.z, e0.w, e1.x, e1.y, e1.z, e1.w};
   uint32_t w[32];
+  uint32_t present = 0;
 #pragma unroll
-  for (int k = 0; k < 32; k++) w[k] = 0;
-#pragma unroll
-  for (int k = 0; k < 8; k++) w[0] |= (st[k] != GPK_LAYOUT_ABSENT ? 1u : 0u) << k;
-  if (st[GPK_DEC_ETHERNET - 1] != GPK_LAYOUT_ABSENT) {  // ethernet.go:46-55
-    const uint32_t d = st[GPK_DEC_ETHERNET - 1];
-    uint32_t et = h.be16(d + 12), len = 0;
-    if (et < 0x0600) {
-      len = et;
-      et = 0;  // EthernetTypeLLC
-    }
-    w[1] = et | len << 16;
-    w[2] = h.u32(d);  // DstMAC, SrcMAC: bytes 8..19 of the record
-    w[3] = h.u32(d + 4);
-    w[4] = h.u32(d + 8);
-  }
-  if (st[GPK_DEC_DOT1Q - 1] != GPK_LAYOUT_ABSENT) {  // dot1q.go:33-37
-    const uint32_t d = st[GPK_DEC_DOT1Q - 1];
-    w[5] = h.be16(d) | h.be16(d + 2) << 16;
-  }
-  if (st[GPK_DEC_IPV4 - 1] != GPK_LAYOUT_ABSENT) {  // ip4.go:183-193, 257-267
-    const uint32_t d = st[GPK_DEC_IPV4 - 1];
-    const uint32_t b0 = h.u32(d);  // bytes 0..3
-    uint32_t length = (b0 >> 16 & 0xffu) << 8 | b0 >> 24;
-    if (length == 0) length = (en[GPK_DEC_IPV4 - 1] - d) & 0xffffu;
-    const uint32_t b4 = h.u32(d + 4), b8 = h.u32(d + 8);  // Id, flags|frag; TTL, Protocol, Checksum
-    w[6] = (b0 & 0xffu) >> 4 | (b0 & 0x0fu) << 8 | (b0 >> 8 & 0xffu) << 16 | (b8 & 0xffu) << 24;
-    w[7] = length | ((b4 & 0xffu) << 8 | (b4 >> 8 & 0xffu)) << 16;
-    w[8] = ((b4 >> 16 & 0xffu) << 8 | b4 >> 24) | (b8 >> 8 & 0xffu) << 16;
-    w[9] = (b8 >> 16 & 0xffu) << 8 | b8 >> 24;
-    w[12] = h.u32(d + 12);
-    w[13] = h.u32(d + 16);
-  }
-  if (st[GPK_DEC_IPV6 - 1] != GPK_LAYOUT_ABSENT) {  // ip6.go:225-234
-    const uint32_t d = st[GPK_DEC_IPV6 - 1];
-    const uint32_t h0 = h.be32(d), b4 = h.u32(d + 4);
-    w[8] |= (h0 >> 28) << 24;                                          // Version
-    w[9] |= (h0 >> 20 & 0xffu) << 16 | (b4 >> 16 & 0xffu) << 24;        // TrafficClass, NextHeader
-    w[10] = h0 & 0x000fffffu;                                          // FlowLabel
-    w[11] = ((b4 & 0xffu) << 8 | (b4 >> 8 & 0xffu)) | (b4 >> 24) << 16;  // Length, HopLimit
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-      w[14 + k] = h.u32(d + 8 + 4 * k);
-      w[18 + k] = h.u32(d + 24 + 4 * k);
-    }
-  }
-  if (st[GPK_DEC_TCP - 1] != GPK_LAYOUT_ABSENT) {  // tcp.go:296-313
-    const uint32_t d = st[GPK_DEC_TCP - 1];
-    const uint32_t b0 = h.u32(d), b12 = h.u32(d + 12);  // ports; DataOffset|NS, flags, Window
-    w[11] |= (b12 & 0xffu) >> 4 << 24;
-    w[22] = ((b0 & 0xffu) << 8 | (b0 >> 8 & 0xffu)) | ((b0 >> 16 & 0xffu) << 8 | b0 >> 24) << 16;
-    w[23] = h.be32(d + 4);
-    w[24] = h.be32(d + 8);
-    w[25] = (b12 >> 8 & 0xffu) | (b12 & 1u) << 8 | ((b12 >> 16 & 0xffu) << 8 | b12 >> 24) << 16;
-    w[26] = h.be16(d + 16) | h.be16(d + 18) << 16;
-  }
-  if (st[GPK_DEC_UDP - 1] != GPK_LAYOUT_ABSENT) {  // udp.go:34-41
-    const uint32_t d = st[GPK_DEC_UDP - 1];
-    const uint32_t b0 = h.u32(d), b4 = h.u32(d + 4);
-    w[27] = ((b0 & 0xffu) << 8 | (b0 >> 8 & 0xffu)) | ((b0 >> 16 & 0xffu) << 8 | b0 >> 24) << 16;
-    w[28] = ((b4 & 0xffu) << 8 | (b4 >> 8 & 0xffu)) | ((b4 >> 16 & 0xffu) << 8 | b4 >> 24) << 16;
-  }
+  for (int k = 0; k < 8; k++) present |= (st[k] != GPK_LAYOUT_ABSENT ? 1u : 0u) << k;
+  gpkf::fields_words(h, present, st, en[GPK_DEC_IPV4 - 1], w);
   // Records out through LDS: lane l's 128 bytes go to the wave's staging area
   // (chunk c at chunk position c ^ (l & 7), spreading the banks), then store
   // k of the wave writes its 1 KiB of records contiguously (coalesced), lane l
@@ -188,7 +128,9 @@ __global__ __launch_bounds__(kBlock) void fields_kernel(const uint8_t* data, con
 }  // namespace
 
 static_assert(sizeof(gpk_fields) == 128, "gpk_fields is 128 bytes");
-static_assert(offsetof(gpk_fields, tcp_seq) == 92 && offsetof(gpk_fields, udp_checksum) == 114, "gpk_fields layout");
+static_assert(offsetof(gpk_fields, tcp_seq) == 92 && offsetof(gpk_fields, udp_checksum) == 114 &&
+                  offsetof(gpk_fields, ip4_start) == 116 && offsetof(gpk_fields, tcp_opt_map) == 123,
+              "gpk_fields layout");
 
 extern "C" int gpk_extract_fields(const gpk_batch* b, const gpk_layout* layouts, gpk_fields* fields, void* stream) {
   if (!b || (b->n && (!b->data || !b->offsets || !b->caplens || !layouts || !fields))) return GPK_EINVAL;

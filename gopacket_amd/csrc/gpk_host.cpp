@@ -26,6 +26,8 @@
 extern "C" hipError_t gpk_launch_decode(const gpk::KParams* P, int with_l4, int with_layout, hipStream_t stream);
 extern "C" int gpk_launch_describe(const gpk::KParams* P, int with_l4, int with_layout, char* buf, size_t cap);
 extern "C" hipError_t gpk_launch_occupancy(const gpk::KParams* P, int with_l4, int with_layout, int* blocks);
+extern "C" hipError_t gpk_launch_decode_fields(const gpk::KParams* P, hipStream_t stream, int* occ);
+extern "C" int gpk_launch_describe_fields(const gpk::KParams* P, char* buf, size_t cap);
 extern "C" hipError_t gpk_launch_list(const gpk::KParams* P, uint64_t index, int64_t* out, uint32_t cap,
                                       uint32_t* out_n, hipStream_t stream);
 
@@ -571,6 +573,7 @@ static int make_params(gpk_ctx* c, const gpk_parser* p, const gpk_batch* b, cons
   P.khash = nullptr;
   P.kcode = nullptr;
   P.diag = g_diag.load();
+  P.fields = nullptr;
   return GPK_OK;
 }
 
@@ -591,6 +594,27 @@ int gpk_decode_batch(gpk_ctx* c, const gpk_parser* p, const gpk_batch* b, const 
   rc = upload(c, p, P, &slot, s);
   if (rc) return rc;
   HIPCHK(gpk_launch_decode(&P, (p->outputs & GPK_OUT_L4_CSUM) != 0, o->layouts != nullptr, s));
+  return note_launch(c, slot, s);
+}
+
+int gpk_decode_batch_fields(gpk_ctx* c, const gpk_parser* p, const gpk_batch* b, const gpk_results* o,
+                            gpk_fields* fields, void* stream) {
+  if (!o || (b && b->n && !fields)) return GPK_EINVAL;
+  if (o->layouts) {  // layouts too: the decode with layouts, then the extraction from them
+    int rc = gpk_decode_batch(c, p, b, o, stream);
+    return rc ? rc : gpk_extract_fields(b, o->layouts, fields, stream);
+  }
+  gpk::KParams P;
+  int rc = make_params(c, p, b, o, P);
+  if (rc) return rc;
+  P.fields = fields;
+  hipStream_t s = (hipStream_t)stream;
+  std::lock_guard<std::mutex> g(c->mu);
+  HIPCHK(hipSetDevice(c->device));
+  int slot = 0;
+  rc = upload(c, p, P, &slot, s);
+  if (rc) return rc;
+  HIPCHK(gpk_launch_decode_fields(&P, s, nullptr));
   return note_launch(c, slot, s);
 }
 
@@ -655,6 +679,7 @@ int gpk_decode_kernel_name(gpk_ctx* c, const gpk_parser* p, const gpk_batch* b, 
   int slot = 0;
   rc = upload(c, p, P, &slot, c->stream);
   if (rc) return rc;
+  if (with_layouts == GPK_NAME_FIELDS) return gpk_launch_describe_fields(&P, buf, cap);
   return gpk_launch_describe(&P, (p->outputs & GPK_OUT_L4_CSUM) != 0, with_layouts != 0, buf, cap);
 }
 
@@ -668,6 +693,11 @@ int gpk_decode_occupancy(gpk_ctx* c, const gpk_parser* p, const gpk_batch* b, in
   int slot = 0;
   rc = upload(c, p, P, &slot, c->stream);
   if (rc) return rc;
+  if (with_layouts == GPK_NAME_FIELDS) {
+    P.fields = reinterpret_cast<gpk_fields*>(16);  // described, never written
+    HIPCHK(gpk_launch_decode_fields(&P, nullptr, blocks_per_cu));
+    return GPK_OK;
+  }
   HIPCHK(gpk_launch_occupancy(&P, (p->outputs & GPK_OUT_L4_CSUM) != 0, with_layouts != 0, blocks_per_cu));
   return GPK_OK;
 }

@@ -34,6 +34,7 @@
 #include <cstdio>
 
 #include "gpk_device.h"
+#include "gpk_fields.h"
 
 namespace gpk {
 
@@ -68,6 +69,9 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 #define GPK_PB_DEPTH7SB 5  // ... in the stream-before-parse kernel's phase B after the parse (the fallback of waves whose
                            // packets are not packed; 6: 20 B of scratch, 8: 40 B; 5 and below: none)
 #endif
+#ifndef GPK_PB_DEPTHF
+#define GPK_PB_DEPTHF 4  // ... in its fused-fields variant
+#endif
 #ifndef GPK_PB_IDPERM
 #define GPK_PB_IDPERM 1  // dense phase B: lanes outside their target pass pull their own prefix (no LDS bank conflicts)
 #endif
@@ -97,6 +101,9 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 #endif
 #ifndef GPK_SB_WAVES
 #define GPK_SB_WAVES GPK_SMALL_WAVES  // ... its register budget (waves per SIMD; LDS allows 6 blocks per CU)
+#endif
+#ifndef GPK_SBF_WAVES
+#define GPK_SBF_WAVES 6  // ... its fused-fields variant (gpk_decode_batch_fields; 72 VGPRs: 68 B of scratch)
 #endif
 #ifndef GPK_SB_DEPTH
 #define GPK_SB_DEPTH 6  // ... its stream depth (passes in flight; 8 no better)
@@ -880,8 +887,50 @@ __device__ __forceinline__ u32x4 sb_chunk(const KParams& P, uint64_t ga, uint64_
   return *reinterpret_cast<const u32x4*>(P.data + ga);
 }
 
+// ---- Fused layer fields (gpk_decode_batch_fields) ---------------------------
+// The header reader gpk_fields.h expects, over the lane's LDS window (bytes
+// past it from memory, byte by byte: a field never reads past its own bytes).
+struct RdF {
+  Rd r;
+  __device__ __forceinline__ uint32_t u8(uint32_t p) const { return rd8(r, p); }
+  __device__ __forceinline__ uint32_t be16(uint32_t p) const { return rd16(r, p); }
+  __device__ __forceinline__ uint32_t u32(uint32_t p) const {
+    if (p + 4 <= r.win) return lds32u(r.lb + p);
+    return rd8(r, p) | rd8(r, p + 1) << 8 | rd8(r, p + 2) << 16 | rd8(r, p + 3) << 24;
+  }
+};
+
+// The wave's 64 records of 128 bytes out as coalesced stores, staged through
+// the wave's LDS window slots (>= 4 KiB) in two halves: lane l puts the 64
+// bytes of its record's half into LDS (16-byte chunk c at chunk position
+// c ^ (l & 3), spreading the banks), then store k of the half writes records
+// 16k .. 16k+15, lane l carrying chunk l & 3 of record 16k + l / 4 (16 runs of
+// 64 contiguous bytes per instruction; the halves meet in L2). Runs with the
+// whole wave active, after every lane's last window read (LDS operations of a
+// wave complete in order; the compiler barriers keep them in program order).
+__device__ __forceinline__ void fields_store(const KParams& P, const uint32_t (&w)[32], uint32_t wave_dw, uint32_t lane,
+                                             uint64_t first) {
+  u32x4* out = reinterpret_cast<u32x4*>(P.fields + first);
+#pragma unroll
+  for (int h = 0; h < 2; h++) {
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (uint32_t c = 0; c < 4; c++)
+      *reinterpret_cast<u32x4*>(gpk_smem + wave_dw + lane * 16 + 4 * (c ^ (lane & 3))) =
+          u32x4{w[16 * h + 4 * c], w[16 * h + 4 * c + 1], w[16 * h + 4 * c + 2], w[16 * h + 4 * c + 3]};
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (uint32_t k = 0; k < 4; k++) {
+      const uint32_t rr = 16 * k + (lane >> 2), c = lane & 3;
+      const u32x4 v = *reinterpret_cast<const u32x4*>(gpk_smem + wave_dw + rr * 16 + 4 * (c ^ (rr & 3)));
+      if (first + rr < P.n) __builtin_nontemporal_store(v, out + 8 * rr + 4 * h + c);
+    }
+  }
+  asm volatile("" ::: "memory");
+}
+
 template <bool kL4, bool kLayout, class TT, bool kKeys, int W, int O, int AL, int kSlotStride = slot_dw_of<W, AL>(),
-          int kEarly = -1, bool kSB = false>
+          int kEarly = -1, bool kSB = false, bool kFields = false>
 __device__ __forceinline__ void decode_packet(const KParams& P, const TT& T, uint64_t i, bool active, uint64_t off,
                                               uint32_t cl, const WinGeo& g, uint32_t slot_dw, uint32_t lane,
                                               uint64_t* dt, const SbPkt sb = SbPkt{0, 0, -1, false}) {
@@ -890,7 +939,8 @@ __device__ __forceinline__ void decode_packet(const KParams& P, const TT& T, uin
 
   // Phase B's stream over the wave's packets starts now when they are packed:
   // its first D KiB load while the headers are parsed.
-  constexpr int D = kLayout ? 4 : (O > 6 ? (kSB ? GPK_PB_DEPTH7SB : GPK_PB_DEPTH7) : GPK_PB_DEPTH);  // layouts: fewer registers left
+  // (layouts: fewer registers left; the stream-before-parse kernel's phase B after the parse is its fallback)
+  constexpr int D = kLayout ? 4 : (kSB ? (kFields ? GPK_PB_DEPTHF : GPK_PB_DEPTH7SB) : (O > 6 ? GPK_PB_DEPTH7 : GPK_PB_DEPTH));
   // early passes: as many as the kernel's register budget carries through
   // DecodeLayers untouched (tools/check_stream_isa.py)
   constexpr int E = kEarly >= 0 ? kEarly : ((kLayout || kKeys) ? 0 : (O > 6 ? GPK_PB_EARLY7 : GPK_PB_EARLY));
@@ -923,6 +973,22 @@ __device__ __forceinline__ void decode_packet(const KParams& P, const TT& T, uin
   if (active && !done) s = run_parser<false>(P, T, r, cl, q);
 #endif
 
+  // fused fields: the decoders' last slices in compact form (presence, the
+  // starts the fields read, the IPv4 end), live to the fields epilogue instead
+  // of the whole parse state
+  uint32_t fpres = 0, fip4e = 0;
+  uint32_t fst[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (kFields && active) {
+    const int slot_kind[8] = {GPK_DEC_ETHERNET, GPK_DEC_DOT1Q, GPK_DEC_IPV4, GPK_DEC_IPV6,
+                              GPK_DEC_IPV6_EXT, GPK_DEC_TCP,   GPK_DEC_UDP,  GPK_DEC_PAYLOAD};
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      const int kd = k == 7 && !clean(q, GPK_DEC_PAYLOAD) ? GPK_DEC_FRAGMENT : slot_kind[k];
+      fpres |= clean(q, kd) ? 1u << k : 0u;
+      if (k != 4 && k != 7) fst[k] = q.start(kd);
+    }
+    fip4e = q.end(GPK_DEC_IPV4);
+  }
   uint32_t st = (s.err & GPK_ST_ERR_MASK) | (s.trunc ? GPK_ST_TRUNCATED : 0u) |
                 ((q.nlayers > GPK_ST_NLAYERS_MASK ? GPK_ST_NLAYERS_MASK : q.nlayers) << GPK_ST_NLAYERS_SHIFT);
   uint32_t ip4c = 0, l4c = 0;
@@ -1023,6 +1089,19 @@ __device__ __forceinline__ void decode_packet(const KParams& P, const TT& T, uin
   }
   const uint32_t lay_lo = (uint32_t)q.layers, lay_hi = (uint32_t)(q.layers >> 32);
 
+  // Fused layer fields (gpk_decode_batch_fields): the fields of the decoders'
+  // last slices (gpk_fields.h) read from this lane's header window, then the
+  // wave's records staged through its window slots. Called once the windows
+  // are no longer needed (after the stream-before-parse correction; before the
+  // phase-B stream of a wave that takes it after the parse, whose head/tail
+  // chunks then come from memory): the window reads and the stream's slots
+  // never hold registers at the same time.
+  auto emit_fields = [&]() __attribute__((always_inline)) {
+    uint32_t fw[32];
+    gpkf::fields_words(RdF{r}, fpres, fst, fip4e, fw);
+    fields_store(P, fw, slot_dw - lane * kSlotStride, lane, i - lane);
+  };
+
   // ---- Phase B: segment sums ---------------------------------------------
 #if GPK_DIAG_TIMES
   dt[3] = __builtin_amdgcn_s_memrealtime();
@@ -1068,6 +1147,7 @@ __device__ __forceinline__ void decode_packet(const KParams& P, const TT& T, uin
       const bool udp = (st & GPK_ST_L4_UDP) != 0;
       if (l4c == jexist || (udp && jexist == 0)) st |= GPK_ST_L4_VALID;
     }
+    if (kFields) emit_fields();
 #if GPK_DIAG_TIMES
     dt[4] = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -1105,6 +1185,11 @@ __device__ __forceinline__ void decode_packet(const KParams& P, const TT& T, uin
         tlds = (slot_dw + kSlotStride) * 4 + nm - (uint32_t)(je & 15);
         tafter = true;
       }
+    }
+    if (kFields) {  // the windows are staging space from here: head and tail chunks from memory
+      emit_fields();
+      hlds = tlds = ~0u;
+      tafter = false;
     }
     const uint32_t sum = segment_sums<D, E>(P, S, job, js, je, lane, hlds, tlds, tafter);
 #if GPK_DIAG_TIMES
@@ -1230,8 +1315,9 @@ __device__ __forceinline__ void window_dma(const KParams& P, const WinGeo& g, ui
   }
 }
 
-template <bool kCompact, int O, int W = 6>
+template <bool kCompact, int O, int W = 6, bool kFields = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(O, 8))) void decode_sb_kernel(KParams P) {
+  static_assert(!kFields || 64 * 4 * W >= 1024, "the fused fields stage a half record per lane in the wave's slots");
   constexpr int D = GPK_SB_DEPTH;
   constexpr int kSbStride = 4 * W;  // one 16-byte cell per window chunk, no pad
   const uint32_t tid = threadIdx.x, lane = tid & 63;
@@ -1262,7 +1348,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(O, 8))) 
   // the stream over the packets' extents, when packed
   uint64_t R0 = 0;
   uint32_t R = 0;
-  const bool ok = dense_region(active, c0.off, c0.off + c0.cl, R0, R);
+  const bool ok = dense_region(active && (P.outputs & GPK_OUT_L4_CSUM) != 0, c0.off, c0.off + c0.cl, R0, R);
   uint32_t L = 0;
   int32_t b = -1;
   if (ok) {
@@ -1285,13 +1371,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(O, 8))) 
   const uint64_t i1 = (uint64_t)blockIdx.x * kBlock + tid1;
   const WinGeo g1 = win_geo<W, 16>(P, c1, i1 < P.n);
   if (kCompact)
-    decode_packet<true, false, LTab, false, W, O, 16, kSbStride, 0, true>(P, LTab{P.cg, base}, i1, i1 < P.n, c1.off,
-                                                                         c1.cl, g1, tid1 * kSbStride, tid1 & 63, dt,
-                                                                         SbPkt{L, R0, b, ok});
+    decode_packet<true, false, LTab, false, W, O, 16, kSbStride, 0, true, kFields>(
+        P, LTab{P.cg, base}, i1, i1 < P.n, c1.off, c1.cl, g1, tid1 * kSbStride, tid1 & 63, dt, SbPkt{L, R0, b, ok});
   else
-    decode_packet<true, false, GTab, false, W, O, 16, kSbStride, 0, true>(P, GTab{P.tab}, i1, i1 < P.n, c1.off, c1.cl,
-                                                                         g1, tid1 * kSbStride, tid1 & 63, dt,
-                                                                         SbPkt{L, R0, b, ok});
+    decode_packet<true, false, GTab, false, W, O, 16, kSbStride, 0, true, kFields>(
+        P, GTab{P.tab}, i1, i1 < P.n, c1.off, c1.cl, g1, tid1 * kSbStride, tid1 & 63, dt, SbPkt{L, R0, b, ok});
 #if GPK_DIAG_TIMES
   dt[5] = __builtin_amdgcn_s_memrealtime();
   dt[6] = (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 4) | (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32;
@@ -1355,15 +1439,15 @@ hipError_t launch(const gpk::KParams* P, hipStream_t stream, int* occ) {
   return hipGetLastError();
 }
 
-template <bool kCompact, int O, int W = 6>
+template <bool kCompact, int O, int W = 6, bool kFields = false>
 hipError_t launch_sb(const gpk::KParams* P, hipStream_t stream, int* occ) {
   using namespace gpk;
   constexpr int fixed = kBlock * 4 * W * 4;
   const int lds = kCompact ? fixed + (int)((P->cg.words + GPK_BLOB_ROUND - 1) & ~(GPK_BLOB_ROUND - 1u)) * 4 : fixed;
-  if (occ) return resident_blocks(decode_sb_kernel<kCompact, O, W>, lds, occ);
+  if (occ) return resident_blocks(decode_sb_kernel<kCompact, O, W, kFields>, lds, occ);
   const uint64_t grid = (P->n + kBlock - 1) / kBlock;
   if (grid > 0xffffffffull) return hipErrorInvalidValue;
-  hipLaunchKernelGGL((decode_sb_kernel<kCompact, O, W>), dim3((unsigned)grid), dim3(kBlock), lds, stream, *P);
+  hipLaunchKernelGGL((decode_sb_kernel<kCompact, O, W, kFields>), dim3((unsigned)grid), dim3(kBlock), lds, stream, *P);
   return hipGetLastError();
 }
 
@@ -1434,11 +1518,27 @@ extern "C" hipError_t gpk_launch_occupancy(const gpk::KParams* P, int with_l4, i
 extern "C" int gpk_launch_describe(const gpk::KParams* P, int with_l4, int with_layout, char* buf, size_t cap) {
   const Sel s = select(P, with_l4, with_layout);
   if (s.sb)
-    return snprintf(buf, cap, "gpk::decode_sb_kernel<%s,%d,%d>", s.compact ? "true" : "false",
+    return snprintf(buf, cap, "gpk::decode_sb_kernel<%s,%d,%d,false>", s.compact ? "true" : "false",
                     s.O == GPK_WAVES_PER_EU ? s.O : GPK_SB_WAVES, gpk::kWinChunks);
   return snprintf(buf, cap, "gpk::decode_kernel<%s,%s,%s,%s,%d,%d,%d>", s.l4 ? "true" : "false",
                   s.layout ? "true" : "false", s.compact ? "true" : "false", s.keys ? "true" : "false", s.W,
                   s.W == 4 ? 6 : s.O, s.AL);
+}
+
+// The fused decode + layer fields launch (gpk_decode_batch_fields without
+// layouts): the stream-before-parse kernel with its fields epilogue, for every
+// parser and batch (its 6-chunk window holds every header the fast path reads;
+// the rest comes from memory). occ: report resident blocks instead; name:
+// describe it instead.
+extern "C" hipError_t gpk_launch_decode_fields(const gpk::KParams* P, hipStream_t stream, int* occ) {
+  if (!occ && P->n == 0) return hipSuccess;
+  if (P->key_kind || !P->fields) return hipErrorInvalidValue;
+  return P->ctab ? launch_sb<true, GPK_SBF_WAVES, gpk::kWinChunks, true>(P, stream, occ)
+                 : launch_sb<false, GPK_SBF_WAVES, gpk::kWinChunks, true>(P, stream, occ);
+}
+extern "C" int gpk_launch_describe_fields(const gpk::KParams* P, char* buf, size_t cap) {
+  return snprintf(buf, cap, "gpk::decode_sb_kernel<%s,%d,%d,true>", P->ctab ? "true" : "false", GPK_SBF_WAVES,
+                  gpk::kWinChunks);
 }
 
 extern "C" hipError_t gpk_launch_list(const gpk::KParams* P, uint64_t index, int64_t* out, uint32_t cap,

@@ -123,9 +123,27 @@ class Context:
         b = _lib.Batch(data.data_ptr(), offsets.data_ptr(), caplens.data_ptr(), n, data.numel())
         check(lib().gpk_extract_fields(ctypes.byref(b), layouts.data_ptr(), fields.data_ptr(), _stream_ptr(stream)))
 
-    def decode_host_fields(self, parser, data, offsets, caplens):
-        """decode_host with layouts, plus the layer fields of every packet, both
-        computed on the device (host arrays in and out; torch for the buffers)."""
+    def decode_device_fields(self, parser, data, offsets, caplens, records, err_args, flows, fields, layouts=None,
+                             stream=None):
+        """gpk_decode_batch_fields: decode_device plus the layer fields of every
+        packet (fields: 128 bytes per packet, FIELDS_DTYPE) in one launch
+        (layouts=None), or decode with layouts + extract_fields. Device tensors."""
+        n = offsets.numel()
+        if fields.numel() * fields.element_size() < 128 * n:
+            raise ValueError("fields needs 128 bytes per packet")
+        b = _lib.Batch(data.data_ptr(), offsets.data_ptr(), caplens.data_ptr(), n, data.numel())
+        r = _lib.Results(records.data_ptr(), err_args.data_ptr() if err_args is not None else None,
+                         flows.data_ptr() if flows is not None else None,
+                         layouts.data_ptr() if layouts is not None else None)
+        check(lib().gpk_decode_batch_fields(self.h, parser.h, ctypes.byref(b), ctypes.byref(r), fields.data_ptr(),
+                                            _stream_ptr(stream)))
+
+    def decode_host_fields(self, parser, data, offsets, caplens, layouts=True):
+        """decode_host plus the layer fields of every packet, both computed on
+        the device (host arrays in and out; torch for the buffers). layouts=True:
+        the decode with layouts, then extract_fields from them (two launches);
+        False: the fused decode + fields launch (gpk_decode_batch_fields), no
+        layouts returned."""
         import torch
         data = np.ascontiguousarray(data, dtype=np.uint8)
         offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
@@ -141,20 +159,25 @@ class Context:
         rec = torch.empty(n * 16, dtype=torch.uint8, device=dev)
         err = torch.zeros(2 * n, dtype=torch.int32, device=dev)
         fl = torch.zeros(3 * n, dtype=torch.int64, device=dev)
-        lay = torch.empty(n * 64, dtype=torch.uint8, device=dev)
+        lay = torch.empty(n * 64, dtype=torch.uint8, device=dev) if layouts else None
         fields = torch.empty(n * 128, dtype=torch.uint8, device=dev)
         stream = torch.cuda.current_stream(dev)
-        self.decode_device(parser, d_data, d_off, d_cap, rec, err, fl, lay, stream=stream)
-        self.extract_fields(d_data, d_off, d_cap, lay, fields, stream=stream)
+        if layouts:
+            self.decode_device(parser, d_data, d_off, d_cap, rec, err, fl, lay, stream=stream)
+            self.extract_fields(d_data, d_off, d_cap, lay, fields, stream=stream)
+        else:
+            self.decode_device_fields(parser, d_data, d_off, d_cap, rec, err, fl, fields, stream=stream)
         torch.cuda.synchronize(dev)
         return (dict(records=rec.cpu().numpy().view(_lib.RECORD_DTYPE), err_args=err.cpu().numpy().view(np.uint32),
-                     flows=fl.cpu().numpy().view(np.uint64), layouts=lay.cpu().numpy().view(_lib.LAYOUT_DTYPE)),
+                     flows=fl.cpu().numpy().view(np.uint64),
+                     layouts=lay.cpu().numpy().view(_lib.LAYOUT_DTYPE) if layouts else None),
                 fields.cpu().numpy().view(_lib.FIELDS_DTYPE))
 
     def kernel_name(self, parser, data, offsets, caplens, layouts=False):
         """The decode kernel specialisation decode_device (torch tensors) or
         decode_host (numpy arrays) launches for this parser and batch
-        (gpk_decode_kernel_name): the name rocprofv3 lists."""
+        (gpk_decode_kernel_name): the name rocprofv3 lists. layouts=
+        _lib.NAME_FIELDS: the fused decode + fields launch."""
         b = _batch_of(data, offsets, caplens)
         buf = ctypes.create_string_buffer(256)
         n = lib().gpk_decode_kernel_name(self.h, parser.h, ctypes.byref(b), int(layouts), buf, 256)

@@ -310,11 +310,14 @@ class DecodingLayerParser:
 
     def DecodeBatch(self, batch, layouts=False, outputs=_lib.OUT_ALL, fields=False):
         """DecodeLayers for every packet of the batch on the device. fields=True
-        also returns each packet's scalar layer fields computed on the device
-        (gpk_extract_fields; implies layouts): BatchResult.fields, FIELDS_DTYPE."""
+        also returns each packet's scalar layer fields and IPv4/TCP option maps
+        computed on the device (BatchResult.fields, FIELDS_DTYPE;
+        BatchResult.IPv4Options / TCPOptions): in the decode launch itself
+        (gpk_decode_batch_fields) when layouts=False, else from the layouts
+        (gpk_extract_fields), which Hydrate needs."""
         cfg = self._config(outputs)
         if fields:
-            r, f = self.ctx().decode_host_fields(cfg, batch.data, batch.offsets, batch.caplens)
+            r, f = self.ctx().decode_host_fields(cfg, batch.data, batch.offsets, batch.caplens, layouts=layouts)
             res = BatchResult(self, batch, r)
             res.fields = f
             return res
@@ -386,6 +389,37 @@ class BatchResult:
         if not st & _lib.ST_L4_CSUM:
             return None
         return bool(st & _lib.ST_L4_VALID), int(self.records[i]["l4_csum"])
+
+    def IPv4Options(self, i):
+        """(Options, Padding) of packet i's IPv4 layer from the device's option
+        map (fields=True results): no DecodeFromBytes on the host. None when
+        the packet has no IPv4 layer."""
+        from .layers import IPv4OptionsFromMap
+        f = self._fields_of(i)
+        if not int(f["present"]) & (1 << (_lib.DEC_IPV4 - 1)):
+            return None
+        return IPv4OptionsFromMap(self._packet_for(i, int(f["ip4_start"]), "ip4"), int(f["ip4_start"]),
+                                  int(f["ip4_ihl"]) * 4, f["ip4_opt_map"])
+
+    def TCPOptions(self, i):
+        """(Options, Padding, Multipath) of packet i's TCP layer from the
+        device's option map (fields=True results). None without a TCP layer."""
+        from .layers import TCPOptionsFromMap
+        f = self._fields_of(i)
+        if not int(f["present"]) & (1 << (_lib.DEC_TCP - 1)):
+            return None
+        return TCPOptionsFromMap(self._packet_for(i, int(f["tcp_start"]), "tcp"), int(f["tcp_start"]),
+                                 int(f["tcp_data_offset"]) * 4, f["tcp_opt_map"])
+
+    def _fields_of(self, i):
+        if self.fields is None:
+            raise ValueError("option maps need fields=True results")
+        return self.fields[i]
+
+    def _packet_for(self, i, start, what):
+        if start == 0xFF:  # the header starts at byte 255 or later: the map's offsets are not in the record
+            raise ValueError("packet %d: %s header beyond byte 254, use Hydrate" % (i, what))
+        return self.batch.packet(i)
 
     def Hydrate(self, i, decoded):
         """Make the parser's layer structs and `decoded` look exactly as after

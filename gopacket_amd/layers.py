@@ -299,6 +299,36 @@ class IPv6(BaseLayer, _Checksummed):
         return NewFlow(EndpointIPv6, self.SrcIP, self.DstIP)
 
 
+def _map_bits(opt_map):
+    m = int.from_bytes(bytes(bytearray(opt_map)), "little")
+    k = 0
+    while m:
+        if m & 1:
+            yield k
+        m >>= 1
+        k += 1
+
+
+def IPv4OptionsFromMap(pkt, start, hlen, opt_map):
+    """IPv4.Options and IPv4.Padding (ip4.go:219-256) of the header at
+    pkt[start:start+hlen] from its gpk_fields option map (include/gpk.h: bit k
+    = an option at header byte 20 + k), reading only the option bytes."""
+    opts, padding = [], None
+    for k in _map_bits(opt_map):
+        b = start + 20 + k
+        t = pkt[b]
+        if t == 0:
+            opts.append(IPv4Option(0, 1))
+            padding = pkt[b + 1:start + hlen]
+            break
+        if t == 1:
+            opts.append(IPv4Option(1, 1))
+            continue
+        ol = pkt[b + 1]
+        opts.append(IPv4Option(t, ol, pkt[b + 2:b + ol]))
+    return opts, padding
+
+
 # ---- layers/ip6.go:434-461 ---------------------------------------------------
 class IPv6ExtensionSkipper(BaseLayer):
     kind = _lib.DEC_IPV6_EXT
@@ -380,6 +410,27 @@ class TCP(BaseLayer, _Checksummed):
 
     def TransportFlow(self):
         return NewFlow(EndpointTCPPort, self.sPort, self.dPort)
+
+
+def TCPOptionsFromMap(pkt, start, hlen, opt_map):
+    """TCP.Options, TCP.Padding and TCP.Multipath (tcp.go:336-549) of the
+    header at pkt[start:start+hlen] from its gpk_fields option map."""
+    opts, padding, mp = [], b"", False
+    for k in _map_bits(opt_map):
+        b = start + 20 + k
+        t = pkt[b]
+        if t == 0:
+            opts.append(TCPOption(0, 1))
+            padding = pkt[b + 1:start + hlen]
+            break
+        if t == 1:
+            opts.append(TCPOption(1, 1))
+        elif t == TCPOptionKindMultipathTCP:
+            mp = True
+            opts.append(TCPOption(t, pkt[b + 1], None, pkt[b + 2] >> 4))
+        else:
+            opts.append(TCPOption(t, pkt[b + 1], pkt[b + 2:b + pkt[b + 1]]))
+    return opts, padding, mp
 
 
 # ---- layers/udp.go:17-56 -----------------------------------------------------

@@ -30,6 +30,7 @@
  *                                          layers/udp.go:132)
  *   gpk_decode_batch_host                  the same, starting and ending in host memory
  *                                          (pcap/afpacket sources hand over host buffers)
+ *   gpk_decode_batch_fields                gpk_decode_batch plus gpk_extract_fields in one launch
  *   gpk_extract_fields                     the scalar fields the six decoders' DecodeFromBytes set
  *                                          on their structs (layers/ethernet.go:42-55,
  *                                          dot1q.go:28-41, ip4.go:178-271, ip6.go:221-278,
@@ -207,8 +208,8 @@ typedef struct gpk_layout {
  * present: bit k set = layout slot k holds a slice (k = GPK_DEC_* - 1; Payload
  * and Fragment share slot 7); every field of an absent layer is 0. Integers in
  * host byte order; MACs and addresses as their bytes. Variable-length parts
- * (IPv4 / TCP options, HopByHop options, Payload) stay in the packet bytes at
- * the layout's range.                                                         */
+ * (HopByHop options, Payload) stay in the packet bytes at the layout's range;
+ * IPv4 and TCP option lists are described by their option start maps.        */
 typedef struct gpk_fields {
   uint32_t present;          /*   0                                                       */
   uint16_t eth_type;         /*   4 Ethernet.EthernetType (EthernetTypeLLC = 0 below 0x0600) */
@@ -249,8 +250,19 @@ typedef struct gpk_fields {
   uint16_t udp_dst_port;     /* 110 UDP.DstPort                                           */
   uint16_t udp_length;       /* 112 UDP.Length                                            */
   uint16_t udp_checksum;     /* 114 UDP.Checksum                                          */
-  uint8_t reserved[12];      /* 116 zero                                                  */
+  uint8_t ip4_start;         /* 116 packet offset of the IPv4 header (its layout start); 0xFF: absent or >= 255 */
+  uint8_t tcp_start;         /* 117 packet offset of the TCP header; 0xFF: absent or >= 255   */
+  uint8_t ip4_opt_map[5];    /* 118 IPv4.Options: bit k (byte k/8, bit k%8) set = an option starts at
+                                    header byte 20 + k (ip4.go:219-256); see below              */
+  uint8_t tcp_opt_map[5];    /* 123 TCP.Options: the same at TCP header byte 20 + k (tcp.go:336-549) */
 } gpk_fields;
+/* Option lists without decoding again: option j of the list is at the j-th set
+ * bit k of the map, at packet byte b = <layer>_start + 20 + k; OptionType =
+ * pkt[b]; OptionLength = 1 for kinds 0 (End of options) and 1 (No-op), else
+ * pkt[b+1]; OptionData = pkt[b+2 : b+OptionLength] (IPv4 and TCP kinds other
+ * than 0, 1 and 30). A list that ends with kind 0 has Padding = the header's
+ * bytes after it (ip4.go:231, tcp.go:343). Every option lies inside the
+ * header the layer decoded (the decode checked each length). */
 
 /* ---- outputs -------------------------------------------------------------- */
 #define GPK_OUT_IP4_CSUM 0x1u  /* IPv4.VerifyChecksum for the last IPv4 in decoded        */
@@ -340,15 +352,27 @@ int gpk_decode_batch(gpk_ctx* ctx, const gpk_parser* p, const gpk_batch* batch,
  * memory), enqueued on `stream`. Asynchronous. The batch is the one decoded. */
 int gpk_extract_fields(const gpk_batch* batch, const gpk_layout* layouts, gpk_fields* fields, void* stream);
 
+/* Device-resident decode of every packet plus the layer fields of each
+ * (gpk_fields, as gpk_extract_fields writes them) in ONE launch: the decode
+ * kernel reads the fields from the header bytes it parsed, so no layout
+ * round trip through HBM. fields[n]: device memory. out->layouts NULL: the
+ * fused launch; non-NULL: the decode with layouts, then gpk_extract_fields
+ * (two launches, same results). Same stream semantics as gpk_decode_batch. */
+int gpk_decode_batch_fields(gpk_ctx* ctx, const gpk_parser* p, const gpk_batch* batch,
+                            const gpk_results* out, gpk_fields* fields, void* stream);
+
 /* Diagnostic: the name of the kernel specialisation gpk_decode_batch launches
- * for this parser and batch (with or without layouts), e.g.
- * "gpk::decode_kernel<true,false,true,false,5,6>" — the name rocprofv3 lists.
+ * for this parser and batch (with_layouts 0 / 1), or gpk_decode_batch_fields
+ * without layouts (with_layouts = GPK_NAME_FIELDS), e.g.
+ * "gpk::decode_kernel<true,false,true,false,5,7,4>" — the name rocprofv3 lists.
  * Returns the name's length. */
+#define GPK_NAME_FIELDS 2
 int gpk_decode_kernel_name(gpk_ctx* ctx, const gpk_parser* p, const gpk_batch* batch, int with_layouts,
                            char* buf, size_t cap);
 
 /* Diagnostic: how many 256-packet blocks of that specialisation are resident
- * per CU with this parser's LDS table blob (hipOccupancyMaxActiveBlocksPerMultiprocessor). */
+ * per CU with this parser's LDS table blob (hipOccupancyMaxActiveBlocksPerMultiprocessor);
+ * with_layouts as for gpk_decode_kernel_name. */
 int gpk_decode_occupancy(gpk_ctx* ctx, const gpk_parser* p, const gpk_batch* batch, int with_layouts,
                          int* blocks_per_cu);
 

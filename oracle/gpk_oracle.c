@@ -787,10 +787,29 @@ static void decode_packet(const oracle_config* c, const uint8_t* pkt, uint32_t c
 }
 
 /* ---- layer fields (gpk_extract_fields) ------------------------------------ */
+/* Option starts of a header whose DecodeFromBytes succeeded, as its option
+ * loop walks them (ip4.go:219-256 pullOutOptions; tcp.go:336-549 OPTIONS):
+ * kind 0 ends the list, kind 1 is one byte, every other kind advances by its
+ * length byte (which that decode checked against the remaining header).
+ * Bit k of the 40-bit map (byte k/8, bit k%8) = an option at header byte 20+k. */
+static void option_map(const uint8_t* hdr, uint32_t hlen, uint8_t map[5]) {
+  memset(map, 0, 5);
+  const uint32_t n = hlen > 20 ? hlen - 20 : 0;
+  const uint8_t* data = hdr + 20;
+  for (uint32_t k = 0; k < n;) {
+    map[k / 8] |= (uint8_t)(1u << (k % 8));
+    if (data[k] == 0) break;                        /* End of options: Padding follows */
+    const uint32_t len = data[k] == 1 ? 1u : data[k + 1]; /* No-op / OptionLength */
+    if (len == 0) break;                            /* (never on a successful decode) */
+    k += len;
+  }
+}
+
 /* The field assignments of each DecodeFromBytes, applied to the slice the
  * layout records for the decoder (the slice of its last successful call). */
 static void fields_of(const uint8_t* pkt, const gpk_layout* lay, gpk_fields* f) {
   memset(f, 0, sizeof(*f));
+  f->ip4_start = f->tcp_start = 0xFF;
   for (int k = 0; k < 8; k++)
     if (lay->start[k] != GPK_LAYOUT_ABSENT) f->present |= 1u << k;
   if (lay->start[GPK_DEC_ETHERNET - 1] != GPK_LAYOUT_ABSENT) { /* ethernet.go:46-55 */
@@ -826,6 +845,8 @@ static void fields_of(const uint8_t* pkt, const gpk_layout* lay, gpk_fields* f) 
     f->ip4_checksum = be16(d + 10);
     memcpy(f->ip4_src, d + 12, 4);
     memcpy(f->ip4_dst, d + 16, 4);
+    f->ip4_start = (uint8_t)(s < 0xFF ? s : 0xFF);
+    option_map(d, (uint32_t)f->ip4_ihl * 4, f->ip4_opt_map);
   }
   if (lay->start[GPK_DEC_IPV6 - 1] != GPK_LAYOUT_ABSENT) { /* ip6.go:225-234 */
     const uint8_t* d = pkt + lay->start[GPK_DEC_IPV6 - 1];
@@ -851,6 +872,9 @@ static void fields_of(const uint8_t* pkt, const gpk_layout* lay, gpk_fields* f) 
     f->tcp_window = be16(d + 14);
     f->tcp_checksum = be16(d + 16);
     f->tcp_urgent = be16(d + 18);
+    const uint32_t s = lay->start[GPK_DEC_TCP - 1];
+    f->tcp_start = (uint8_t)(s < 0xFF ? s : 0xFF);
+    option_map(d, (uint32_t)f->tcp_data_offset * 4, f->tcp_opt_map);
   }
   if (lay->start[GPK_DEC_UDP - 1] != GPK_LAYOUT_ABSENT) { /* udp.go:34-41 */
     const uint8_t* d = pkt + lay->start[GPK_DEC_UDP - 1];

@@ -28,7 +28,8 @@ def test_fields_record_layout():
     assert _lib.FIELDS_DTYPE.itemsize == 128
     for name, off in (("eth_type", 4), ("eth_dst", 8), ("d1q_tci", 20), ("ip4_length", 28), ("ip6_flow_label", 40),
                       ("ip4_src", 48), ("ip6_src", 56), ("ip6_dst", 72), ("tcp_seq", 92), ("tcp_flags", 100),
-                      ("udp_checksum", 114), ("reserved", 116)):
+                      ("udp_checksum", 114), ("ip4_start", 116), ("tcp_start", 117), ("ip4_opt_map", 118),
+                      ("tcp_opt_map", 123)):
         assert _lib.FIELDS_DTYPE.fields[name][1] == off, name
 
 
@@ -49,7 +50,10 @@ def test_simple_tcp_fields():
     assert int(f["tcp_flags"]) == B["ACK"] | B["PSH"]
     assert (int(f["tcp_window"]), int(f["tcp_checksum"]), int(f["tcp_urgent"])) == (0x73, 0x9a8f, 0)
     # absent layers read 0
-    assert int(f["udp_length"]) == 0 and int(f["ip6_version"]) == 0 and bytes(f["reserved"]) == bytes(12)
+    assert int(f["udp_length"]) == 0 and int(f["ip6_version"]) == 0
+    # option maps: no IPv4 options; TCP NOP, NOP, Timestamps at header bytes 20, 21, 22
+    assert (int(f["ip4_start"]), int(f["tcp_start"])) == (14, 34)
+    assert bytes(f["ip4_opt_map"]) == bytes(5) and bytes(f["tcp_opt_map"]) == bytes([0b111, 0, 0, 0, 0])
 
 
 # layers/udp_test.go:39-98 TestUDPPacketDNS
@@ -134,3 +138,77 @@ def test_fields_match_hydrated_layers():
                 assert (int(x["udp_length"]), int(x["udp_dst_port"])) == (v.Length, int(v.DstPort))
             checked += 1
     assert checked > 600
+
+
+def options_of(f, pkt, r, i, cls):
+    from gopacket_amd import layers
+    if cls == "ip4":
+        return layers.IPv4OptionsFromMap(pkt, int(f["ip4_start"]), int(f["ip4_ihl"]) * 4, f["ip4_opt_map"])
+    return layers.TCPOptionsFromMap(pkt, int(f["tcp_start"]), int(f["tcp_data_offset"]) * 4, f["tcp_opt_map"])
+
+
+# layers/ip4_test.go:126-223 TestIPv4Options: the option lists and Padding the
+# reference expects, from the option maps alone
+def test_ipv4_option_maps():
+    want = {0: ([(130, 11, bytes(9)), (0, 1, None)], None),
+            1: ([(1, 1, None), (130, 11, bytes(9)), (0, 1, None)], bytes([1, 2, 3])),
+            2: ([(130, 12, bytes(10))], None),
+            3: ([(0, 1, None)], bytes([0x82, 0x0b] + [0] * 10 + [1, 2, 3])),
+            4: ([(7, 7, bytes([4, 0, 0, 0, 0])), (1, 1, None), (0, 1, None)], bytes(3))}
+    for k, (opts, padding) in want.items():
+        pkt = pktutil.golden_bytes("ip4_options_%d" % k)
+        f, r = fields_of(20, [IP4], [pkt])
+        assert int(f[0]["ip4_start"]) == 0
+        got, pad = options_of(f[0], pkt, r, 0, "ip4")
+        assert [(o.OptionType, o.OptionLength, o.OptionData) for o in got] == opts, k
+        assert (pad or b"") == (padding or b""), k
+
+
+# layers/tcp_test.go:87-109 (MSS 8192, EndList) and :123-157 (MSS, MP_CAPABLE v1, EndList)
+def test_tcp_option_maps():
+    pkt = pktutil.golden_bytes("tcp_option_mss_eol")
+    f, r = fields_of(17, [ETH, IP4, TCP, PAY], [pkt])
+    got, pad, mp = options_of(f[0], pkt, r, 0, "tcp")
+    assert [(o.OptionType, o.OptionLength, o.OptionData) for o in got] == [(2, 4, bytes([32, 0])), (0, 1, None)]
+    assert not mp
+    pkt = pktutil.golden_bytes("mptcp_capable")
+    f, r = fields_of(17, [ETH, IP4, TCP, PAY], [pkt])
+    got, pad, mp = options_of(f[0], pkt, r, 0, "tcp")
+    assert [(o.OptionType, o.OptionLength) for o in got] == [(2, 4), (30, 4), (0, 1)]
+    assert got[1].OptionMultipath == 0 and mp
+
+
+def test_option_maps_match_hydrated_layers():
+    """Fuzzed packets (IPv4 options, TCP options incl. MPTCP and bad lengths):
+    the lists rebuilt from the option maps equal the lists the layer structs
+    decode from the same slices, Padding and Multipath included."""
+    from gopacket_amd import layers
+    from gopacket_amd import synth
+    pkts = list(pktutil.fuzz_packets(11, 3000)) + [pktutil.golden_bytes("simple_tcp")]
+    pkts += [synth.packet(4, i) for i in range(50)]
+    # Linux SYN options, SACK blocks, EOL with padding, an MPTCP option
+    for opts in (bytes([2, 4, 5, 0xb4, 4, 2, 8, 10]) + bytes(8) + bytes([1, 3, 3, 7]),
+                 bytes([1, 1, 5, 18]) + bytes(16) + bytes([1, 1, 8, 10]) + bytes(8),
+                 bytes([2, 4, 1, 0, 0, 9, 9, 9]), bytes([30, 4, 0x10, 0, 1, 0, 0, 0])):
+        ip = struct.pack(">BBHHHBBH4s4s", 0x45, 0, 40 + len(opts), 0, 0, 64, 6, 0, bytes(4), bytes(4))
+        tcp = struct.pack(">HHIIBBHHH", 1, 2, 3, 4, (5 + len(opts) // 4) << 4, 0x12, 100, 0, 0) + opts
+        pkts.append(bytes(12) + b"\x08\x00" + ip + tcp)
+    f, r = fields_of(17, [ETH, D1Q, IP4, IP6, EXT, TCP, UDP, PAY], pkts)
+    n4 = nt = 0
+    for i, pkt in enumerate(pkts):
+        lay = r["layouts"][i]
+        s = int(lay["start"][2])
+        if s != _lib.LAYOUT_ABSENT and s < 0xFF:
+            v = layers.IPv4()
+            v._hydrate(pkt[s:int(lay["end"][2])])
+            got, pad = options_of(f[i], pkt, r, i, "ip4")
+            assert got == v.Options and (pad or b"") == (v.Padding or b""), i
+            n4 += len(got) > 0
+        s = int(lay["start"][5])
+        if s != _lib.LAYOUT_ABSENT and s < 0xFF:
+            v = layers.TCP()
+            v._hydrate(pkt[s:int(lay["end"][5])])
+            got, pad, mp = options_of(f[i], pkt, r, i, "tcp")
+            assert got == v.Options and pad == v.Padding and mp == v.Multipath, i
+            nt += len(got) > 0
+    assert n4 > 20 and nt > 25

@@ -12,28 +12,36 @@ import pytest
 import torch
 
 import pktutil
-from configs import CONFIGS, device_parser, oracle_parser
+from configs import CONFIGS, assert_same, device_parser, oracle_parser
 from gopacket_amd import _lib
 from oracle import oracle as O
 
 pytestmark = pytest.mark.gpu
+FUSED_WAVES = 6  # gpk_kernels.hip GPK_SBF_WAVES
 
 
-def device_fields(ctx, cfg, data, off, cap):
-    r, f = ctx.decode_host_fields(device_parser(cfg), data, off, cap)
+def device_fields(ctx, cfg, data, off, cap, layouts=True):
+    r, f = ctx.decode_host_fields(device_parser(cfg), data, off, cap, layouts=layouts)
     return r, f.view(np.uint8).reshape(-1, 128)
 
 
 def check(ctx, cfg_name, packets, align=1):
+    """Both paths against the oracle: the decode with layouts + gpk_extract_fields,
+    and the fused decode + fields launch (gpk_decode_batch_fields, no layouts),
+    whose records, error arguments and flows must also equal the oracle's."""
     cfg = CONFIGS[cfg_name]
     data, off, cap = pktutil.pack(packets, align=align)
-    r, f = device_fields(ctx, cfg, data, off, cap)
     ref = oracle_parser(cfg).decode(data, off, cap, nthreads=8, layouts=True)
-    assert np.array_equal(r["layouts"].view(np.uint8), ref["layouts"].view(np.uint8)), cfg_name
     want = O.extract_fields(data, off, ref["layouts"])
-    bad = np.nonzero((f != want).any(axis=1))[0]
-    assert len(bad) == 0, "%s: %d packets differ, first %d: %s vs %s" % (
-        cfg_name, len(bad), bad[0], f[bad[0]].tobytes().hex(), want[bad[0]].tobytes().hex())
+    for layouts in (True, False):
+        r, f = device_fields(ctx, cfg, data, off, cap, layouts=layouts)
+        what = "%s (%s)" % (cfg_name, "layouts + extract" if layouts else "fused")
+        if layouts:
+            assert np.array_equal(r["layouts"].view(np.uint8), ref["layouts"].view(np.uint8)), what
+        assert_same(r, ref, what)
+        bad = np.nonzero((f != want).any(axis=1))[0]
+        assert len(bad) == 0, "%s: %d packets differ, first %d: %s vs %s" % (
+            what, len(bad), bad[0], f[bad[0]].tobytes().hex(), want[bad[0]].tobytes().hex())
     return f.view(_lib.FIELDS_DTYPE).reshape(-1)
 
 
@@ -67,6 +75,40 @@ def test_fields_golden(gpu_ctx):
         check(gpu_ctx, cfg_name, packets)
 
 
+@pytest.mark.parametrize("layout", ["sparse_mix", "gapped", "wave_shuffled", "reversed"])
+def test_fields_fused_layouts(gpu_ctx, layout):
+    """The fused kernel on unordered and sparse batches (its phase B after the
+    parse, whose head/tail chunks then come from memory), the kernel named."""
+    from test_gpu_parity import golden_packets, phase_b_layout
+    packets = pktutil.fuzz_packets(77, 8000) + golden_packets()
+    data, off, cap = phase_b_layout(packets, layout)
+    for cfg_name in ("statsassembly", "eth_ip4_tcp_payload", "eth_ip4_udp_payload"):
+        cfg = CONFIGS[cfg_name]
+        dp = device_parser(cfg)
+        assert gpu_ctx.kernel_name(dp, data, off, cap, layouts=_lib.NAME_FIELDS) == \
+            "gpk::decode_sb_kernel<true,%d,6,true>" % FUSED_WAVES
+        ref = oracle_parser(cfg).decode(data, off, cap, nthreads=8, layouts=True)
+        r, f = device_fields(gpu_ctx, cfg, data, off, cap, layouts=False)
+        assert_same(r, ref, layout + "/" + cfg_name)
+        want = O.extract_fields(data, off, ref["layouts"])
+        assert np.array_equal(f, want), layout + "/" + cfg_name
+
+
+def test_fields_fused_output_subsets(gpu_ctx):
+    """Every GPK_OUT_* subset through the fused launch (without the L4 checksum
+    the kernel skips the stream before the parse)."""
+    from gopacket_amd import synth
+    data, off, cap = synth.host_batch(4, 4321, 30000)
+    for outputs in range(8):
+        cfg = dict(CONFIGS["statsassembly"], outputs=outputs)
+        ref = oracle_parser(cfg).decode(data, off, cap, nthreads=8, layouts=True)
+        r, f = device_fields(gpu_ctx, cfg, data, off, cap, layouts=False)
+        if not outputs & 4:
+            r["flows"][:] = 0
+        assert_same(r, ref, "outputs=%d" % outputs)
+        assert np.array_equal(f, O.extract_fields(data, off, ref["layouts"])), outputs
+
+
 def test_fields_empty_batch(gpu_ctx):
     t = torch.zeros(16, dtype=torch.uint8, device="cuda")
     e = torch.zeros(0, dtype=torch.int64, device="cuda")
@@ -82,7 +124,7 @@ def test_decode_batch_fields_api(gpu_ctx):
                                ctx=gpu_ctx)
     from gopacket_amd import synth
     data, off, cap = synth.host_batch(4, 5, 2000)
-    res = p.DecodeBatch(gp.PacketBatch(data, off, cap), fields=True)
+    res = p.DecodeBatch(gp.PacketBatch(data, off, cap), fields=True, layouts=True)
     assert res.fields is not None and len(res.fields) == len(off)
     decoded = []
     n = 0
@@ -138,3 +180,36 @@ def test_fields_header_ends_at_buffer_end(gpu_ctx):
     assert np.array_equal(got, want)
     f = got[-1:].view(_lib.FIELDS_DTYPE)[0]
     assert (int(f["tcp_checksum"]), int(f["tcp_urgent"]), int(f["tcp_window"])) == (0x1234, 0xBEEF, 512)
+
+
+def test_decode_batch_fused_options(gpu_ctx):
+    """DecodeBatch(fields=True) without layouts (one launch): the IPv4 and TCP
+    option lists rebuilt from the device's option maps equal the ones Hydrate
+    decodes on the host from a layouts run of the same packets."""
+    from gopacket_amd import gopacket as gp, layers
+    p = gp.DecodingLayerParser(layers.LayerTypeEthernet, layers.Ethernet(), layers.Dot1Q(), layers.IPv4(),
+                               layers.IPv6(), layers.TCP(), layers.UDP(), gp.Payload(), ctx=gpu_ctx)
+    pkts = pktutil.fuzz_packets(99, 6000)
+    data, off, cap = pktutil.pack(pkts)
+    batch = gp.PacketBatch(data, off, cap)
+    fused = p.DecodeBatch(batch, fields=True)
+    assert fused.layouts is None
+    full = p.DecodeBatch(batch, layouts=True)
+    n4 = nt = 0
+    for i in range(len(off)):
+        pkt = batch.packet(i)
+        lay = full.layouts[i]
+        s4, st = int(lay["start"][2]), int(lay["start"][5])
+        if s4 != _lib.LAYOUT_ABSENT and int(fused.fields[i]["ip4_start"]) != 0xFF:
+            v = layers.IPv4()  # fresh: the reference leaves Padding stale across packets
+            v._hydrate(pkt[s4:int(lay["end"][2])])
+            opts, pad = fused.IPv4Options(i)
+            assert opts == v.Options and (pad or b"") == (v.Padding or b""), i
+            n4 += len(opts) > 0
+        if st != _lib.LAYOUT_ABSENT and int(fused.fields[i]["tcp_start"]) != 0xFF:
+            v = layers.TCP()  # fresh: Multipath is stale across packets in the reference
+            v._hydrate(pkt[st:int(lay["end"][5])])
+            opts, pad, mp = fused.TCPOptions(i)
+            assert opts == v.Options and pad == v.Padding and mp == v.Multipath, i
+            nt += len(opts) > 0
+    assert n4 > 20 and nt > 20

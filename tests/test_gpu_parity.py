@@ -296,8 +296,8 @@ def phase_b_layout(packets, layout):
 # kernel for parsers without; batches with a mean packet of 1 KiB or more take
 # the 80-VGPR 6-chunk kernel
 PHASE_B_KERNELS = {
-    "statsassembly": "gpk::decode_sb_kernel<true,7,6>",
-    "raw_ip6": "gpk::decode_sb_kernel<true,7,6>",
+    "statsassembly": "gpk::decode_sb_kernel<true,7,6,false>",
+    "raw_ip6": "gpk::decode_sb_kernel<true,7,6,false>",
     "eth_ip4_tcp_payload": "gpk::decode_kernel<true,false,true,false,5,7,4>",
 }
 

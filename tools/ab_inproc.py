@@ -8,6 +8,8 @@ in interleaved rounds so clocks and thermals affect them alike.
 
 "base" = gopacket_amd/libgpk.so, NAME = gopacket_amd/build/libgpk_NAME.so;
 NAME@global runs that library with gpk_ctx_set_table_mode(GPK_TABLES_GLOBAL).
+--fields times gpk_decode_batch_fields (the fused decode + layer fields launch)
+instead of gpk_decode_batch.
 Prints, per config and variant, the median and min kernel ms over rounds.
 """
 import argparse
@@ -29,6 +31,8 @@ def load(name):
     L.gpk_parser_add_decoder.argtypes = [vp, ctypes.c_int]
     L.gpk_parser_set_outputs.argtypes = [vp, ctypes.c_uint32]
     L.gpk_decode_batch.argtypes = [vp, vp, vp, vp, vp]
+    if hasattr(L, "gpk_decode_batch_fields"):
+        L.gpk_decode_batch_fields.argtypes = [vp, vp, vp, vp, vp, vp]
     return L
 
 
@@ -38,6 +42,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--packets", type=int, default=64 * 2**20)
+    ap.add_argument("--fields", action="store_true")
     ap.add_argument("variants", nargs="+")
     a = ap.parse_args()
     import numpy as np
@@ -57,6 +62,7 @@ def main():
         err = torch.zeros(2 * n, dtype=torch.int32, device="cuda")
         fl = torch.empty(3 * n, dtype=torch.int64, device="cuda")
         algo = int(cap.sum(dtype=torch.int64).item()) + 12 * n
+        fields = torch.empty(n * 128 if a.fields else 16, dtype=torch.uint8, device="cuda")
         b = _lib.Batch(data.data_ptr(), off.data_ptr(), cap.data_ptr(), n, data.numel())
         r = _lib.Results(rec.data_ptr(), err.data_ptr(), fl.data_ptr(), None)
         handles = {}
@@ -79,7 +85,8 @@ def main():
                 continue
             o = ctypes.c_int()
             f.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
-            occ[v] = o.value if f(handles[v][0], handles[v][1], ctypes.byref(b), 0, ctypes.byref(o)) == 0 else "?"
+            occ[v] = o.value if f(handles[v][0], handles[v][1], ctypes.byref(b), _lib.NAME_FIELDS if a.fields else 0,
+                                  ctypes.byref(o)) == 0 else "?"
         times = {v: [] for v in libs}
         for rnd in range(a.rounds + 1):
             for v, L in libs.items():
@@ -87,7 +94,13 @@ def main():
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record(stream)
                 for _ in range(a.steps):
-                    rc = L.gpk_decode_batch(ctx, p, ctypes.byref(b), ctypes.byref(r), ctypes.c_void_p(stream.cuda_stream))
+                    if a.fields:
+                        rc = L.gpk_decode_batch_fields(ctx, p, ctypes.byref(b), ctypes.byref(r),
+                                                       ctypes.c_void_p(fields.data_ptr()),
+                                                       ctypes.c_void_p(stream.cuda_stream))
+                    else:
+                        rc = L.gpk_decode_batch(ctx, p, ctypes.byref(b), ctypes.byref(r),
+                                                ctypes.c_void_p(stream.cuda_stream))
                     assert rc == 0
                 e1.record(stream)
                 torch.cuda.synchronize()
@@ -98,7 +111,7 @@ def main():
             print("%-4s %-10s median %8.3f ms  min %8.3f ms  %7.1f GB/s (%.1f%% of 8 TB/s)  blocks/CU %s" % (
                 name, v, np.median(t), t.min(), algo / (np.median(t) * 1e-3) / 1e9,
                 algo / (np.median(t) * 1e-3) / 8e12 * 100, occ[v]), flush=True)
-        del data, off, cap, rec, err, fl
+        del data, off, cap, rec, err, fl, fields
         torch.cuda.empty_cache()
 
 

