@@ -167,7 +167,7 @@ class ReplayStats(ctypes.Structure):
                 ("wall_s", ctypes.c_double), ("read_s", ctypes.c_double), ("index_s", ctypes.c_double),
                 ("gpu_s", ctypes.c_double), ("kernel_s", ctypes.c_double), ("deliver_s", ctypes.c_double),
                 ("reader_status", ctypes.c_int), ("error", ctypes.c_char * 160), ("kernel", ctypes.c_char * 96),
-                ("device_walk_packets", ctypes.c_uint64)]
+                ("device_walk_packets", ctypes.c_uint64), ("alloc_wait_s", ctypes.c_double)]
 
 
 REPLAY_CB = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p,

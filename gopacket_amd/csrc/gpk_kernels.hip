@@ -111,6 +111,15 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 #ifndef GPK_DIAG_TIMES
 #define GPK_DIAG_TIMES 0  // diagnostic builds: per-wave phase timestamps into KParams.diag (tools/wave_times.py)
 #endif
+#ifndef GPK_FIELDS_STAGE
+#define GPK_FIELDS_STAGE 1  // fused fields: 1 = half records through LDS (64-byte runs), 2 = whole records (1 KiB runs)
+#endif
+#ifndef GPK_FIELDS_TEMPORAL
+#define GPK_FIELDS_TEMPORAL 0  // fused fields: record stores with the default policy instead of non-temporal
+#endif
+#ifndef GPK_DIAG_FIELDS
+#define GPK_DIAG_FIELDS 0  // timing only: 1 = fused fields computed, not stored; 2 = stored, not read
+#endif
 #ifndef GPK_PB_NULL
 #define GPK_PB_NULL 0  // timing only: phase-B stream loads read nothing (zero-record descriptors)
 #endif
@@ -911,6 +920,37 @@ struct RdF {
 __device__ __forceinline__ void fields_store(const KParams& P, const uint32_t (&w)[32], uint32_t wave_dw, uint32_t lane,
                                              uint64_t first) {
   u32x4* out = reinterpret_cast<u32x4*>(P.fields + first);
+#if GPK_FIELDS_STAGE == 2
+  // whole records: lanes [48g, 48g + 48) put theirs into the 6 KiB (chunk c at
+  // c ^ (l & 7)), then 1 KiB stores of 8 whole records each
+#pragma unroll
+  for (uint32_t g = 0; g < 2; g++) {
+    const uint32_t l0 = 48 * g, nrec = g ? 16u : 48u;
+    asm volatile("" ::: "memory");
+    if (lane >= l0 && lane < l0 + nrec) {
+      const uint32_t q = lane - l0;
+#pragma unroll
+      for (uint32_t c = 0; c < 8; c++)
+        *reinterpret_cast<u32x4*>(gpk_smem + wave_dw + q * 32 + 4 * (c ^ (q & 7))) =
+            u32x4{w[4 * c], w[4 * c + 1], w[4 * c + 2], w[4 * c + 3]};
+    }
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (uint32_t k = 0; k < 6; k++) {
+      if (g && k >= 2) break;
+      const uint32_t q = 8 * k + (lane >> 3), c = lane & 7, rr = l0 + q;
+      const u32x4 v = *reinterpret_cast<const u32x4*>(gpk_smem + wave_dw + q * 32 + 4 * (c ^ (q & 7)));
+      if (first + rr < P.n) {
+        if (GPK_FIELDS_TEMPORAL)
+          out[8 * rr + c] = v;
+        else
+          __builtin_nontemporal_store(v, out + 8 * rr + c);
+      }
+    }
+  }
+  asm volatile("" ::: "memory");
+  return;
+#endif
 #pragma unroll
   for (int h = 0; h < 2; h++) {
     asm volatile("" ::: "memory");
@@ -923,7 +963,12 @@ __device__ __forceinline__ void fields_store(const KParams& P, const uint32_t (&
     for (uint32_t k = 0; k < 4; k++) {
       const uint32_t rr = 16 * k + (lane >> 2), c = lane & 3;
       const u32x4 v = *reinterpret_cast<const u32x4*>(gpk_smem + wave_dw + rr * 16 + 4 * (c ^ (rr & 3)));
-      if (first + rr < P.n) __builtin_nontemporal_store(v, out + 8 * rr + 4 * h + c);
+      if (first + rr < P.n) {
+        if (GPK_FIELDS_TEMPORAL)
+          out[8 * rr + 4 * h + c] = v;
+        else
+          __builtin_nontemporal_store(v, out + 8 * rr + 4 * h + c);
+      }
     }
   }
   asm volatile("" ::: "memory");
@@ -1098,8 +1143,20 @@ __device__ __forceinline__ void decode_packet(const KParams& P, const TT& T, uin
   // never hold registers at the same time.
   auto emit_fields = [&]() __attribute__((always_inline)) {
     uint32_t fw[32];
+#if GPK_DIAG_FIELDS == 2  // timing only: the stores without the field reads
+#pragma unroll
+    for (int k = 0; k < 32; k++) fw[k] = fst[k & 7] + fpres * k;
+#else
     gpkf::fields_words(RdF{r}, fpres, fst, fip4e, fw);
+#endif
+#if GPK_DIAG_FIELDS == 1  // timing only: the field reads without the record stores
+    uint32_t x = 0;
+#pragma unroll
+    for (int k = 0; k < 32; k++) x ^= fw[k];
+    if (x == 0x9E3779B9u) P.fields[i].present = x;
+#else
     fields_store(P, fw, slot_dw - lane * kSlotStride, lane, i - lane);
+#endif
   };
 
   // ---- Phase B: segment sums ---------------------------------------------

@@ -35,6 +35,7 @@
 #include <zlib.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cctype>
 #include <cstdlib>
 #include <chrono>
@@ -160,6 +161,7 @@ struct Fill {      // one read of a slot's fresh bytes
   bool end;        // the stream ended with this read
   double t0, t1;   // read start / end (GPK_REPLAY_TRACE=2)
   hipEvent_t sent; // recorded after the read's HtoD (device walk), or null
+  std::string err; // the slot's allocation failed (the read did not run)
 };
 
 struct Slot {
@@ -206,6 +208,12 @@ struct Pipeline {
   void* user = nullptr;
   gpk_replay_stats* st = nullptr;
   std::string herr;
+  // first call: the slots' and batches' buffers are allocated in the
+  // background (slot 0 and the first two batches first, the rest behind
+  // them while slot 0 is read); the read of a slot and the first use of a
+  // batch wait for their own allocation (empty string = done)
+  std::vector<std::shared_future<std::string>> slot_ready, bat_ready;
+  std::atomic<uint64_t> alloc_wait_ns{0};  // time the pipeline waited for them
 
   bool ok(hipError_t e, const char* what) {
     if (e != hipSuccess && herr.empty()) herr = std::string(what) + ": " + hipGetErrorString(e);
@@ -234,10 +242,34 @@ struct Pipeline {
       if (!deliver_oldest()) return -1;
     int b = free_bats.front();
     free_bats.pop_front();
+    if ((size_t)b < bat_ready.size() && bat_ready[b].valid()) {
+      const double t = now_s();
+      const std::string e = bat_ready[b].get();
+      alloc_wait_ns += (uint64_t)((now_s() - t) * 1e9);
+      bat_ready[b] = std::shared_future<std::string>();
+      if (!e.empty()) {
+        if (herr.empty()) herr = e;
+        return -1;
+      }
+    }
     return b;
   }
 
+  // every background allocation has finished (their buffers can be freed or kept)
+  std::string settle() {
+    std::string first;
+    for (auto* v : {&slot_ready, &bat_ready})
+      for (auto& f : *v)
+        if (f.valid()) {
+          const std::string e = f.get();
+          if (first.empty()) first = e;
+          f = std::shared_future<std::string>();
+        }
+    return first;
+  }
+
   ~Pipeline() {
+    (void)settle();
     for (auto& s : slots) {
       if (s.fill_pending) s.fill.wait();
       if (s.stream) (void)hipStreamSynchronize(s.stream);
@@ -463,25 +495,39 @@ extern "C" int gpk_replay_file(gpk_ctx* ctx, const gpk_parser* parser, const cha
     if (cached) free_cached(cached);
     pl.slots.resize(opt.slots);
     pl.bats.resize(2 * opt.slots);
-    // every slot and batch allocated on its own thread (pinning GBs is the slow part)
+    // Every slot and batch is allocated on its own thread (pinning GBs is the
+    // slow part), in the background: slot 0 and the first two batches first,
+    // the rest once slot 0 is done, while it is being read. The call goes on
+    // as soon as the buffers it needs next exist (the cold call used to wait
+    // for all of them: 0.45 s against 0.21 s with the buffers kept).
     int dev = 0;
     (void)hipGetDevice(&dev);
-    std::vector<std::future<std::string>> jobs;
-    for (auto& s : pl.slots)
-      jobs.push_back(std::async(std::launch::async, [&, dev, sp = &s] {
-        (void)hipSetDevice(dev);
-        return alloc_slot(*sp, C, R, dev_walk, max_pk);
-      }));
-    for (auto& b : pl.bats)
-      jobs.push_back(std::async(std::launch::async, [&, dev, bp = &b] {
-        (void)hipSetDevice(dev);
-        return alloc_bat(*bp, P);
-      }));
-    for (auto& jb : jobs) {
-      const std::string e = jb.get();
+    const bool lazy = !(getenv("GPK_REPLAY_EAGER_ALLOC") && getenv("GPK_REPLAY_EAGER_ALLOC")[0] == '1');
+    auto slot_job = [&pl, C, R, dev_walk, max_pk, dev](size_t k, std::shared_future<std::string> after) {
+      return std::async(std::launch::async, [&pl, C, R, dev_walk, max_pk, dev, k, after] {
+               if (after.valid()) after.wait();
+               (void)hipSetDevice(dev);
+               return alloc_slot(pl.slots[k], C, R, dev_walk, max_pk);
+             }).share();
+    };
+    auto bat_job = [&pl, P, dev](size_t b, std::shared_future<std::string> after) {
+      return std::async(std::launch::async, [&pl, P, dev, b, after] {
+               if (after.valid()) after.wait();
+               (void)hipSetDevice(dev);
+               return alloc_bat(pl.bats[b], P);
+             }).share();
+    };
+    pl.slot_ready.resize(pl.slots.size());
+    pl.bat_ready.resize(pl.bats.size());
+    pl.slot_ready[0] = slot_job(0, {});
+    const std::shared_future<std::string> gate = lazy ? pl.slot_ready[0] : std::shared_future<std::string>();
+    for (size_t b = 0; b < pl.bats.size(); b++) pl.bat_ready[b] = bat_job(b, b < 2 ? std::shared_future<std::string>() : gate);
+    for (size_t k = 1; k < pl.slots.size(); k++) pl.slot_ready[k] = slot_job(k, gate);
+    if (!lazy) {
+      const std::string e = pl.settle();
       if (!e.empty()) {
         good = false;
-        if (pl.herr.empty()) pl.herr = e;
+        pl.herr = e;
       }
     }
   }
@@ -511,8 +557,23 @@ extern "C" int gpk_replay_file(gpk_ctx* ctx, const gpk_parser* parser, const cha
     std::shared_future<Fill> prev = last_fill;
     // (mutable: the previous fill's future is dropped as soon as it has been
     // read, so the async states do not chain every fill of the call together)
-    s.fill = std::async(std::launch::async, [&src, &s, C, R, stats, dev, dev_walk, prev]() mutable {
+    std::shared_future<std::string> ready;  // the slot's allocation (first call)
+    const size_t si = (size_t)(&s - pl.slots.data());
+    if (si < pl.slot_ready.size()) {
+      ready = pl.slot_ready[si];
+      pl.slot_ready[si] = std::shared_future<std::string>();
+    }
+    s.fill = std::async(std::launch::async, [&src, &s, &pl, C, R, stats, dev, dev_walk, prev, ready]() mutable {
       if (src.pin) (void)pthread_setaffinity_np(pthread_self(), sizeof(src.cpus), &src.cpus);
+      if (ready.valid()) {
+        const double ta = now_s();
+        std::string e = ready.get();
+        pl.alloc_wait_ns += (uint64_t)((now_s() - ta) * 1e9);
+        if (!e.empty()) {
+          if (prev.valid()) (void)prev.get();  // keep the chain's order
+          return Fill{0, true, ta, ta, nullptr, e};
+        }
+      }
       hipEvent_t before = nullptr;
       if (prev.valid()) before = prev.get().sent;
       prev = std::shared_future<Fill>();
@@ -533,7 +594,7 @@ extern "C" int gpk_replay_file(gpk_ctx* ctx, const gpk_parser* parser, const cha
         if (s.h2d_err == hipSuccess) s.h2d_err = hipEventRecord(s.sent, s.stream);
         if (s.h2d_err == hipSuccess) sent = s.sent;
       }
-      return Fill{k, end, t, t1, sent};
+      return Fill{k, end, t, t1, sent, std::string()};
     }).share();
     s.fill_pending = true;
     last_fill = s.fill;
@@ -565,6 +626,12 @@ extern "C" int gpk_replay_file(gpk_ctx* ctx, const gpk_parser* parser, const cha
     const Fill fl = S.fill.get();
     const double t_got = now_s();
     S.fill_pending = false;
+    if (!fl.err.empty()) {
+      good = false;
+      if (pl.herr.empty()) pl.herr = fl.err;
+      rc = GPK_ENOMEM;
+      break;
+    }
     const uint64_t fresh = fl.bytes;
     const bool eof = fl.end;
     if (carry_len > C) {  // a record longer than the carry region: not supported
@@ -832,6 +899,15 @@ extern "C" int gpk_replay_file(gpk_ctx* ctx, const gpk_parser* parser, const cha
       s.fill_pending = false;
     }
   stats->packets = packet_index;
+  {
+    const std::string e = pl.settle();  // allocations the call did not reach
+    if (!e.empty() && good) {
+      good = false;
+      pl.herr = e;
+      rc = GPK_ENOMEM;
+    }
+  }
+  stats->alloc_wait_s = pl.alloc_wait_ns.load() * 1e-9;
   stats->wall_s = now_s() - t_start;
   if (trace && trace[0] == '1')
     fprintf(stderr, "gpk_replay: setup %.4f s, loop %.4f s, %llu slots\n", t_loop - t_start, now_s() - t_loop,

@@ -164,6 +164,8 @@ typedef struct gpk_replay_stats {
   char error[160];
   char kernel[96];       /* the decode kernel specialisation of the last launch */
   uint64_t device_walk_packets; /* packets the device record walk indexed (the rest: the host reader) */
+  double alloc_wait_s;   /* first call with these sizes: time the reads and launches waited for their
+                            staging buffers, which are allocated in the background (0 when kept) */
 } gpk_replay_stats;
 
 /* Results of one device launch, in packet order, delivered on the calling
