@@ -103,7 +103,8 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 #define GPK_SB_WAVES GPK_SMALL_WAVES  // ... its register budget (waves per SIMD; LDS allows 6 blocks per CU)
 #endif
 #ifndef GPK_SBF_WAVES
-#define GPK_SBF_WAVES 6  // ... its fused-fields variant (gpk_decode_batch_fields; 72 VGPRs: 68 B of scratch)
+#define GPK_SBF_WAVES 5  // ... its fused-fields variant (gpk_decode_batch_fields): 96 VGPRs, no scratch (A/B r15,
+                         // C4 + fields: 80 VGPRs 44 B of scratch +7.5 %, 72 VGPRs 64 B +10 %)
 #endif
 #ifndef GPK_SB_DEPTH
 #define GPK_SB_DEPTH 6  // ... its stream depth (passes in flight; 8 no better)
@@ -112,10 +113,12 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 #define GPK_DIAG_TIMES 0  // diagnostic builds: per-wave phase timestamps into KParams.diag (tools/wave_times.py)
 #endif
 #ifndef GPK_FIELDS_STAGE
-#define GPK_FIELDS_STAGE 1  // fused fields: 1 = half records through LDS (64-byte runs), 2 = whole records (1 KiB runs)
+#define GPK_FIELDS_STAGE 2  // fused fields: 1 = half records through LDS (64-byte runs), 2 = whole records (1 KiB runs;
+                            // A/B r15 C4 + fields: 6.62 against 7.74 ms)
 #endif
 #ifndef GPK_FIELDS_TEMPORAL
-#define GPK_FIELDS_TEMPORAL 0  // fused fields: record stores with the default policy instead of non-temporal
+#define GPK_FIELDS_TEMPORAL 0  // fused fields: record stores with the default policy instead of non-temporal (A/B r15:
+                               // +3 % with whole records, -9 % with half records)
 #endif
 #ifndef GPK_DIAG_FIELDS
 #define GPK_DIAG_FIELDS 0  // timing only: 1 = fused fields computed, not stored; 2 = stored, not read

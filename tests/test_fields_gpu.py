@@ -17,7 +17,7 @@ from gopacket_amd import _lib
 from oracle import oracle as O
 
 pytestmark = pytest.mark.gpu
-FUSED_WAVES = 6  # gpk_kernels.hip GPK_SBF_WAVES
+FUSED_WAVES = 5  # gpk_kernels.hip GPK_SBF_WAVES
 
 
 def device_fields(ctx, cfg, data, off, cap, layouts=True):
