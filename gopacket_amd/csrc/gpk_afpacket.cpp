@@ -43,6 +43,7 @@
 #include <thread>
 #include <vector>
 
+#include "gpk_pinned.h"
 #include "../../include/gpk_afpacket.h"
 
 extern "C" int gpk_decode_batch_ex(gpk_ctx* c, const gpk_parser* p, const gpk_batch* b, const gpk_results* o,
@@ -1039,13 +1040,13 @@ extern "C" int gpk_tpacket_pump(gpk_ctx* ctx, const gpk_parser* parser, gpk_tpac
   const uint64_t ring_bytes = t->bytes;
   bool good = ok(hipMalloc((void**)&dev, ring_bytes + NB * side_cap + 64), "hipMalloc ring mirror");
   for (auto& b : B) {
-    good = good && ok(hipHostMalloc((void**)&b.h_off, P * 8, 0), "hipHostMalloc") &&
-           ok(hipHostMalloc((void**)&b.h_cap, P * 4, 0), "hipHostMalloc") &&
-           ok(hipHostMalloc((void**)&b.h_ci, P * sizeof(gpk_tp_info), 0), "hipHostMalloc") &&
-           ok(hipHostMalloc((void**)&b.h_rec, P * sizeof(gpk_record), 0), "hipHostMalloc") &&
-           ok(hipHostMalloc((void**)&b.h_err, P * 8, 0), "hipHostMalloc") &&
-           ok(hipHostMalloc((void**)&b.h_flow, P * 24, 0), "hipHostMalloc") &&
-           ok(hipHostMalloc((void**)&b.h_side, side_cap, 0), "hipHostMalloc") &&
+    good = good && ok(gpk_pin_alloc((void**)&b.h_off, P * 8), "pinned batch") &&
+           ok(gpk_pin_alloc((void**)&b.h_cap, P * 4), "pinned batch") &&
+           ok(gpk_pin_alloc((void**)&b.h_ci, P * sizeof(gpk_tp_info)), "pinned batch") &&
+           ok(gpk_pin_alloc((void**)&b.h_rec, P * sizeof(gpk_record)), "pinned batch") &&
+           ok(gpk_pin_alloc((void**)&b.h_err, P * 8), "pinned batch") &&
+           ok(gpk_pin_alloc((void**)&b.h_flow, P * 24), "pinned batch") &&
+           ok(gpk_pin_alloc((void**)&b.h_side, side_cap), "pinned batch") &&
            ok(hipMalloc((void**)&b.d_off, P * 8), "hipMalloc") && ok(hipMalloc((void**)&b.d_cap, P * 4), "hipMalloc") &&
            ok(hipMalloc((void**)&b.d_rec, P * sizeof(gpk_record)), "hipMalloc") &&
            ok(hipMalloc((void**)&b.d_err, P * 8), "hipMalloc") && ok(hipMalloc((void**)&b.d_flow, P * 24), "hipMalloc") &&
@@ -1254,7 +1255,7 @@ extern "C" int gpk_tpacket_pump(gpk_ctx* ctx, const gpk_parser* parser, gpk_tpac
     if (b.stream) (void)hipStreamSynchronize(b.stream);
     for (void* p : {(void*)b.h_off, (void*)b.h_cap, (void*)b.h_ci, (void*)b.h_rec, (void*)b.h_err, (void*)b.h_flow,
                     (void*)b.h_side})
-      if (p) (void)hipHostFree(p);
+      if (p) (void)gpk_pin_free(p);
     for (void* p : {(void*)b.d_off, (void*)b.d_cap, (void*)b.d_rec, (void*)b.d_err, (void*)b.d_flow})
       if (p) (void)hipFree(p);
     for (hipEvent_t e : {b.e0, b.h2d, b.k0, b.k1, b.done})

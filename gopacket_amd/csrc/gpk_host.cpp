@@ -10,6 +10,8 @@
 // There is no CPU decode path here: every packet is decoded by the device.
 #include <hip/hip_runtime.h>
 
+#include <sys/mman.h>
+
 #include <cstdio>
 #include <cstring>
 #include <atomic>
@@ -22,6 +24,7 @@
 #include "../../include/gpk.h"
 #include "gpk_device.h"
 #include "gpk_registry_gen.h"
+#include "gpk_pinned.h"
 
 extern "C" hipError_t gpk_launch_decode(const gpk::KParams* P, int with_l4, int with_layout, hipStream_t stream);
 extern "C" int gpk_launch_describe(const gpk::KParams* P, int with_l4, int with_layout, char* buf, size_t cap);
@@ -818,14 +821,64 @@ int gpk_decoded_list_host(gpk_ctx* c, const gpk_parser* p, const uint8_t* pkt, u
   return GPK_OK;
 }
 
+// ---- pinned host memory (gpk_pinned.h) --------------------------------------
+namespace {
+constexpr size_t kHuge = 2u << 20;
+std::mutex g_pin_mu;
+std::unordered_map<void*, size_t> g_pinned;  // mapped (huge-page) buffers -> their mapping length
+}  // namespace
+
+hipError_t gpk_pin_alloc(void** out, size_t bytes) {
+  *out = nullptr;
+  if (bytes >= 2 * kHuge) {
+    const size_t len = (bytes + kHuge - 1) & ~(kHuge - 1);
+    void* m = mmap(nullptr, len + kHuge, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
+    if (m != MAP_FAILED) {
+      // 2 MiB-aligned, so transparent huge pages can back all of it
+      const uintptr_t a = ((uintptr_t)m + kHuge - 1) & ~(uintptr_t)(kHuge - 1);
+      if (a > (uintptr_t)m) munmap(m, a - (uintptr_t)m);
+      const uintptr_t end = (uintptr_t)m + len + kHuge;
+      if (end > a + len) munmap((void*)(a + len), end - (a + len));
+      char* p = (char*)a;
+      (void)madvise(p, len, MADV_HUGEPAGE);
+      for (size_t o = 0; o < len; o += 4096) p[o] = 0;  // fault it in (one fault per huge page)
+      if (hipHostRegister(p, len, hipHostRegisterDefault) == hipSuccess) {
+        std::lock_guard<std::mutex> g(g_pin_mu);
+        g_pinned[p] = len;
+        *out = p;
+        return hipSuccess;
+      }
+      munmap(p, len);
+    }
+  }
+  return hipHostMalloc(out, bytes, hipHostMallocDefault);
+}
+
+hipError_t gpk_pin_free(void* p) {
+  if (!p) return hipSuccess;
+  size_t len = 0;
+  {
+    std::lock_guard<std::mutex> g(g_pin_mu);
+    auto it = g_pinned.find(p);
+    if (it != g_pinned.end()) {
+      len = it->second;
+      g_pinned.erase(it);
+    }
+  }
+  if (!len) return hipHostFree(p);
+  const hipError_t e = hipHostUnregister(p);
+  munmap(p, len);
+  return e;
+}
+
 int gpk_host_alloc(void** out, size_t bytes) {
   if (!out) return GPK_EINVAL;
-  HIPCHK(hipHostMalloc(out, bytes, hipHostMallocDefault));
+  HIPCHK(gpk_pin_alloc(out, bytes));
   return GPK_OK;
 }
 
 int gpk_host_free(void* p) {
-  if (p) HIPCHK(hipHostFree(p));
+  if (p) HIPCHK(gpk_pin_free(p));
   return GPK_OK;
 }
 

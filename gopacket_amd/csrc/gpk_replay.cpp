@@ -48,6 +48,7 @@
 #include <vector>
 
 #include "../../include/gpk_capture.h"
+#include "gpk_pinned.h"
 #include "gpk_walk.h"
 
 extern "C" int gpk_decode_batch_ex(gpk_ctx* c, const gpk_parser* p, const gpk_batch* b, const gpk_results* o,
@@ -273,7 +274,7 @@ struct Pipeline {
     for (auto& s : slots) {
       if (s.fill_pending) s.fill.wait();
       if (s.stream) (void)hipStreamSynchronize(s.stream);
-      if (s.host) (void)hipHostFree(s.host);
+      if (s.host) (void)gpk_pin_free(s.host);
       if (s.dev) (void)hipFree(s.dev);
       for (void* p : {(void*)s.d_seg.sync, (void*)s.d_seg.end, (void*)s.d_seg.count, (void*)s.d_seg.base,
                       (void*)s.d_off, (void*)s.d_cap, (void*)s.d_ci})
@@ -287,7 +288,7 @@ struct Pipeline {
     for (auto& B : bats) {
       for (void* p : {(void*)B.h_off, (void*)B.h_cap, (void*)B.h_ci, (void*)B.h_rec, (void*)B.h_err,
                       (void*)B.h_flow})
-        if (p) (void)hipHostFree(p);
+        if (p) (void)gpk_pin_free(p);
       for (void* p : {(void*)B.d_off, (void*)B.d_cap, (void*)B.d_rec, (void*)B.d_err, (void*)B.d_flow})
         if (p) (void)hipFree(p);
       for (hipEvent_t e : {B.e0, B.k0, B.k1, B.done})
@@ -305,7 +306,7 @@ constexpr uint64_t kOpenPrefix = 64 << 10;  // host-read bytes before the device
   } while (0)
 
 std::string alloc_slot(Slot& s, uint64_t C, uint64_t R, bool dev_walk, uint64_t max_pk) {
-  ALLOC_OK(hipHostMalloc((void**)&s.host, C + R + 16, hipHostMallocDefault), "hipHostMalloc slot");
+  ALLOC_OK(gpk_pin_alloc((void**)&s.host, C + R + 16), "pinned slot");
   memset(s.host + C + R, 0, 16);
   ALLOC_OK(hipMalloc((void**)&s.dev, C + R + 16), "hipMalloc slot");
   ALLOC_OK(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking), "hipStreamCreate");
@@ -359,12 +360,12 @@ std::string grow_index(Slot& s, uint64_t keep, uint64_t need) {
 }
 
 std::string alloc_bat(Bat& B, uint64_t P) {
-  ALLOC_OK(hipHostMalloc((void**)&B.h_off, P * 8, 0), "hipHostMalloc");
-  ALLOC_OK(hipHostMalloc((void**)&B.h_cap, P * 4, 0), "hipHostMalloc");
-  ALLOC_OK(hipHostMalloc((void**)&B.h_ci, P * sizeof(gpk_capture_info), 0), "hipHostMalloc");
-  ALLOC_OK(hipHostMalloc((void**)&B.h_rec, P * sizeof(gpk_record), 0), "hipHostMalloc");
-  ALLOC_OK(hipHostMalloc((void**)&B.h_err, P * 8, 0), "hipHostMalloc");
-  ALLOC_OK(hipHostMalloc((void**)&B.h_flow, P * 24, 0), "hipHostMalloc");
+  ALLOC_OK(gpk_pin_alloc((void**)&B.h_off, P * 8), "pinned batch");
+  ALLOC_OK(gpk_pin_alloc((void**)&B.h_cap, P * 4), "pinned batch");
+  ALLOC_OK(gpk_pin_alloc((void**)&B.h_ci, P * sizeof(gpk_capture_info)), "pinned batch");
+  ALLOC_OK(gpk_pin_alloc((void**)&B.h_rec, P * sizeof(gpk_record)), "pinned batch");
+  ALLOC_OK(gpk_pin_alloc((void**)&B.h_err, P * 8), "pinned batch");
+  ALLOC_OK(gpk_pin_alloc((void**)&B.h_flow, P * 24), "pinned batch");
   ALLOC_OK(hipMalloc((void**)&B.d_off, P * 8), "hipMalloc");
   ALLOC_OK(hipMalloc((void**)&B.d_cap, P * 4), "hipMalloc");
   ALLOC_OK(hipMalloc((void**)&B.d_rec, P * sizeof(gpk_record)), "hipMalloc");
