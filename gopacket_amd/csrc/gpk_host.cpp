@@ -30,6 +30,7 @@ extern "C" hipError_t gpk_launch_decode(const gpk::KParams* P, int with_l4, int 
 extern "C" int gpk_launch_describe(const gpk::KParams* P, int with_l4, int with_layout, char* buf, size_t cap);
 extern "C" hipError_t gpk_launch_occupancy(const gpk::KParams* P, int with_l4, int with_layout, int* blocks);
 extern "C" hipError_t gpk_launch_decode_fields(const gpk::KParams* P, hipStream_t stream, int* occ);
+extern "C" void gpk_walk_preload(void);
 extern "C" int gpk_launch_describe_fields(const gpk::KParams* P, char* buf, size_t cap);
 extern "C" hipError_t gpk_launch_list(const gpk::KParams* P, uint64_t index, int64_t* out, uint32_t cap,
                                       uint32_t* out_n, hipStream_t stream);
@@ -283,6 +284,7 @@ int gpk_ctx_create(gpk_ctx** out, int device) {
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return GPK_ENODEV;
   HIPCHK(hipSetDevice(device));
+  gpk_walk_preload();  // the replay's record-walk module (gpk_walk.hip), loaded with the context
   gpk_ctx* c = new (std::nothrow) gpk_ctx;
   if (!c) return GPK_ENOMEM;
   c->device = device;

@@ -496,14 +496,16 @@ extern "C" int gpk_replay_file(gpk_ctx* ctx, const gpk_parser* parser, const cha
     if (cached) free_cached(cached);
     pl.slots.resize(opt.slots);
     pl.bats.resize(2 * opt.slots);
-    // Every slot and batch is allocated on its own thread (pinning GBs is the
-    // slow part), in the background: slot 0 and the first two batches first,
-    // the rest once slot 0 is done, while it is being read. The call goes on
-    // as soon as the buffers it needs next exist (the cold call used to wait
-    // for all of them: 0.45 s against 0.21 s with the buffers kept).
+    // Every slot and batch is allocated on its own thread. With the pinned
+    // staging from huge-page memory (gpk_pinned.h: 2 GiB in ~20 ms) the call
+    // allocates everything before the first read: GPK_REPLAY_LAZY_ALLOC=1
+    // instead starts with slot 0 and two batches and allocates the rest behind
+    // the first read, which won while pinning took 0.38 s and now loses
+    // (tools/c5_cold.py, profiles/r15_c5_cold.txt: cold calls 0.235 s eager
+    // against 0.26-0.28 s lazy, 0.20 s with the buffers kept).
     int dev = 0;
     (void)hipGetDevice(&dev);
-    const bool lazy = !(getenv("GPK_REPLAY_EAGER_ALLOC") && getenv("GPK_REPLAY_EAGER_ALLOC")[0] == '1');
+    const bool lazy = getenv("GPK_REPLAY_LAZY_ALLOC") && getenv("GPK_REPLAY_LAZY_ALLOC")[0] == '1';
     auto slot_job = [&pl, C, R, dev_walk, max_pk, dev](size_t k, std::shared_future<std::string> after) {
       return std::async(std::launch::async, [&pl, C, R, dev_walk, max_pk, dev, k, after] {
                if (after.valid()) after.wait();

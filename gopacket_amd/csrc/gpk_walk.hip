@@ -149,3 +149,12 @@ hipError_t gpk_walk_emit(const uint8_t* buf, uint64_t len, uint32_t nseg, const 
                      offsets, caplens, ci);
   return hipGetLastError();
 }
+
+// Load this module's code object on the device now (HIP loads a module at the
+// first use of one of its kernels): gpk_ctx_create calls it, so the first
+// replay does not pay it inside its own wall time.
+extern "C" __attribute__((visibility("hidden"))) void gpk_walk_preload(void) {
+  hipFuncAttributes a;
+  (void)hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&gpk::walk_kernel));
+  (void)hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&gpk::emit_kernel));
+}
