@@ -279,18 +279,50 @@ static void free_slots(gpk_ctx* c) {
   c->aggs.clear();
 }
 
+// The first C++ exception a process throws initialises the unwinder's
+// frame tables for every loaded object: ~80 ms on the GPU box with PyTorch's
+// libraries loaded (350 ms in this container), paid by whichever call throws
+// first. The capture reader throws one at every chunk end (a record cut by
+// the chunk: NeedMore, gpk_capture.cpp), so the first replay of a process
+// paid it inside its wall time (GPK_REPLAY_TRACE=3: its first 64 KiB host
+// walk took 83 ms, 0.06 ms afterwards). A context takes it at creation.
+__attribute__((noinline)) static void warm_unwinder() {
+  try {
+    throw std::bad_alloc();
+  } catch (const std::bad_alloc&) {
+  }
+}
+
 int gpk_ctx_create(gpk_ctx** out, int device) {
   if (!out) return GPK_EINVAL;
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return GPK_ENODEV;
   HIPCHK(hipSetDevice(device));
   gpk_walk_preload();  // the replay's record-walk module (gpk_walk.hip), loaded with the context
+  warm_unwinder();
   gpk_ctx* c = new (std::nothrow) gpk_ctx;
   if (!c) return GPK_ENOMEM;
   c->device = device;
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
     delete c;
     return GPK_EHIP;
+  }
+  // The first host<->device copies of a process pay a one-time setup inside
+  // the HIP runtime (~80 ms before the first replay's first slot landed on the
+  // box: tools/c5_cold.py with GPK_REPLAY_TRACE=2): paid here, with the
+  // context, on a 4 MiB pinned buffer in both directions.
+  {
+    void* h = nullptr;
+    void* d = nullptr;
+    constexpr size_t kWarm = 4u << 20;
+    if (gpk_pin_alloc(&h, kWarm) == hipSuccess && hipMalloc(&d, kWarm) == hipSuccess) {
+      memset(h, 0, kWarm);
+      if (hipMemcpyAsync(d, h, kWarm, hipMemcpyHostToDevice, c->stream) == hipSuccess &&
+          hipMemcpyAsync(h, d, kWarm, hipMemcpyDeviceToHost, c->stream) == hipSuccess)
+        (void)hipStreamSynchronize(c->stream);
+    }
+    if (d) (void)hipFree(d);
+    if (h) (void)gpk_pin_free(h);
   }
   *out = c;
   return GPK_OK;

@@ -687,6 +687,7 @@ extern "C" int gpk_replay_file(gpk_ctx* ctx, const gpk_parser* parser, const cha
         pos += hu;
         ended = st != GPK_CAP_MORE;
         on_dev = !ended && gpk_capreader_walk_state(rd, &ws);
+        if (trace && trace[0] == '3') fprintf(stderr, "  slot %llu host prefix %.2f ms\n", (unsigned long long)si, (now_s() - t_ix) * 1e3);
       }
       if (good && on_dev) {
         const uint64_t seg = std::max<uint64_t>(4096, ((L + kMaxSeg - 1) / kMaxSeg + 3) & ~3ull);
@@ -698,6 +699,7 @@ extern "C" int gpk_replay_file(gpk_ctx* ctx, const gpk_parser* parser, const cha
                pl.ok(hipMemcpyAsync(S.h_seg.count, S.d_seg.count, nseg * 4ull, hipMemcpyDeviceToHost, S.stream),
                      "DtoH walk") &&
                pl.ok(hipStreamSynchronize(S.stream), "hipStreamSynchronize");
+        if (trace && trace[0] == '3') fprintf(stderr, "  slot %llu device walk %.2f ms\n", (unsigned long long)si, (now_s() - t_ix) * 1e3);
         // Accept segments while each starts where the previous one's chain
         // ended (segment 0 starts where the reader stands) and covers its
         // segment. Where one does not, the exact reader walks on the host from
@@ -742,6 +744,7 @@ extern "C" int gpk_replay_file(gpk_ctx* ctx, const gpk_parser* parser, const cha
           if (!gpk_capreader_walk_state(rd, &w2) || memcmp(&w2, &ws, sizeof(ws)) != 0) break;  // the host takes the rest
           k = pos == S.h_seg.sync[j] ? j : j + 1;  // landed: resume there; else sync[j] was inside a record
         }
+        if (trace && trace[0] == '3') fprintf(stderr, "  slot %llu accepted %.2f ms\n", (unsigned long long)si, (now_s() - t_ix) * 1e3);
         if (good && dev_pk) {
           g_emit = G;
           const std::string ge = grow_index(S, 0, G);
@@ -787,6 +790,7 @@ extern "C" int gpk_replay_file(gpk_ctx* ctx, const gpk_parser* parser, const cha
                        "HtoD index");
         }
         good = pl.ok(hipStreamSynchronize(S.stream), "hipStreamSynchronize") && good;  // the chunks are freed below
+        if (trace && trace[0] == '3') fprintf(stderr, "  slot %llu host chunks copied %.2f ms\n", (unsigned long long)si, (now_s() - t_ix) * 1e3);
       }
       for (auto& ch : chunks) gpk_capindex_free(&ch.second);
       stats->device_walk_packets += dev_pk;

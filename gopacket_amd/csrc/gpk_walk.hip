@@ -150,11 +150,17 @@ hipError_t gpk_walk_emit(const uint8_t* buf, uint64_t len, uint32_t nseg, const 
   return hipGetLastError();
 }
 
-// Load this module's code object on the device now (HIP loads a module at the
-// first use of one of its kernels): gpk_ctx_create calls it, so the first
-// replay does not pay it inside its own wall time.
+// Load this module's code object on the device now and run its pass-1 kernel
+// once over 128 zero bytes (no interface, so no block is plain and nothing is
+// accepted): gpk_ctx_create calls it, so the first replay of a process does
+// not pay the module's first use inside its own wall time.
 extern "C" __attribute__((visibility("hidden"))) void gpk_walk_preload(void) {
-  hipFuncAttributes a;
-  (void)hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&gpk::walk_kernel));
-  (void)hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&gpk::emit_kernel));
+  uint8_t* d = nullptr;
+  if (hipMalloc(&d, 256) != hipSuccess) return;
+  gpk::WalkState ws{};
+  gpk::WalkSegs out{reinterpret_cast<uint64_t*>(d + 128), reinterpret_cast<uint64_t*>(d + 144),
+                    reinterpret_cast<uint32_t*>(d + 160), reinterpret_cast<uint64_t*>(d + 176)};
+  if (hipMemset(d, 0, 256) == hipSuccess && gpk_walk_segments(d, 0, 128, 128, 1, ws, out, nullptr) == hipSuccess)
+    (void)hipDeviceSynchronize();
+  (void)hipFree(d);
 }
