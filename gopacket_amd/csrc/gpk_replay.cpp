@@ -400,7 +400,7 @@ extern "C" int gpk_replay_file(gpk_ctx* ctx, const gpk_parser* parser, const cha
   if (!ctx || !parser || !path || !stats) return GPK_EINVAL;
   memset(stats, 0, sizeof(*stats));
   const double t_start = now_s();
-  gpk_replay_opts opt{0, 0, 256ull << 20, 4, 2ull << 20, 8};
+  gpk_replay_opts opt{0, 0, 256ull << 20, 4, 1ull << 20, 8};
   if (o) {
     opt.format = o->format;
     opt.ng_flags = o->ng_flags;
@@ -473,7 +473,14 @@ extern "C" int gpk_replay_file(gpk_ctx* ctx, const gpk_parser* parser, const cha
   // ---- buffers ---------------------------------------------------------------
   // (kept in the context between calls: the pinned staging slots are ~GBs and
   // allocating them costs as much as replaying a 10 GB file)
-  const uint64_t R = opt.slot_bytes, C = opt.slot_bytes;  // fresh bytes, carry region
+  // fresh bytes per slot, and the carry region before them (the record cut by
+  // the previous slot's end is moved there, so a record may be as long as
+  // it): the whole slot up to 1 MiB, else a quarter of it and at least 1 MiB
+  // (64 MiB of 256 MiB: a pcapng block can be longer only in theory, and the
+  // region is pinned memory every slot holds; C5's first call allocated 3.4 GB
+  // of pinned staging with 256 MiB carry regions and 2 Mi-packet batches,
+  // 2.0 GB now)
+  const uint64_t R = opt.slot_bytes, C = R <= (1ull << 20) ? R : std::max<uint64_t>(1ull << 20, R / 4);
   Pipeline pl;
   pl.cb = cb;
   pl.user = user;
@@ -638,7 +645,7 @@ extern "C" int gpk_replay_file(gpk_ctx* ctx, const gpk_parser* parser, const cha
     const uint64_t fresh = fl.bytes;
     const bool eof = fl.end;
     if (carry_len > C) {  // a record longer than the carry region: not supported
-      snprintf(stats->error, sizeof(stats->error), "capture record larger than the %llu-byte staging slot",
+      snprintf(stats->error, sizeof(stats->error), "capture record larger than the %llu-byte staging carry region",
                (unsigned long long)C);
       rc = GPK_EUNSUPP;
       break;
