@@ -887,12 +887,13 @@ def fields_bench(ctx, name="c4", n=64 * 2**20, reps=5, check_packets=4 << 20):
         bad += int((~ok).sum())
     written = 16 + 24 + 128  # record, three flow hashes, fields (+8 on error)
     ach = algo / (fused * 1e-3) / 1e9
+    traffic, traffic_profile = load_traffic("c4f", n)  # the fused launch's PMC profile (tools/profile.sh c4f)
     res = dict(workload=CONFIGS[name]["workload"] + " + layer fields (gpk_decode_batch_fields)",
                kernel=ctx.kernel_name(parser, data, off, cap, layouts=_lib.NAME_FIELDS),
                blocks_per_cu=ctx.occupancy(parser, data, off, cap, layouts=_lib.NAME_FIELDS),
                kernel_ms=round(fused, 4), value=round(n / fused / 1e3, 2), unit="Mpkts/s",
                achieved_GBps=round(ach, 1), frac=round(ach / HBM_PEAK_GBS, 4),
-               written_bytes_per_packet=written,
+               written_bytes_per_packet=written, traffic=traffic, traffic_profile=traffic_profile,
                read_plus_written_GBps=round((algo + written * n) / (fused * 1e-3) / 1e9, 1),
                two_launch_ms=round(two, 4), two_launch_kernels=[ctx.kernel_name(parser, data, off, cap, layouts=True),
                                                                 "fields_kernel"],

@@ -14,9 +14,11 @@
 
 #include <cstdio>
 #include <cstring>
+#include <algorithm>
 #include <atomic>
 #include <mutex>
 #include <unordered_map>
+#include <thread>
 #include <vector>
 #include <new>
 #include <string>
@@ -875,7 +877,19 @@ hipError_t gpk_pin_alloc(void** out, size_t bytes) {
       if (end > a + len) munmap((void*)(a + len), end - (a + len));
       char* p = (char*)a;
       (void)madvise(p, len, MADV_HUGEPAGE);
-      for (size_t o = 0; o < len; o += 4096) p[o] = 0;  // fault it in (one fault per huge page)
+      // fault it in (one fault per huge page; the kernel zeroes each): a
+      // buffer of 64 MiB or more on up to 8 threads (pin_probe: 4 x 512 MiB
+      // in 18 ms touched 4 ways each)
+      const size_t nt = len >= (64u << 20) ? std::min<size_t>(8, len / (32u << 20)) : 1;
+      const size_t per = ((len / nt) + kHuge - 1) & ~(kHuge - 1);
+      auto touch = [p, len, per](size_t t) {
+        const size_t a = t * per, b = std::min(len, a + per);
+        for (size_t o = a; o < b; o += 4096) p[o] = 0;
+      };
+      std::vector<std::thread> th;
+      for (size_t t = 1; t < nt; t++) th.emplace_back(touch, t);
+      touch(0);
+      for (auto& x : th) x.join();
       if (hipHostRegister(p, len, hipHostRegisterDefault) == hipSuccess) {
         std::lock_guard<std::mutex> g(g_pin_mu);
         g_pinned[p] = len;

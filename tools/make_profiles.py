@@ -31,7 +31,7 @@ import pmc_summary  # noqa: E402
 
 def packets_of(cfg):
     import bench
-    c = bench.CONFIGS[cfg]
+    c = bench.CONFIGS[cfg[:-1] if cfg.endswith("f") else cfg]  # c4f: C4's batch with the fused fields
     return c.get("packets", 64 * 2**20)
 
 
