@@ -475,12 +475,12 @@ extern "C" int gpk_replay_file(gpk_ctx* ctx, const gpk_parser* parser, const cha
   // allocating them costs as much as replaying a 10 GB file)
   // fresh bytes per slot, and the carry region before them (the record cut by
   // the previous slot's end is moved there, so a record may be as long as
-  // it): the whole slot up to 1 MiB, else a quarter of it and at least 1 MiB
-  // (64 MiB of 256 MiB: a pcapng block can be longer only in theory, and the
-  // region is pinned memory every slot holds; C5's first call allocated 3.4 GB
-  // of pinned staging with 256 MiB carry regions and 2 Mi-packet batches,
-  // 2.0 GB now)
-  const uint64_t R = opt.slot_bytes, C = R <= (1ull << 20) ? R : std::max<uint64_t>(1ull << 20, R / 4);
+  // it): the whole slot up to 1 MiB, else a sixteenth of it and at least 1 MiB
+  // (16 MiB of 256 MiB: 64 times the largest snap length pcap writers use; a
+  // longer pcapng block exists only in theory, and the region is pinned memory
+  // every slot holds: C5's first call allocated 3.4 GB of pinned staging with
+  // 256 MiB carry regions and 8 batches of 2 Mi packets, 1.6 GB now)
+  const uint64_t R = opt.slot_bytes, C = R <= (1ull << 20) ? R : std::max<uint64_t>(1ull << 20, R / 16);
   Pipeline pl;
   pl.cb = cb;
   pl.user = user;
@@ -502,7 +502,7 @@ extern "C" int gpk_replay_file(gpk_ctx* ctx, const gpk_parser* parser, const cha
   } else {
     if (cached) free_cached(cached);
     pl.slots.resize(opt.slots);
-    pl.bats.resize(2 * opt.slots);
+    pl.bats.resize(opt.slots + 2);  // batches in flight: about one per slot (a slot of the C4 mix holds ~0.7 Mi packets)
     // Every slot and batch is allocated on its own thread. With the pinned
     // staging from huge-page memory (gpk_pinned.h: 2 GiB in ~20 ms) the call
     // allocates everything before the first read: GPK_REPLAY_LAZY_ALLOC=1

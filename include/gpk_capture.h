@@ -148,7 +148,7 @@ typedef struct gpk_replay_opts {
   uint32_t ng_flags;     /* GPK_NG_* */
   uint64_t slot_bytes;   /* file bytes per pinned staging slot (default 256 MiB); a record (pcap
                             record, pcapng block) may be as long as the slot's carry region:
-                            slot_bytes up to 1 MiB, else max(1 MiB, slot_bytes / 4); a longer
+                            slot_bytes up to 1 MiB, else max(1 MiB, slot_bytes / 16); a longer
                             one ends the call with GPK_EUNSUPP */
   int slots;             /* staging slots in flight (default 4)                 */
   uint64_t batch_pkts;   /* packets per device launch (default 1 Mi)            */
