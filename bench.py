@@ -512,6 +512,13 @@ def c5_replay(ctx, gib=10.0, reps=2, threads=8, cpu_threads=16):
     path = os.path.join(os.environ.get("TMPDIR", "/tmp"), "gpk_c5_%d.pcapng" % os.getpid())
     t0 = time.perf_counter()
     size = S.gpk_synth_write_pcapng(path.encode(), 4, 0, n, cpu_threads)
+    if size:
+        # the file is replayed from the page cache as a capture written earlier would be: its
+        # writeback done first (the first replay otherwise shares the host with the kernel
+        # flushing 10 GB of dirty pages: profiles/r15_c5_cold.txt)
+        fd = os.open(path, os.O_RDONLY)
+        os.fsync(fd)
+        os.close(fd)
     gen_s = time.perf_counter() - t0
     if not size:
         raise RuntimeError("could not write %s" % path)

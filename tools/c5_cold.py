@@ -24,6 +24,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gib", type=float, default=10.0)
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--no-fsync", action="store_true", help="replay while the file's writeback may still run")
     a = ap.parse_args()
     import torch  # noqa: F401
     import bench
@@ -34,6 +35,10 @@ def main():
     n = int(a.gib * 2**30 / per)
     path = os.path.join(os.environ.get("TMPDIR", "/tmp"), "gpk_c5cold_%d.pcapng" % os.getpid())
     size = S.gpk_synth_write_pcapng(path.encode(), 4, 0, n, 16)
+    if not a.no_fsync:  # writeback done before the first call (as bench.py's C5)
+        fd = os.open(path, os.O_RDONLY)
+        os.fsync(fd)
+        os.close(fd)
     out = dict(file_bytes=size, packets=n, runs=[])
 
     def call(ctx, label):
