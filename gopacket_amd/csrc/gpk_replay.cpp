@@ -503,16 +503,18 @@ extern "C" int gpk_replay_file(gpk_ctx* ctx, const gpk_parser* parser, const cha
     if (cached) free_cached(cached);
     pl.slots.resize(opt.slots);
     pl.bats.resize(opt.slots + 2);  // batches in flight: about one per slot (a slot of the C4 mix holds ~0.7 Mi packets)
-    // Every slot and batch is allocated on its own thread. With the pinned
-    // staging from huge-page memory (gpk_pinned.h: 2 GiB in ~20 ms) the call
-    // allocates everything before the first read: GPK_REPLAY_LAZY_ALLOC=1
-    // instead starts with slot 0 and two batches and allocates the rest behind
-    // the first read, which won while pinning took 0.38 s and now loses
-    // (tools/c5_cold.py, profiles/r15_c5_cold.txt: cold calls 0.235 s eager
-    // against 0.26-0.28 s lazy, 0.20 s with the buffers kept).
+    // Every slot and batch is allocated on its own thread, in the background:
+    // slot 0 and the first two batches first, the rest once slot 0 is done,
+    // while it is being read; the read of a slot and the first use of a batch
+    // wait for their own allocation. With 1.6 GB of pinned staging from
+    // huge-page memory (gpk_pinned.h) a cold call took 0.215 s this way against
+    // 0.223 s allocating everything first and 0.20 s with the buffers kept
+    // (tools/c5_cold.py, profiles/r15_c5_cold.txt); with 3.4 GB from
+    // hipHostMalloc (0.38 s to pin) it was 0.45 s. GPK_REPLAY_EAGER_ALLOC=1
+    // allocates everything before the first read.
     int dev = 0;
     (void)hipGetDevice(&dev);
-    const bool lazy = getenv("GPK_REPLAY_LAZY_ALLOC") && getenv("GPK_REPLAY_LAZY_ALLOC")[0] == '1';
+    const bool lazy = !(getenv("GPK_REPLAY_EAGER_ALLOC") && getenv("GPK_REPLAY_EAGER_ALLOC")[0] == '1');
     auto slot_job = [&pl, C, R, dev_walk, max_pk, dev](size_t k, std::shared_future<std::string> after) {
       return std::async(std::launch::async, [&pl, C, R, dev_walk, max_pk, dev, k, after] {
                if (after.valid()) after.wait();

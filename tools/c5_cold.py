@@ -1,9 +1,9 @@
 #!/usr/bin/env python3
 """C5 cold call: gpk_replay_file on a fresh context (staging buffers not yet
 allocated) against the same call with the context's kept buffers, and the
-allocation of everything before the first read (default) against the
-background allocation behind it (GPK_REPLAY_LAZY_ALLOC=1), alternating, in
-one process.
+background allocation behind the first read (default) against allocating
+everything before it (GPK_REPLAY_EAGER_ALLOC=1), alternating, in one
+process.
 
     python tools/c5_cold.py [--gib 10] [--rounds 3]
 
@@ -57,16 +57,16 @@ def main():
         call(first, "process first call (the context loaded the walk module)")
         call(first, "warm (kept buffers)")
         for k in range(a.rounds):
-            for lazy in (False, True):
-                if lazy:
-                    os.environ["GPK_REPLAY_LAZY_ALLOC"] = "1"
+            for eager in (False, True):
+                if eager:
+                    os.environ["GPK_REPLAY_EAGER_ALLOC"] = "1"
                 else:
-                    os.environ.pop("GPK_REPLAY_LAZY_ALLOC", None)
+                    os.environ.pop("GPK_REPLAY_EAGER_ALLOC", None)
                 ctx = engine.Context(0)
-                call(ctx, "cold lazy" if lazy else "cold eager (default)")
+                call(ctx, "cold eager" if eager else "cold background allocation (default)")
                 call(ctx, "warm")
                 del ctx
-        os.environ.pop("GPK_REPLAY_LAZY_ALLOC", None)
+        os.environ.pop("GPK_REPLAY_EAGER_ALLOC", None)
     finally:
         os.unlink(path)
     print(json.dumps(out))
