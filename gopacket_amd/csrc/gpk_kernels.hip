@@ -78,6 +78,10 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 #ifndef GPK_PB_LDS_HT
 #define GPK_PB_LDS_HT 1  // segment head/tail chunks from the LDS header windows when they hold them
 #endif
+#ifndef GPK_BLOB_DMA
+#define GPK_BLOB_DMA 0  // each wave copies the table blob into LDS by LDS-DMA itself, no block barrier (A/B r15:
+                        // C4 +-0, C2 +1 %, C1 +5 %: the barrier was not what held the waves)
+#endif
 #ifndef GPK_BLOB_ROUND
 #define GPK_BLOB_ROUND 128  // dwords: the table blob's LDS share is rounded to this
 #endif
@@ -258,6 +262,28 @@ __device__ __forceinline__ uint32_t l_to_words(uint32_t L, uint32_t odd) {
 __device__ __forceinline__ u32x4 lds_chunk(uint32_t a) {
   const uint32_t* p = gpk_smem + ((a == ~0u ? 0u : a) >> 2);
   return u32x4{p[0], p[1], p[2], p[3]};
+}
+
+// The parser's compact table blob (P.cg.words dwords) into LDS at byte
+// address lds_base by THIS wave alone, by LDS-DMA (global_load_lds_dword:
+// lane l's dword lands at M0 + 4 l; no registers held, completion counted by
+// vmcnt). Every wave of the block writes the same words to the same
+// addresses, so a wave needs only its own copy to have landed (s_waitcnt
+// vmcnt) and the block needs no barrier: before, the block's waves waited for
+// each other there (in the stream-before-parse kernel after their streams).
+// Writes stay inside the blob's LDS share (rounded to GPK_BLOB_ROUND dwords >=
+// 64); lanes past the blob re-read its last word.
+__device__ __forceinline__ void blob_dma(const KParams& P, uint32_t lds_base, uint32_t lane) {
+  const uint32_t words = P.cg.words, last = words - 1;
+  const uint64_t src = (uint64_t)(uintptr_t)P.ctab;
+  for (uint32_t k = 0; 64 * k < words; k++) {  // wave-uniform trip count
+    const uint32_t j = 64 * k + lane;
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(src + 4ull * (j < last ? j : last)), "s"(lds_base + 256u * k)
+                 : "memory");
+  }
 }
 
 // A granule: kGran consecutive 16-byte chunks.
@@ -1302,7 +1328,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W == 4 ?
   const WinGeo g0 = win_geo<W, AL>(P, c0, i0 < P.n);
   WinT<W> w0;
   load_window<W, AL>(P, g0, w0);
-  if (kCompact) {  // the table blob (<= kCtDwords): clamped indices, duplicate writes of equal values
+  if (kCompact && GPK_BLOB_DMA) {
+    static_assert(GPK_BLOB_ROUND % 64 == 0, "the blob's LDS share holds whole 64-dword DMA rows");
+    blob_dma(P, (uint32_t)(uintptr_t)gpk_smem + 4u * base, tid & 63);
+  } else if (kCompact) {  // the table blob (<= kCtDwords): clamped indices, duplicate writes of equal values
     static_assert(kCtDwords <= 3 * kBlock, "three blob words per thread");
     const uint32_t last = P.cg.words - 1;
 #pragma unroll
@@ -1313,6 +1342,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W == 4 ?
     __syncthreads();
   }
   store_window<W, AL>(slot_dw, w0);
+  // this wave's blob DMA has landed before the parse reads the tables (and
+  // before decode_packet issues any stream load)
+  if (kCompact && GPK_BLOB_DMA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #if GPK_DIAG_TIMES
   dt[2] = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -1393,7 +1425,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(O, 8))) 
   const Idx c0 = load_index(P, i0);
   const WinGeo g0 = win_geo<W, 16>(P, c0, active);
   window_dma<W>(P, g0, (uint32_t)(uintptr_t)gpk_smem + wave * (64u * kSbStride * 4u), lane);
-  if (kCompact) {  // the table blob (read after the barrier below)
+  if (kCompact && GPK_BLOB_DMA) {  // this wave's own copy (the vmcnt(0) below waits for it)
+    blob_dma(P, (uint32_t)(uintptr_t)gpk_smem + 4u * base, lane);
+  } else if (kCompact) {  // the table blob (read after the barrier below)
     static_assert(kCtDwords <= 3 * kBlock, "three blob words per thread");
     const uint32_t last = P.cg.words - 1;
 #pragma unroll
@@ -1418,8 +1452,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(O, 8))) 
     S.on = true;
     L = sb_stream<D>(P, S, R0, R, lane, a1, b);
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the windows have landed (the stream waited for them too)
-  if (kCompact) __syncthreads();
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the windows (and this wave's blob) have landed
+  if (kCompact && !GPK_BLOB_DMA) __syncthreads();
 #if GPK_DIAG_TIMES
   dt[2] = __builtin_amdgcn_s_memrealtime();
 #endif
