@@ -52,6 +52,10 @@ for _o in (1, 3, 5):
 CONFIGS["c1x1"] = dict(CONFIGS["c1"], outputs=1, workload="C1 packets, IPv4 checksum only (diagnostic)")
 CONFIGS["c4x0"] = dict(CONFIGS["c4"], outputs=0, workload="C4 packets, decode only (diagnostic)")
 CONFIGS["c2x0"] = dict(CONFIGS["c2"], outputs=0, workload="C2 packets, decode only (diagnostic)")
+# C4's IMIX packets through a parser with no IPv6 decoder: the dword-window kernel (decode_kernel<..., 4>)
+# on waves of mixed sizes (diagnostic)
+CONFIGS["c4m"] = dict(CONFIGS["c4"], decoders=("Ethernet", "Dot1Q", "IPv4", "TCP", "UDP", "Payload"),
+                      workload="C4 packets, parser without IPv6 (diagnostic: dword-window kernel)")
 # BASELINE configs[3] as written: ONE 64M IMIX batch split across the ranks at byte-balanced
 # cuts (shard.byte_balanced_bounds; strong scaling, run by default when world > 1)
 CONFIGS["c4s"] = dict(CONFIGS["c4"], strong=True,

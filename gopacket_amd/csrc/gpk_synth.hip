@@ -111,6 +111,42 @@ __global__ __launch_bounds__(256) void probe_read_kernel(const uint8_t* data, ui
   if (acc == 0x9e3779b9u) out[0] = acc;  // keep the loads live; practically never stores
 }
 
+// Mixed probe: the streaming read of probe_read_kernel over data[0, nbytes)
+// and, at the same time, non-temporal 16-byte stores over wbuf[0, wbytes) (the
+// records / flows / fields a decode writes): the first `writers` blocks store,
+// the rest read, each side grid-strided over its own blocks. Its rate (read +
+// written bytes over the time) is the box's achievable HBM rate for that mix.
+__global__ __launch_bounds__(256) void probe_mixed_kernel(const uint8_t* data, uint64_t nvec, uint8_t* wbuf,
+                                                          uint64_t wvec, uint32_t writers, uint32_t* out) {
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  if (blockIdx.x < writers) {
+    u32x4* w = reinterpret_cast<u32x4*>(wbuf);
+    const uint64_t stride = (uint64_t)writers * 256;
+    const u32x4 x = {blockIdx.x, threadIdx.x, 0x9e3779b9u, 1u};
+    for (uint64_t k = (uint64_t)blockIdx.x * 256 + threadIdx.x; k < wvec; k += stride) __builtin_nontemporal_store(x, w + k);
+    return;
+  }
+  const u32x4* v = reinterpret_cast<const u32x4*>(data);
+  const uint64_t stride = (uint64_t)(gridDim.x - writers) * 256;
+  uint64_t k = (uint64_t)(blockIdx.x - writers) * 256 + threadIdx.x;
+  uint32_t acc = 0;
+  for (; k + 3 * stride < nvec; k += 4 * stride) {
+    u32x4 a = __builtin_nontemporal_load(v + k);
+    u32x4 b = __builtin_nontemporal_load(v + k + stride);
+    u32x4 c = __builtin_nontemporal_load(v + k + 2 * stride);
+    u32x4 d = __builtin_nontemporal_load(v + k + 3 * stride);
+    acc = __builtin_amdgcn_udot4(a.x ^ b.y ^ c.z ^ d.w, 0x01010101u, acc, false);
+    acc = __builtin_amdgcn_udot4(a.y ^ b.z ^ c.w ^ d.x, 0x01010101u, acc, false);
+    acc = __builtin_amdgcn_udot4(a.z ^ b.w ^ c.x ^ d.y, 0x01010101u, acc, false);
+    acc = __builtin_amdgcn_udot4(a.w ^ b.x ^ c.y ^ d.z, 0x01010101u, acc, false);
+  }
+  for (; k < nvec; k += stride) {
+    u32x4 a = __builtin_nontemporal_load(v + k);
+    acc = __builtin_amdgcn_udot4(a.x ^ a.y ^ a.z ^ a.w, 0x01010101u, acc, false);
+  }
+  if (acc == 0x9e3779b9u) out[0] = acc;
+}
+
 // Re-read probe (the traffic question): one wave per region of
 // 64 "packets" of pkt bytes, the decode kernel's access pattern without its
 // work. mode 0: the region streamed once (1 KiB per pass, 16 B per lane,
@@ -421,6 +457,15 @@ int gpk_probe_reread(const uint8_t* data, uint64_t nbytes, uint32_t pkt, int mod
 // Launch the streaming-read probe over data[0, nbytes & ~15) on `stream`.
 int gpk_probe_read(const uint8_t* data, uint64_t nbytes, uint32_t* out, int blocks, void* stream) {
   hipLaunchKernelGGL(probe_read_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, data, nbytes / 16, out);
+  return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+// Launch the mixed read + write probe (blocks in all; writers of them store).
+int gpk_probe_mixed(const uint8_t* data, uint64_t nbytes, uint8_t* wbuf, uint64_t wbytes, int blocks, int writers,
+                    uint32_t* out, void* stream) {
+  if (writers < 0 || writers >= blocks) return -1;
+  hipLaunchKernelGGL(probe_mixed_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, data, nbytes / 16, wbuf,
+                     wbytes / 16, (uint32_t)writers, out);
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 

@@ -9,7 +9,8 @@ in interleaved rounds so clocks and thermals affect them alike.
 "base" = gopacket_amd/libgpk.so, NAME = gopacket_amd/build/libgpk_NAME.so;
 NAME@global runs that library with gpk_ctx_set_table_mode(GPK_TABLES_GLOBAL).
 --fields times gpk_decode_batch_fields (the fused decode + layer fields launch)
-instead of gpk_decode_batch.
+instead of gpk_decode_batch. --check compares every variant's records, error
+arguments and flows (and fields) with the first variant's, bit for bit.
 Prints, per config and variant, the median and min kernel ms over rounds.
 """
 import argparse
@@ -43,6 +44,7 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--packets", type=int, default=64 * 2**20)
     ap.add_argument("--fields", action="store_true")
+    ap.add_argument("--check", action="store_true")
     ap.add_argument("variants", nargs="+")
     a = ap.parse_args()
     import numpy as np
@@ -111,6 +113,28 @@ def main():
             print("%-4s %-10s median %8.3f ms  min %8.3f ms  %7.1f GB/s (%.1f%% of 8 TB/s)  blocks/CU %s" % (
                 name, v, np.median(t), t.min(), algo / (np.median(t) * 1e-3) / 1e9,
                 algo / (np.median(t) * 1e-3) / 8e12 * 100, occ[v]), flush=True)
+        if a.check:
+            ref = None
+            for v, L in libs.items():
+                ctx, p = handles[v]
+                rec.fill_(0xA5)
+                err.fill_(-1)
+                fl.fill_(-1)
+                fields.fill_(0x5A)
+                if a.fields:
+                    rc = L.gpk_decode_batch_fields(ctx, p, ctypes.byref(b), ctypes.byref(r),
+                                                   ctypes.c_void_p(fields.data_ptr()), ctypes.c_void_p(stream.cuda_stream))
+                else:
+                    rc = L.gpk_decode_batch(ctx, p, ctypes.byref(b), ctypes.byref(r), ctypes.c_void_p(stream.cuda_stream))
+                assert rc == 0
+                torch.cuda.synchronize()
+                out = [x.clone() for x in (rec, err, fl, fields)]
+                if ref is None:
+                    ref = out
+                    continue
+                same = all(torch.equal(x, y) for x, y in zip(ref, out))
+                print("%-4s %-10s outputs %s the first variant's" % (name, v, "equal" if same else "DIFFER from"), flush=True)
+            del ref, out
         del data, off, cap, rec, err, fl, fields
         torch.cuda.empty_cache()
 
