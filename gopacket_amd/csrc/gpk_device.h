@@ -69,6 +69,7 @@ struct KParams {
   uint32_t small_headers;   // no Dot1Q / IPv6 / IPv6-extension / TCP decoder: a 4-chunk window suffices
   uint32_t mid_headers;     // no IPv6 / IPv6-extension decoder: the small-packet kernel's 5-chunk window suffices
   uint32_t big_packets;     // batch bytes / packets >= 1 KiB: launch choice only (occupancy)
+  uint32_t mean_bytes;      // batch bytes / packets (capped at 2^32 - 1): launch choice only
   uint32_t* keys;
   uint64_t* khash;
   int32_t* kcode;

@@ -592,7 +592,9 @@ static int make_params(gpk_ctx* c, const gpk_parser* p, const gpk_batch* b, cons
   P.offsets = b->offsets;
   P.caplens = b->caplens;
   P.n = b->n;
-  P.big_packets = b->n && (packet_bytes ? packet_bytes : b->data_bytes) / b->n >= 1024;
+  const uint64_t mean = b->n ? (packet_bytes ? packet_bytes : b->data_bytes) / b->n : 0;
+  P.big_packets = mean >= 1024;
+  P.mean_bytes = mean > 0xffffffffull ? 0xffffffffu : (uint32_t)mean;
   P.data_end = (b->data_bytes + 15) & ~15ull;
   P.records = o ? o->records : nullptr;
   P.err_args = o ? o->err_args : nullptr;

@@ -178,7 +178,7 @@ def test_fields_header_ends_at_buffer_end(gpu_ctx):
     want = O.extract_fields(buf, off, ref["layouts"])
     got = fields.cpu().numpy().reshape(-1, 128)
     assert np.array_equal(got, want)
-    f = got[-1:].view(_lib.FIELDS_DTYPE)[0]
+    f = got[-1:].view(_lib.FIELDS_DTYPE).reshape(-1)[0]
     assert (int(f["tcp_checksum"]), int(f["tcp_urgent"]), int(f["tcp_window"])) == (0x1234, 0xBEEF, 512)
 
 

@@ -293,13 +293,24 @@ def phase_b_layout(packets, layout):
 
 # the kernels the no-layout runs must take (gpk_decode_kernel_name): the
 # stream-before-parse kernel for parsers with IPv6, the dword-aligned 5-chunk
-# kernel for parsers without; batches with a mean packet of 1 KiB or more take
-# the 80-VGPR 6-chunk kernel
+# kernel for parsers without when the batch's mean (buffer bytes / packets) is
+# under 256 B (GPK_MID_MAXMEAN; the stream-before-parse kernel from there on);
+# batches with a mean packet of 1 KiB or more take the 80-VGPR 6-chunk kernel
+SB_KERNEL = "gpk::decode_sb_kernel<true,7,6,false>"
 PHASE_B_KERNELS = {
-    "statsassembly": "gpk::decode_sb_kernel<true,7,6,false>",
-    "raw_ip6": "gpk::decode_sb_kernel<true,7,6,false>",
+    "statsassembly": SB_KERNEL,
+    "raw_ip6": SB_KERNEL,
     "eth_ip4_tcp_payload": "gpk::decode_kernel<true,false,true,false,5,7,4>",
 }
+
+
+def phase_b_kernel(name, data, off):
+    mean = len(data) // max(1, len(off))
+    if mean >= 1024:
+        return "gpk::decode_kernel<true,false,true,false,6,6,16>"
+    if name == "eth_ip4_tcp_payload" and mean >= 256:
+        return SB_KERNEL
+    return PHASE_B_KERNELS[name]
 
 
 @pytest.mark.parametrize("layouts", [True, False])
@@ -318,8 +329,7 @@ def test_phase_b_layouts(gpu_ctx, layout, layouts):
         cfg = CONFIGS[name]
         dp = device_parser(cfg)
         if not layouts:
-            want = ("gpk::decode_kernel<true,false,true,false,6,6,16>" if layout == "sparse4k"
-                    else PHASE_B_KERNELS[name])
+            want = phase_b_kernel(name, data, off)
             assert gpu_ctx.kernel_name(dp, data, off, cap, layouts=False) == want, (layout, name)
         dev = gpu_ctx.decode_host(dp, data, off, cap, layouts=layouts)
         ref = oracle_parser(cfg).decode(data, off, cap, nthreads=8, layouts=layouts)
