@@ -63,6 +63,26 @@ def test_synthetic(gpu_ctx, synth_cfg, cfg_name):
     assert_same(dev, ref, "synth%d" % synth_cfg)
 
 
+@pytest.mark.parametrize("synth_cfg,want", [
+    (2, "gpk::decode_kernel<true,false,true,false,5,7,4>"),  # 64-76 B: the dword-aligned 5-chunk kernel
+    (4, "gpk::decode_sb_kernel<true,7,6,false>"),            # IMIX, mean 362 B: stream before the parse
+    (3, "gpk::decode_kernel<true,false,true,false,6,6,16>"),  # 1500 B: the 80-VGPR 6-chunk kernel
+])
+def test_kernel_choice_by_mean_packet(gpu_ctx, synth_cfg, want):
+    """A parser without IPv6 (Ethernet, IPv4, TCP, Payload) takes the kernel
+    its batch's mean packet selects (GPK_MID_MAXMEAN = 256 B, big packets from
+    1 KiB); each gives the oracle's results on the same packets (tagged, IPv6
+    and UDP packets end in UnsupportedLayerType, as DecodeLayers does)."""
+    from gopacket_amd import synth
+    cfg = CONFIGS["eth_ip4_tcp_payload"]
+    data, off, cap = synth.host_batch(synth_cfg, 99, 40000)
+    dp = device_parser(cfg)
+    assert gpu_ctx.kernel_name(dp, data, off, cap, layouts=False) == want
+    dev = gpu_ctx.decode_host(dp, data, off, cap, layouts=False)
+    ref = oracle_parser(cfg).decode(data, off, cap, nthreads=8, layouts=False)
+    assert_same(dev, ref, "synth%d through %s" % (synth_cfg, want))
+
+
 def test_edge_sizes(gpu_ctx):
     """Empty packets, 1-byte packets, a jumbogram larger than 64 KiB and the
     snaplen maximum, at odd offsets."""
