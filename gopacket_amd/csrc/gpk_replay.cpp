@@ -908,12 +908,15 @@ extern "C" int gpk_replay_file(gpk_ctx* ctx, const gpk_parser* parser, const cha
       finished = true;
     }
   }
+  const double t_tail = now_s();
   while (good && !pl.inflight.empty()) good = pl.deliver_oldest();
+  const double t_delivered = now_s();
   for (auto& s : pl.slots)
     if (s.fill_pending) {
       s.fill.wait();
       s.fill_pending = false;
     }
+  const double t_fills = now_s();
   stats->packets = packet_index;
   {
     const std::string e = pl.settle();  // allocations the call did not reach
@@ -923,6 +926,9 @@ extern "C" int gpk_replay_file(gpk_ctx* ctx, const gpk_parser* parser, const cha
       rc = GPK_ENOMEM;
     }
   }
+  if (trace && trace[0] == '2')
+    fprintf(stderr, "gpk_replay tail: delivered %.2f ms, fills %.2f, settled %.2f (from the last launch)\n",
+            (t_delivered - t_tail) * 1e3, (t_fills - t_tail) * 1e3, (now_s() - t_tail) * 1e3);
   stats->alloc_wait_s = pl.alloc_wait_ns.load() * 1e-9;
   stats->wall_s = now_s() - t_start;
   if (trace && trace[0] == '1')
