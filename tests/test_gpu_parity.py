@@ -3,6 +3,7 @@ field, error argument, flow hash and layer layout must be identical.
 
 All packets are built here; nothing reads /root/reference at run time.
 """
+import struct
 import zlib
 
 import numpy as np
@@ -81,6 +82,52 @@ def test_kernel_choice_by_mean_packet(gpu_ctx, synth_cfg, want):
     dev = gpu_ctx.decode_host(dp, data, off, cap, layouts=False)
     ref = oracle_parser(cfg).decode(data, off, cap, nthreads=8, layouts=False)
     assert_same(dev, ref, "synth%d through %s" % (synth_cfg, want))
+
+
+def unsupported_type_packets():
+    """Packets whose decode ends at an EtherType or IPProtocol with no
+    registered decoder in some configs (ARP, LLDP, an unknown EtherType, ICMP,
+    GRE, ICMPv6, an unassigned protocol, IPv6 behind tags), each at several
+    payload lengths and behind 0, 1 and 2 VLAN tags."""
+    mac = b"\x02\x00\x00\x00\x00\x01\x02\x00\x00\x00\x00\x02"
+
+    def ip4(proto, payload):
+        h = struct.pack(">BBHHHBBH4s4s", 0x45, 0, 20 + len(payload), 7, 0, 64, proto, 0, b"\x0a\x00\x00\x01",
+                        b"\x0a\x00\x00\x02")
+        return h + payload
+
+    def ip6(nh, payload):
+        return struct.pack(">IHBB16s16s", 6 << 28, len(payload), nh, 64, b"\x20\x01" + b"\x00" * 13 + b"\x01",
+                           b"\x20\x01" + b"\x00" * 13 + b"\x02") + payload
+
+    bodies = []
+    for n in (1, 8, 28, 46):
+        pay = bytes(range(n))
+        bodies += [(0x0806, pay), (0x88CC, pay), (0x9999, pay), (0x0800, ip4(1, pay)), (0x0800, ip4(47, pay)),
+                   (0x0800, ip4(253, pay)), (0x0800, ip4(6, b"")), (0x86DD, ip6(58, pay)), (0x86DD, ip6(59, pay))]
+    out = []
+    for et, body in bodies:
+        for tags in (b"", struct.pack(">HH", 0x8100, 5), struct.pack(">HHHH", 0x88A8, 5, 0x8100, 6)):
+            if tags:
+                out.append(mac + tags[:2] + tags[2:] + struct.pack(">H", et) + body)
+            else:
+                out.append(mac + struct.pack(">H", et) + body)
+    return out
+
+
+@pytest.mark.parametrize("layouts", [False, True])
+@pytest.mark.parametrize("cfg_name", sorted(CONFIGS))
+def test_unsupported_types(gpu_ctx, cfg_name, layouts):
+    """DecodeLayers stops with UnsupportedLayerType (or without an error for
+    LayerTypeZero, or with IgnoreUnsupported) at a type no decoder handles
+    (layers_decoder.go:71-79): the lanes the fast path hands to the general
+    decoder there give the oracle's results, in every test parser."""
+    pk = unsupported_type_packets() * 3
+    dev, ref = run_both(gpu_ctx, CONFIGS[cfg_name], pk, layouts=layouts)
+    assert_same(dev, ref, "%s unsupported types (layouts=%s)" % (cfg_name, layouts))
+    if cfg_name == "eth_ip4_tcp_payload":
+        err = dev["records"]["status"] & 0x7F
+        assert len(np.unique(err)) >= 2
 
 
 def test_edge_sizes(gpu_ctx):
