@@ -1016,10 +1016,8 @@ struct PBat {
 
 }  // namespace
 
-extern "C" int gpk_tpacket_pump(gpk_ctx* ctx, const gpk_parser* parser, gpk_tpacket* t, const gpk_tp_pump_opts* o,
-                                gpk_tp_pump_cb cb, void* user, gpk_tp_pump_stats* st) {
-  if (!ctx || !parser || !t || !st) return GPK_EINVAL;
-  memset(st, 0, sizeof(*st));
+static int tpacket_pump(gpk_ctx* ctx, const gpk_parser* parser, gpk_tpacket* t, const gpk_tp_pump_opts* o,
+                        gpk_tp_pump_cb cb, void* user, gpk_tp_pump_stats* st) {
   gpk_tp_pump_opts opt{1ull << 20, 0, 0, 4};
   if (o) {
     if (o->batch_pkts) opt.batch_pkts = o->batch_pkts;
@@ -1268,4 +1266,21 @@ extern "C" int gpk_tpacket_pump(gpk_ctx* ctx, const gpk_parser* parser, gpk_tpac
     return GPK_EHIP;
   }
   return rc;
+}
+
+// The C entry point: no C++ exception crosses it (a thread or an allocation
+// the host cannot provide ends the call with an error).
+extern "C" int gpk_tpacket_pump(gpk_ctx* ctx, const gpk_parser* parser, gpk_tpacket* t, const gpk_tp_pump_opts* o,
+                                gpk_tp_pump_cb cb, void* user, gpk_tp_pump_stats* st) {
+  if (!ctx || !parser || !t || !st) return GPK_EINVAL;
+  memset(st, 0, sizeof(*st));
+  try {
+    return tpacket_pump(ctx, parser, t, o, cb, user, st);
+  } catch (const std::bad_alloc&) {
+    snprintf(st->error, sizeof(st->error), "out of host memory");
+    return GPK_ENOMEM;
+  } catch (const std::exception& e) {
+    snprintf(st->error, sizeof(st->error), "%s", e.what());
+    return GPK_EHIP;
+  }
 }

@@ -18,6 +18,7 @@
 #include <atomic>
 #include <mutex>
 #include <unordered_map>
+#include <system_error>
 #include <thread>
 #include <vector>
 #include <new>
@@ -870,7 +871,9 @@ hipError_t gpk_pin_alloc(void** out, size_t bytes) {
   *out = nullptr;
   if (bytes >= 2 * kHuge) {
     const size_t len = (bytes + kHuge - 1) & ~(kHuge - 1);
-    void* m = mmap(nullptr, len + kHuge, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
+    // (no MAP_NORESERVE: a request the host cannot back fails here, not as a
+    // fault while it is touched)
+    void* m = mmap(nullptr, len + kHuge, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
     if (m != MAP_FAILED) {
       // 2 MiB-aligned, so transparent huge pages can back all of it
       const uintptr_t a = ((uintptr_t)m + kHuge - 1) & ~(uintptr_t)(kHuge - 1);
@@ -889,7 +892,12 @@ hipError_t gpk_pin_alloc(void** out, size_t bytes) {
         for (size_t o = a; o < b; o += 4096) p[o] = 0;
       };
       std::vector<std::thread> th;
-      for (size_t t = 1; t < nt; t++) th.emplace_back(touch, t);
+      size_t t = 1;
+      try {
+        for (; t < nt; t++) th.emplace_back(touch, t);
+      } catch (const std::system_error&) {  // no thread to spare: the rest on this one
+        for (size_t u = t; u < nt; u++) touch(u);
+      }
       touch(0);
       for (auto& x : th) x.join();
       if (hipHostRegister(p, len, hipHostRegisterDefault) == hipSuccess) {

@@ -395,10 +395,8 @@ void free_cached(void* p) {
 
 }  // namespace
 
-extern "C" int gpk_replay_file(gpk_ctx* ctx, const gpk_parser* parser, const char* path, const gpk_replay_opts* o,
-                               gpk_replay_cb cb, void* user, gpk_replay_stats* stats) {
-  if (!ctx || !parser || !path || !stats) return GPK_EINVAL;
-  memset(stats, 0, sizeof(*stats));
+static int replay_file(gpk_ctx* ctx, const gpk_parser* parser, const char* path, const gpk_replay_opts* o,
+                       gpk_replay_cb cb, void* user, gpk_replay_stats* stats) {
   const double t_start = now_s();
   gpk_replay_opts opt{0, 0, 256ull << 20, 4, 1ull << 20, 8};
   if (o) {
@@ -945,4 +943,22 @@ extern "C" int gpk_replay_file(gpk_ctx* ctx, const gpk_parser* parser, const cha
   if (good)  // idle buffers for the next call
     gpk_ctx_replay_put(ctx, new Cached{C, R, P, dev_walk, std::move(pl.slots), std::move(pl.bats)}, free_cached);
   return rc;
+}
+
+// The C entry point: no C++ exception crosses it (a thread or an allocation
+// the host cannot provide ends the call with an error; the pipeline's
+// destructors have waited for its streams and threads by then).
+extern "C" int gpk_replay_file(gpk_ctx* ctx, const gpk_parser* parser, const char* path, const gpk_replay_opts* o,
+                               gpk_replay_cb cb, void* user, gpk_replay_stats* stats) {
+  if (!ctx || !parser || !path || !stats) return GPK_EINVAL;
+  memset(stats, 0, sizeof(*stats));
+  try {
+    return replay_file(ctx, parser, path, o, cb, user, stats);
+  } catch (const std::bad_alloc&) {
+    snprintf(stats->error, sizeof(stats->error), "out of host memory");
+    return GPK_ENOMEM;
+  } catch (const std::exception& e) {
+    snprintf(stats->error, sizeof(stats->error), "%s", e.what());
+    return GPK_EHIP;
+  }
 }
