@@ -157,15 +157,38 @@ __global__ __launch_bounds__(256) void probe_mixed_kernel(const uint8_t* data, u
 // bandwidth, mode 1 takes about mode 0 + the re-fetched share; if it is served
 // on chip (L2 / Infinity Cache), mode 1 takes about mode 0. mode 3: the
 // header windows, then a stream that skips the granules they hold (what a
-// phase B taking those granules from the LDS windows would fetch).
+// phase B taking those granules from the LDS windows would fetch). mode 4:
+// the block's four waves stream its 256-packet region together, wave w taking
+// the w-th KiB of every 4 KiB (the same bytes as mode 0 in 4 KiB passes per
+// block instead of 1 KiB passes per wave: a quarter as many concurrent streams).
 __global__ __launch_bounds__(256) void probe_reread_kernel(const uint8_t* data, uint64_t nbytes, uint32_t pkt,
                                                            int mode, uint32_t* out) {
   typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
   const uint32_t lane = threadIdx.x & 63;
   const uint64_t wave = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const uint64_t R = 64ull * pkt, base = wave * R;
-  if (base + R > nbytes) return;
   uint32_t acc = 0;
+  if (mode == 4) {
+    const uint64_t bb = (uint64_t)blockIdx.x * 4 * R;
+    if (bb + 4 * R > nbytes) return;
+    const u32x4* v = reinterpret_cast<const u32x4*>(data + bb);
+    const uint32_t nv = (uint32_t)(4 * R / 16);
+    uint32_t k = threadIdx.x;  // wave w's lanes: vectors 64 w .. 64 w + 63 of each 256
+    for (; k + 7 * 256 < nv; k += 8 * 256) {
+      u32x4 a[8];
+#pragma unroll
+      for (int j = 0; j < 8; j++) a[j] = __builtin_nontemporal_load(v + k + 256 * j);
+#pragma unroll
+      for (int j = 0; j < 8; j++) acc = __builtin_amdgcn_udot4(a[j].x ^ a[j].y ^ a[j].z ^ a[j].w, 0x01010101u, acc, false);
+    }
+    for (; k < nv; k += 256) {
+      const u32x4 a = __builtin_nontemporal_load(v + k);
+      acc = __builtin_amdgcn_udot4(a.x ^ a.y ^ a.z ^ a.w, 0x01010101u, acc, false);
+    }
+    if (acc == 0x9e3779b9u) out[0] = acc;
+    return;
+  }
+  if (base + R > nbytes) return;
   if (mode >= 1) {  // 1, 2, 3
     const uint8_t* h = data + ((base + (uint64_t)lane * pkt) & ~15ull);
     u32x4 w[6];
@@ -451,6 +474,18 @@ int gpk_probe_reread(const uint8_t* data, uint64_t nbytes, uint32_t pkt, int mod
   if (!pkt || !blocks) return -1;
   hipLaunchKernelGGL(probe_reread_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, data, nbytes, pkt,
                      mode, out);
+  return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+// The same with `lds` bytes of (unused) dynamic LDS per block: caps the
+// blocks a CU holds at once (160 KiB / lds), the occupancy sweep of
+// tools/stream_shape_probe.py --occ.
+int gpk_probe_reread_lds(const uint8_t* data, uint64_t nbytes, uint32_t pkt, int mode, uint32_t lds, uint32_t* out,
+                         void* stream) {
+  const uint64_t waves = nbytes / (64ull * pkt), blocks = (waves + 3) / 4;
+  if (!pkt || !blocks || lds > 160u * 1024u) return -1;
+  hipLaunchKernelGGL(probe_reread_kernel, dim3((unsigned)blocks), dim3(256), lds, (hipStream_t)stream, data, nbytes,
+                     pkt, mode, out);
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
