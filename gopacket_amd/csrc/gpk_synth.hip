@@ -233,7 +233,165 @@ __global__ __launch_bounds__(256) void probe_reread_kernel(const uint8_t* data, 
   if (acc == 0x9e3779b9u) out[0] = acc;  // keep the loads live; practically never stores
 }
 
+// Skeleton probe (DESIGN.md §5, C3's gap to its stream shape): the decode
+// kernel's memory accesses per wave without its work, one wave per 64
+// packets of pkt bytes. flags: 1 = first each lane's 12-byte index entry
+// (offset + caplen, from idx[], the window addresses depend on it); 2 = its
+// 6-chunk header window at the packet (temporal) into LDS; 4 = after the
+// stream, the 16-byte record and three 8-byte flow hashes per lane
+// (non-temporal, into wbuf); 8 = those stores with the default policy;
+// 16 = the block's waves store together after a barrier. The stream itself:
+// mode 0 of probe_reread.
+__global__ __launch_bounds__(256) void probe_skeleton_kernel(const uint8_t* data, uint64_t nbytes, uint32_t pkt,
+                                                             const uint32_t* idx, uint8_t* wbuf, int flags,
+                                                             uint32_t* out) {
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+  __shared__ u32x4 win[256 * 6];
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t wave = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const uint64_t R = 64ull * pkt, base = wave * R;
+  if (base + R > nbytes) return;
+  const uint64_t pk = wave * 64 + lane;
+  uint32_t acc = 0;
+  uint64_t dep = 0;
+  if (flags & 1) {  // the index entry: 8-byte offset + 4-byte caplen, as two coalesced loads
+    const u32x2 o = *reinterpret_cast<const u32x2*>(idx + 2 * pk);
+    const uint32_t c = idx[2 * (nbytes / pkt) + pk];
+    dep = (uint64_t)((o.x ^ o.y ^ c) & 0u);  // zero, but the window addresses wait for it
+    acc += o.x + c;
+  }
+  if (flags & 2) {
+    const uint8_t* h = data + ((base + (uint64_t)lane * pkt + dep) & ~15ull);
+    u32x4 w[6];
+#pragma unroll
+    for (int k = 0; k < 6; k++) w[k] = *reinterpret_cast<const u32x4*>(h + 16 * k);
+#pragma unroll
+    for (int k = 0; k < 6; k++) win[threadIdx.x * 6 + k] = w[k];
+    __syncthreads();
+    const u32x4 x = win[((threadIdx.x + 1) & 255) * 6 + (lane & 3)];
+    acc = __builtin_amdgcn_udot4(x.x ^ x.y ^ x.z ^ x.w, 0x01010101u, acc, false);
+  }
+  const u32x4* v = reinterpret_cast<const u32x4*>(data + base + dep);
+  const uint32_t nv = (uint32_t)(R / 16);
+  uint32_t k = lane;
+  for (; k + 7 * 64 < nv; k += 8 * 64) {
+    u32x4 a[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) a[j] = __builtin_nontemporal_load(v + k + 64 * j);
+#pragma unroll
+    for (int j = 0; j < 8; j++) acc = __builtin_amdgcn_udot4(a[j].x ^ a[j].y ^ a[j].z ^ a[j].w, 0x01010101u, acc, false);
+  }
+  for (; k < nv; k += 64) {
+    const u32x4 a = __builtin_nontemporal_load(v + k);
+    acc = __builtin_amdgcn_udot4(a.x ^ a.y ^ a.z ^ a.w, 0x01010101u, acc, false);
+  }
+  if (flags & 4) {
+    const uint64_t n = nbytes / pkt;
+    if (flags & 16) __syncthreads();  // the block's four waves store together (4 KiB of records at once)
+    u32x4* r = reinterpret_cast<u32x4*>(wbuf) + pk;
+    uint64_t* f = reinterpret_cast<uint64_t*>(wbuf + 16 * n);
+    if (flags & 8) {  // default (temporal) policy: the stores go through L2
+      *r = u32x4{acc, lane, 0u, 1u};
+#pragma unroll
+      for (int j = 0; j < 3; j++) f[j * n + pk] = (uint64_t)acc * (j + 1);
+    } else {
+      __builtin_nontemporal_store(u32x4{acc, lane, 0u, 1u}, r);
+#pragma unroll
+      for (int j = 0; j < 3; j++) __builtin_nontemporal_store((uint64_t)acc * (j + 1), f + j * n + pk);
+    }
+  } else if (acc == 0x9e3779b9u) {
+    out[0] = acc;
+  }
+}
+
+// The skeleton of any packed batch (offsets / caplens as the decode takes
+// them): per wave of 64 packets, the index entries; the header windows
+// (flags & 2: 6 chunks at each packet's 16-byte-aligned start, temporal);
+// unless flags & 64, the stream over the wave's extent (first packet's chunk to last packet's
+// end, 1 KiB passes, 8 in flight, non-temporal); then wbytes bytes per packet
+// written (16: record; 40: record + flows; 168: + layer fields), non-temporal.
+__global__ __launch_bounds__(256) void probe_skeleton_idx_kernel(const uint8_t* data, const uint64_t* offsets,
+                                                                 const uint32_t* caplens, uint64_t n, uint8_t* wbuf,
+                                                                 uint32_t wbytes, int flags, uint32_t* out) {
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  __shared__ u32x4 win[256 * 6];
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t w0 = ((uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 64;
+  if (w0 >= n) return;
+  const uint64_t i = w0 + lane < n ? w0 + lane : n - 1;
+  const uint64_t o = offsets[i];
+  const uint32_t c = caplens[i];
+  uint32_t acc = c;
+  if (flags & 2) {
+    const uint8_t* h = data + (o & ~15ull);
+    u32x4 w[6];
+#pragma unroll
+    for (int k = 0; k < 6; k++) w[k] = *reinterpret_cast<const u32x4*>(h + 16 * k);
+#pragma unroll
+    for (int k = 0; k < 6; k++) win[threadIdx.x * 6 + k] = w[k];
+    __syncthreads();
+    const u32x4 x = win[((threadIdx.x + 1) & 255) * 6 + (lane & 3)];
+    acc = __builtin_amdgcn_udot4(x.x ^ x.y ^ x.z ^ x.w, 0x01010101u, acc, false);
+  }
+  const uint64_t lo = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)o) |
+                      (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(o >> 32)) << 32;
+  const uint64_t e = o + c;
+  const uint64_t hi = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)e, 63) |
+                      (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(e >> 32), 63) << 32;
+  const uint64_t b = lo & ~15ull;
+  const uint32_t nv = (flags & 64) || hi <= b ? 0u : (uint32_t)((hi - b + 15) / 16);  // 64: windows only
+  const u32x4* v = reinterpret_cast<const u32x4*>(data + b);
+  uint32_t k = lane;
+  for (; k + 7 * 64 < nv; k += 8 * 64) {
+    u32x4 a[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) a[j] = __builtin_nontemporal_load(v + k + 64 * j);
+#pragma unroll
+    for (int j = 0; j < 8; j++) acc = __builtin_amdgcn_udot4(a[j].x ^ a[j].y ^ a[j].z ^ a[j].w, 0x01010101u, acc, false);
+  }
+  for (; k < nv; k += 64) {
+    const u32x4 a = __builtin_nontemporal_load(v + k);
+    acc = __builtin_amdgcn_udot4(a.x ^ a.y ^ a.z ^ a.w, 0x01010101u, acc, false);
+  }
+  if (w0 + lane < n) {
+    uint8_t* r = wbuf + (w0 + lane) * 16;
+    if (wbytes >= 16) __builtin_nontemporal_store(u32x4{acc, lane, 0u, 1u}, reinterpret_cast<u32x4*>(r));
+    if (wbytes >= 40) {
+      uint64_t* f = reinterpret_cast<uint64_t*>(wbuf + 16 * n);
+#pragma unroll
+      for (int j = 0; j < 3; j++) __builtin_nontemporal_store((uint64_t)acc * (j + 1), f + j * n + w0 + lane);
+    }
+    if (wbytes >= 168) {  // the wave's 64 128-byte records as eight coalesced 1 KiB runs (as the fused kernel stores)
+      u32x4* fl = reinterpret_cast<u32x4*>(wbuf + 40 * n) + w0 * 8;
+#pragma unroll
+      for (int j = 0; j < 8; j++) __builtin_nontemporal_store(u32x4{acc, (uint32_t)j, lane, 0u}, fl + 64 * j + lane);
+    }
+  }
+  if (acc == 0x9e3779b9u) out[0] = acc;
+}
+
 extern "C" {
+
+int gpk_probe_skeleton_idx(const uint8_t* data, const uint64_t* offsets, const uint32_t* caplens, uint64_t n,
+                           uint8_t* wbuf, uint32_t wbytes, int flags, uint32_t* out, void* stream) {
+  const uint64_t blocks = (n + 255) / 256;
+  if (!n || blocks > 0xffffffffull) return -1;
+  hipLaunchKernelGGL(probe_skeleton_idx_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, data,
+                     offsets, caplens, n, wbuf, wbytes, flags, out);
+  return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+// Launch the skeleton probe: idx holds 3 dwords per packet (nbytes / pkt
+// packets: offsets as 2 dwords, then caplens), wbuf 40 bytes per packet.
+int gpk_probe_skeleton(const uint8_t* data, uint64_t nbytes, uint32_t pkt, const uint32_t* idx, uint8_t* wbuf, int flags,
+                       uint32_t* out, void* stream) {
+  const uint64_t waves = nbytes / (64ull * pkt), blocks = (waves + 3) / 4;
+  if (!pkt || !blocks) return -1;
+  hipLaunchKernelGGL(probe_skeleton_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, data, nbytes,
+                     pkt, idx, wbuf, flags, out);
+  return hipGetLastError() == hipSuccess ? 0 : -3;
+}
 
 uint32_t gpk_synth_len(int cfg, uint64_t i) { return frame_len(cfg, i); }
 
