@@ -180,6 +180,7 @@ def run_config(name, n, steps, warmup, rank, world, ctx, check_sample=2048, prob
     wall_max = shard.max_over_ranks(wall, world, device="cuda")
 
     probe_gbs = probe_read(data, payload_bytes, steps, stream) if probe else None
+    skel_ms = skeleton_ms(cfg, data, off, cap, n, steps, stream) if probe and not strong else None
     parity = None
     if check_sample:
         parity = sample_parity(name, cfg, rec, fl, err, first, n, check_sample)
@@ -188,11 +189,44 @@ def run_config(name, n, steps, warmup, rank, world, ctx, check_sample=2048, prob
         full, full_s = full_parity(name, cfg, data, off, cap, rec, fl, err, n, host_cores()[0])
         full = dict(result=full, seconds=round(full_s, 2))
     res = dict(full_parity=full, n=n, payload_bytes=payload_bytes, wall_s=wall_max, kernel_ms=kernel_ms,
-               algo_bytes=payload_bytes + INDEX_BYTES * n, parity=parity, probe_gbs=probe_gbs, strong=strong,
+               algo_bytes=payload_bytes + INDEX_BYTES * n, parity=parity, probe_gbs=probe_gbs, skeleton_ms=skel_ms,
+               strong=strong,
                kernel=kernel, blocks_per_cu=blocks_per_cu)
     del data, off, cap, rec, err, fl
     torch.cuda.empty_cache()
     return res
+
+
+# Bytes a decode writes per packet, and whether it streams the packet bytes
+# (an L4 checksum), for its memory skeleton (tools/skeleton_all.py)
+def skeleton_shape(cfg):
+    return (16 + (24 if cfg["outputs"] & 4 else 0)), bool(cfg["outputs"] & 2)
+
+
+def skeleton_ms(cfg, data, off, cap, n, steps, stream):
+    """The decode's memory skeleton on the same batch (gpk_probe_skeleton_idx:
+    index, header windows, the wave's stream, the bytes the decode writes;
+    none of its work), timed like the decode."""
+    import torch
+    from gopacket_amd import _lib
+    S = _lib.synth_lib()
+    wbytes, streamed = skeleton_shape(cfg)
+    wbuf = torch.empty(wbytes * n, dtype=torch.uint8, device="cuda")
+    sink = torch.zeros(1, dtype=torch.int32, device="cuda")
+
+    def go():
+        assert S.gpk_probe_skeleton_idx(data.data_ptr(), off.data_ptr(), cap.data_ptr(), n, wbuf.data_ptr(), wbytes,
+                                        2 | (0 if streamed else 64), sink.data_ptr(), stream.cuda_stream) == 0
+
+    go()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(steps):
+        go()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    del wbuf
+    return e0.elapsed_time(e1) / steps
 
 
 def pcap_packets(path):
@@ -999,7 +1033,9 @@ def main():
                          "blocks_per_cu": r["blocks_per_cu"],
                          "traffic_unit": "bytes per launch", "kernel_ms": round(r["kernel_ms"], 4),
                          "algo_bytes_per_launch": r["algo_bytes"],
-                         "probe_read_GBps": r["probe_gbs"] and round(r["probe_gbs"], 1)},
+                         "probe_read_GBps": r["probe_gbs"] and round(r["probe_gbs"], 1),
+                         "skeleton_ms": r["skeleton_ms"] and round(r["skeleton_ms"], 4),
+                         "of_skeleton": r["skeleton_ms"] and round(r["skeleton_ms"] / r["kernel_ms"], 4)},
             "parity": r["parity"],
             "full_parity": r["full_parity"],
             "dist_backend": dist.get_backend() if dist.is_initialized() else None,
@@ -1014,7 +1050,9 @@ def main():
                    "value": round(pk * args.steps / s["wall_s"] / 1e6, 2), "unit": "Mpkts/s",
                    "kernel": s["kernel"], "blocks_per_cu": s["blocks_per_cu"], "kernel_ms": round(s["kernel_ms"], 4), "achieved_GBps": round(ach, 1),
                    "frac": round(ach / HBM_PEAK_GBS, 4), "parity": s["parity"], "full_parity": s["full_parity"],
-                   "probe_read_GBps": s["probe_gbs"] and round(s["probe_gbs"], 1)}
+                   "probe_read_GBps": s["probe_gbs"] and round(s["probe_gbs"], 1),
+                   "skeleton_ms": s["skeleton_ms"] and round(s["skeleton_ms"], 4),
+                   "of_skeleton": s["skeleton_ms"] and round(s["skeleton_ms"] / s["kernel_ms"], 4)}
             if st:
                 row.update(scaling="strong", total_packets=st["total_packets"], byte_balance=st["balance"],
                            note="one batch split at byte-balanced cuts; kernel_ms/achieved are rank 0's shard")
