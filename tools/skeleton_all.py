@@ -30,6 +30,7 @@ def main():
     ap.add_argument("--configs", default="c3,c4,c4f,c2,c1")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--no-write", action="store_true", help="also time the skeleton without its writes")
     a = ap.parse_args()
     import torch
     import bench
@@ -65,7 +66,13 @@ def main():
             else:
                 ctx.decode_device(parser, data, off, cap, rec, err, fl, stream=stream)
 
+        def skeleton_nowrite():
+            assert S.gpk_probe_skeleton_idx(data.data_ptr(), off.data_ptr(), cap.data_ptr(), n, wbuf.data_ptr(), 0,
+                                            flags, sink.data_ptr(), stream.cuda_stream) == 0
+
         runs = {"skeleton": skeleton, "decode": decode}
+        if a.no_write:
+            runs["skeleton_no_writes"] = skeleton_nowrite
         times = {k: [] for k in runs}
         for rnd in range(a.rounds + 1):
             for k, f in runs.items():
@@ -82,7 +89,9 @@ def main():
         print(json.dumps({"config": name, "packets": n, "written_bytes_per_packet": wbytes, "streamed": streamed,
                           "skeleton_ms": round(sk, 4), "decode_ms": round(de, 4),
                           "decode_algorithmic_GBps": round(algo / (de * 1e-3) / 1e9, 1),
-                          "decode_over_skeleton_rate": round(sk / de, 4)}), flush=True)
+                          "decode_over_skeleton_rate": round(sk / de, 4),
+                          "skeleton_no_writes_ms": round(float(np.median(times["skeleton_no_writes"])), 4)
+                          if a.no_write else None}), flush=True)
         del data, off, cap, wbuf, rec, err, fl, fld
         torch.cuda.empty_cache()
 
