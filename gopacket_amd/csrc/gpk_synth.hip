@@ -310,7 +310,8 @@ __global__ __launch_bounds__(256) void probe_skeleton_kernel(const uint8_t* data
 // (flags & 2: 6 chunks at each packet's 16-byte-aligned start, temporal);
 // unless flags & 64, the stream over the wave's extent (first packet's chunk to last packet's
 // end, 1 KiB passes, 8 in flight, non-temporal); then wbytes bytes per packet
-// written (16: record; 40: record + flows; 168: + layer fields), non-temporal.
+// written (16: record; 40: record + flows; 168: + layer fields), non-temporal
+// (flags & 8: default policy; flags & 16: the block's waves store together).
 __global__ __launch_bounds__(256) void probe_skeleton_idx_kernel(const uint8_t* data, const uint64_t* offsets,
                                                                  const uint32_t* caplens, uint64_t n, uint8_t* wbuf,
                                                                  uint32_t wbytes, int flags, uint32_t* out) {
@@ -354,13 +355,20 @@ __global__ __launch_bounds__(256) void probe_skeleton_idx_kernel(const uint8_t* 
     const u32x4 a = __builtin_nontemporal_load(v + k);
     acc = __builtin_amdgcn_udot4(a.x ^ a.y ^ a.z ^ a.w, 0x01010101u, acc, false);
   }
+  if (flags & 16) __syncthreads();  // the block's four waves store together
   if (w0 + lane < n) {
     uint8_t* r = wbuf + (w0 + lane) * 16;
-    if (wbytes >= 16) __builtin_nontemporal_store(u32x4{acc, lane, 0u, 1u}, reinterpret_cast<u32x4*>(r));
-    if (wbytes >= 40) {
-      uint64_t* f = reinterpret_cast<uint64_t*>(wbuf + 16 * n);
+    uint64_t* f = reinterpret_cast<uint64_t*>(wbuf + 16 * n);
+    if (flags & 8) {  // default (temporal) store policy
+      if (wbytes >= 16) *reinterpret_cast<u32x4*>(r) = u32x4{acc, lane, 0u, 1u};
+      if (wbytes >= 40)
 #pragma unroll
-      for (int j = 0; j < 3; j++) __builtin_nontemporal_store((uint64_t)acc * (j + 1), f + j * n + w0 + lane);
+        for (int j = 0; j < 3; j++) f[j * n + w0 + lane] = (uint64_t)acc * (j + 1);
+    } else {
+      if (wbytes >= 16) __builtin_nontemporal_store(u32x4{acc, lane, 0u, 1u}, reinterpret_cast<u32x4*>(r));
+      if (wbytes >= 40)
+#pragma unroll
+        for (int j = 0; j < 3; j++) __builtin_nontemporal_store((uint64_t)acc * (j + 1), f + j * n + w0 + lane);
     }
     if (wbytes >= 168) {  // the wave's 64 128-byte records as eight coalesced 1 KiB runs (as the fused kernel stores)
       u32x4* fl = reinterpret_cast<u32x4*>(wbuf + 40 * n) + w0 * 8;

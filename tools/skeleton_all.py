@@ -31,6 +31,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--no-write", action="store_true", help="also time the skeleton without its writes")
+    ap.add_argument("--write-forms", action="store_true",
+                    help="also time the skeleton with default-policy stores, and with block-synchronous stores")
     a = ap.parse_args()
     import torch
     import bench
@@ -70,9 +72,16 @@ def main():
             assert S.gpk_probe_skeleton_idx(data.data_ptr(), off.data_ptr(), cap.data_ptr(), n, wbuf.data_ptr(), 0,
                                             flags, sink.data_ptr(), stream.cuda_stream) == 0
 
+        def skeleton_flags(extra):
+            return lambda: S.gpk_probe_skeleton_idx(data.data_ptr(), off.data_ptr(), cap.data_ptr(), n, wbuf.data_ptr(),
+                                                    wbytes, flags | extra, sink.data_ptr(), stream.cuda_stream)
+
         runs = {"skeleton": skeleton, "decode": decode}
         if a.no_write:
             runs["skeleton_no_writes"] = skeleton_nowrite
+        if a.write_forms:
+            runs["skeleton_temporal_writes"] = skeleton_flags(8)
+            runs["skeleton_block_writes"] = skeleton_flags(16)
         times = {k: [] for k in runs}
         for rnd in range(a.rounds + 1):
             for k, f in runs.items():
@@ -90,8 +99,8 @@ def main():
                           "skeleton_ms": round(sk, 4), "decode_ms": round(de, 4),
                           "decode_algorithmic_GBps": round(algo / (de * 1e-3) / 1e9, 1),
                           "decode_over_skeleton_rate": round(sk / de, 4),
-                          "skeleton_no_writes_ms": round(float(np.median(times["skeleton_no_writes"])), 4)
-                          if a.no_write else None}), flush=True)
+                          **{k + "_ms": round(float(np.median(v)), 4) for k, v in times.items()
+                             if k not in ("skeleton", "decode")}}), flush=True)
         del data, off, cap, wbuf, rec, err, fl, fld
         torch.cuda.empty_cache()
 
