@@ -311,7 +311,8 @@ __global__ __launch_bounds__(256) void probe_skeleton_kernel(const uint8_t* data
 // unless flags & 64, the stream over the wave's extent (first packet's chunk to last packet's
 // end, 1 KiB passes, 8 in flight, non-temporal); then wbytes bytes per packet
 // written (16: record; 40: record + flows; 168: + layer fields), non-temporal
-// (flags & 8: default policy; flags & 16: the block's waves store together).
+// (flags & 8: default policy; flags & 16: the block's waves store together;
+// flags & 32: before the stream instead of after it).
 __global__ __launch_bounds__(256) void probe_skeleton_idx_kernel(const uint8_t* data, const uint64_t* offsets,
                                                                  const uint32_t* caplens, uint64_t n, uint8_t* wbuf,
                                                                  uint32_t wbytes, int flags, uint32_t* out) {
@@ -335,6 +336,63 @@ __global__ __launch_bounds__(256) void probe_skeleton_idx_kernel(const uint8_t* 
     const u32x4 x = win[((threadIdx.x + 1) & 255) * 6 + (lane & 3)];
     acc = __builtin_amdgcn_udot4(x.x ^ x.y ^ x.z ^ x.w, 0x01010101u, acc, false);
   }
+  auto store_out = [&]() {
+    if (flags & 16) __syncthreads();  // the block's four waves store together
+    if (w0 + lane < n) {
+      // flags & 128: the outputs of packet i at i mod 2^20 (a 40 MiB ring that stays on chip) instead of i
+      const uint64_t q = (flags & 128) ? ((w0 + lane) & ((1u << 20) - 1)) : w0 + lane;
+      uint8_t* r = wbuf + q * 16;
+      uint64_t* f = reinterpret_cast<uint64_t*>(wbuf + 16 * n) + (q - (w0 + lane));
+      if (flags & 8) {  // default (temporal) store policy
+        if (wbytes >= 16) *reinterpret_cast<u32x4*>(r) = u32x4{acc, lane, 0u, 1u};
+        if (wbytes >= 40)
+#pragma unroll
+          for (int j = 0; j < 3; j++) f[j * n + w0 + lane] = (uint64_t)acc * (j + 1);
+      } else {
+        if (wbytes >= 16) __builtin_nontemporal_store(u32x4{acc, lane, 0u, 1u}, reinterpret_cast<u32x4*>(r));
+        if (wbytes >= 40)
+#pragma unroll
+          for (int j = 0; j < 3; j++) __builtin_nontemporal_store((uint64_t)acc * (j + 1), f + j * n + w0 + lane);
+      }
+      if (wbytes >= 168) {  // the wave's 64 128-byte records as eight coalesced 1 KiB runs (as the fused kernel stores)
+        u32x4* fl = reinterpret_cast<u32x4*>(wbuf + 40 * n) + w0 * 8;
+#pragma unroll
+        for (int j = 0; j < 8; j++) __builtin_nontemporal_store(u32x4{acc, (uint32_t)j, lane, 0u}, fl + 64 * j + lane);
+      }
+    }
+  };
+  if (flags & 32) store_out();  // the outputs before the stream (their values are whatever acc holds then)
+  // flags & 256: the block's outputs through LDS, stored by its first wave alone
+  auto store_by_wave0 = [&]() {  // (records only when wbytes < 40; no fields)
+    __syncthreads();  // every wave is past its window reads
+    uint32_t* l = reinterpret_cast<uint32_t*>(win);
+    const uint32_t t = threadIdx.x;
+    l[4 * t + 0] = acc;
+    l[4 * t + 1] = lane;
+    l[4 * t + 2] = 0u;
+    l[4 * t + 3] = 1u;
+    uint64_t* lf = reinterpret_cast<uint64_t*>(l + 1024);
+#pragma unroll
+    for (int j = 0; j < 3; j++) lf[256 * j + t] = (uint64_t)acc * (j + 1);
+    __syncthreads();
+    if (threadIdx.x < 64) {
+      const uint64_t b0 = (uint64_t)blockIdx.x * 256;
+      u32x4* r = reinterpret_cast<u32x4*>(wbuf) + b0;
+#pragma unroll
+      for (int k = 0; k < 4; k++)
+        if (b0 + 64 * k + lane < n)
+          __builtin_nontemporal_store(reinterpret_cast<const u32x4*>(l)[64 * k + lane], r + 64 * k + lane);
+      if (wbytes >= 40) {  // the flows only where the buffer has them
+        uint64_t* f = reinterpret_cast<uint64_t*>(wbuf + 16 * n) + b0;
+#pragma unroll
+        for (int j = 0; j < 3; j++)
+#pragma unroll
+          for (int k = 0; k < 4; k++)
+            if (b0 + 64 * k + lane < n)
+              __builtin_nontemporal_store(lf[256 * j + 64 * k + lane], f + j * n + 64 * k + lane);
+      }
+    }
+  };
   const uint64_t lo = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)o) |
                       (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(o >> 32)) << 32;
   const uint64_t e = o + c;
@@ -355,27 +413,8 @@ __global__ __launch_bounds__(256) void probe_skeleton_idx_kernel(const uint8_t* 
     const u32x4 a = __builtin_nontemporal_load(v + k);
     acc = __builtin_amdgcn_udot4(a.x ^ a.y ^ a.z ^ a.w, 0x01010101u, acc, false);
   }
-  if (flags & 16) __syncthreads();  // the block's four waves store together
-  if (w0 + lane < n) {
-    uint8_t* r = wbuf + (w0 + lane) * 16;
-    uint64_t* f = reinterpret_cast<uint64_t*>(wbuf + 16 * n);
-    if (flags & 8) {  // default (temporal) store policy
-      if (wbytes >= 16) *reinterpret_cast<u32x4*>(r) = u32x4{acc, lane, 0u, 1u};
-      if (wbytes >= 40)
-#pragma unroll
-        for (int j = 0; j < 3; j++) f[j * n + w0 + lane] = (uint64_t)acc * (j + 1);
-    } else {
-      if (wbytes >= 16) __builtin_nontemporal_store(u32x4{acc, lane, 0u, 1u}, reinterpret_cast<u32x4*>(r));
-      if (wbytes >= 40)
-#pragma unroll
-        for (int j = 0; j < 3; j++) __builtin_nontemporal_store((uint64_t)acc * (j + 1), f + j * n + w0 + lane);
-    }
-    if (wbytes >= 168) {  // the wave's 64 128-byte records as eight coalesced 1 KiB runs (as the fused kernel stores)
-      u32x4* fl = reinterpret_cast<u32x4*>(wbuf + 40 * n) + w0 * 8;
-#pragma unroll
-      for (int j = 0; j < 8; j++) __builtin_nontemporal_store(u32x4{acc, (uint32_t)j, lane, 0u}, fl + 64 * j + lane);
-    }
-  }
+  if (flags & 256) store_by_wave0();
+  else if (!(flags & 32)) store_out();
   if (acc == 0x9e3779b9u) out[0] = acc;
 }
 

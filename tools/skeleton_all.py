@@ -82,6 +82,9 @@ def main():
         if a.write_forms:
             runs["skeleton_temporal_writes"] = skeleton_flags(8)
             runs["skeleton_block_writes"] = skeleton_flags(16)
+            runs["skeleton_writes_first"] = skeleton_flags(32)
+            runs["skeleton_writes_ring"] = skeleton_flags(128)
+            runs["skeleton_writes_by_wave0"] = skeleton_flags(256)
         times = {k: [] for k in runs}
         for rnd in range(a.rounds + 1):
             for k, f in runs.items():
