@@ -1,0 +1,55 @@
+#!/usr/bin/env python3
+"""A wider fuzz sweep than tests/test_gpu_parity.py::test_fuzz: many seeds,
+every test parser, with and without layouts, packed at several alignments, and
+on every third seed the layer fields through both forms (layouts + extraction,
+and the fused launch; tests/test_fields_gpu.check). Each batch is
+compared with the oracle bit for bit (tests/configs.assert_same); the first
+mismatch is printed with its seed and the run stops.
+
+    python tools/fuzz_sweep.py [--seeds 20] [--packets 30000]
+"""
+import argparse
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--seeds", type=int, default=20)
+    ap.add_argument("--first-seed", type=int, default=5000)
+    ap.add_argument("--packets", type=int, default=30000)
+    a = ap.parse_args()
+    import torch  # noqa: F401  (libgpk runs on torch's HIP runtime)
+    import pktutil
+    from configs import CONFIGS, assert_same, device_parser, oracle_parser
+    from test_fields_gpu import check as fields_check
+    from gopacket_amd import engine
+    ctx = engine.Context()
+    t0 = time.time()
+    n_batches = 0
+    for seed in range(a.first_seed, a.first_seed + a.seeds):
+        packets = pktutil.fuzz_packets(seed, a.packets)
+        align = (1, 2, 4, 16)[seed % 4]
+        data, off, cap = pktutil.pack(packets, align=align, pad=(seed * 7) % 24)
+        for name in sorted(CONFIGS):
+            cfg = CONFIGS[name]
+            for layouts in (True, False):
+                dev = ctx.decode_host(device_parser(cfg), data, off, cap, layouts=layouts)
+                ref = oracle_parser(cfg).decode(data, off, cap, nthreads=8, layouts=layouts)
+                assert_same(dev, ref, "seed %d align %d %s layouts=%s" % (seed, align, name, layouts))
+                n_batches += 1
+            if seed % 3 == 0:
+                fields_check(ctx, name, packets, align=align)
+                n_batches += 2
+        print("seed %d (align %d): %d parsers x 2 bit-exact, %.0f s" % (seed, align, len(CONFIGS), time.time() - t0),
+              flush=True)
+    print("fuzz sweep: %d batches of %d packets, all bit-exact" % (n_batches, a.packets), flush=True)
+
+
+if __name__ == "__main__":
+    main()
