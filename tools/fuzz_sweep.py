@@ -23,11 +23,14 @@ def main():
     ap.add_argument("--seeds", type=int, default=20)
     ap.add_argument("--first-seed", type=int, default=5000)
     ap.add_argument("--packets", type=int, default=30000)
+    ap.add_argument("--layouts", default="", type=lambda x: [y for y in x.split(",") if y],
+                    help="placements to cycle through: packed, shuffled, reversed, wave_shuffled, gapped, sparse_mix")
     a = ap.parse_args()
     import torch  # noqa: F401  (libgpk runs on torch's HIP runtime)
     import pktutil
     from configs import CONFIGS, assert_same, device_parser, oracle_parser
     from test_fields_gpu import check as fields_check
+    from test_gpu_parity import phase_b_layout
     from gopacket_amd import engine
     ctx = engine.Context()
     t0 = time.time()
@@ -35,18 +38,23 @@ def main():
     for seed in range(a.first_seed, a.first_seed + a.seeds):
         packets = pktutil.fuzz_packets(seed, a.packets)
         align = (1, 2, 4, 16)[seed % 4]
-        data, off, cap = pktutil.pack(packets, align=align, pad=(seed * 7) % 24)
+        layout = a.layouts[seed % len(a.layouts)] if a.layouts else "packed"
+        if layout == "packed":
+            data, off, cap = pktutil.pack(packets, align=align, pad=(seed * 7) % 24)
+        else:  # the parity suite's unordered / gapped / sparse placements
+            data, off, cap = phase_b_layout(packets, layout)
         for name in sorted(CONFIGS):
             cfg = CONFIGS[name]
             for layouts in (True, False):
                 dev = ctx.decode_host(device_parser(cfg), data, off, cap, layouts=layouts)
                 ref = oracle_parser(cfg).decode(data, off, cap, nthreads=8, layouts=layouts)
-                assert_same(dev, ref, "seed %d align %d %s layouts=%s" % (seed, align, name, layouts))
+                assert_same(dev, ref, "seed %d align %d %s %s layouts=%s" % (seed, align, layout, name, layouts))
                 n_batches += 1
-            if seed % 3 == 0:
+            if seed % 3 == 0 and layout == "packed":
                 fields_check(ctx, name, packets, align=align)
                 n_batches += 2
-        print("seed %d (align %d): %d parsers x 2 bit-exact, %.0f s" % (seed, align, len(CONFIGS), time.time() - t0),
+        print("seed %d (%s, align %d): %d parsers x 2 bit-exact, %.0f s" % (seed, layout, align, len(CONFIGS),
+                                                                          time.time() - t0),
               flush=True)
     print("fuzz sweep: %d batches of %d packets, all bit-exact" % (n_batches, a.packets), flush=True)
 
