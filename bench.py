@@ -203,14 +203,15 @@ def skeleton_shape(cfg):
     return (16 + (24 if cfg["outputs"] & 4 else 0)), bool(cfg["outputs"] & 2)
 
 
-def skeleton_ms(cfg, data, off, cap, n, steps, stream):
+def skeleton_ms(cfg, data, off, cap, n, steps, stream, wbytes=None):
     """The decode's memory skeleton on the same batch (gpk_probe_skeleton_idx:
     index, header windows, the wave's stream, the bytes the decode writes;
     none of its work), timed like the decode."""
     import torch
     from gopacket_amd import _lib
     S = _lib.synth_lib()
-    wbytes, streamed = skeleton_shape(cfg)
+    w, streamed = skeleton_shape(cfg)
+    wbytes = w if wbytes is None else wbytes
     wbuf = torch.empty(wbytes * n, dtype=torch.uint8, device="cuda")
     sink = torch.zeros(1, dtype=torch.int32, device="cuda")
 
@@ -931,6 +932,7 @@ def fields_bench(ctx, name="c4", n=64 * 2**20, reps=5, check_packets=4 << 20):
         ok &= (fields[a * 128:b * 128].cpu().numpy().reshape(-1, 128) == want).all(1)
         bad += int((~ok).sum())
     written = 16 + 24 + 128  # record, three flow hashes, fields (+8 on error)
+    skel = skeleton_ms(cfg, data, off, cap, n, 5, stream, wbytes=written)
     ach = algo / (fused * 1e-3) / 1e9
     traffic, traffic_profile = load_traffic("c4f", n)  # the fused launch's PMC profile (tools/profile.sh c4f)
     res = dict(workload=CONFIGS[name]["workload"] + " + layer fields (gpk_decode_batch_fields)",
@@ -940,6 +942,7 @@ def fields_bench(ctx, name="c4", n=64 * 2**20, reps=5, check_packets=4 << 20):
                achieved_GBps=round(ach, 1), frac=round(ach / HBM_PEAK_GBS, 4),
                written_bytes_per_packet=written, traffic=traffic, traffic_profile=traffic_profile,
                read_plus_written_GBps=round((algo + written * n) / (fused * 1e-3) / 1e9, 1),
+               skeleton_ms=round(skel, 4), of_skeleton=round(skel / fused, 4),
                two_launch_ms=round(two, 4), two_launch_kernels=[ctx.kernel_name(parser, data, off, cap, layouts=True),
                                                                 "fields_kernel"],
                parity=("bit-exact" if not bad else "MISMATCH (%d packets)" % bad) +
