@@ -128,7 +128,7 @@ def test_bench_rccl_world_one():
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1", "--master-addr",
            "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "1", "--force-dist",
            "--configs", "c3,c2", "--packets", str(1 << 20), "--steps", "3", "--warmup", "1",
-           "--no-cpu-baseline", "--c5", "0", "--no-probe", "--no-full-parity"]
+           "--no-cpu-baseline", "--c5", "0", "--no-full-parity"]
     out = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=280)
     assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-3000:]
     line = [x for x in out.stdout.splitlines() if x.startswith("{")][-1]
@@ -136,3 +136,6 @@ def test_bench_rccl_world_one():
     assert r["dist_backend"] == "nccl"
     assert r["n_gpus"] == 1 and r["steps"] == 3 and r["scaling"] == "weak" and r["value"] > 0
     assert r["parity"].startswith("bit-exact") and r["configs"]["c2"]["parity"].startswith("bit-exact")
+    # the probes ran: the streaming read and each config's memory skeleton beside its kernel
+    for row in (r["roofline"], r["configs"]["c2"]):
+        assert row["probe_read_GBps"] > 0 and row["skeleton_ms"] > 0 and 0.2 < row["of_skeleton"] < 5
