@@ -350,6 +350,9 @@ def synth_lib():
                                              ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int, ctypes.c_void_p,
                                              ctypes.c_void_p]
         S.gpk_probe_skeleton_idx.restype = ctypes.c_int
+        S.gpk_probe_skeleton_storer.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                                                ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]
+        S.gpk_probe_skeleton_storer.restype = ctypes.c_int
         S.gpk_synth_tpacket_v3.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int,
                                            ctypes.c_uint64, ctypes.c_int32, ctypes.c_uint32, ctypes.c_void_p]
         S.gpk_synth_tpacket_v3.restype = ctypes.c_uint64

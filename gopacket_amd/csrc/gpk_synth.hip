@@ -418,7 +418,96 @@ __global__ __launch_bounds__(256) void probe_skeleton_idx_kernel(const uint8_t* 
   if (acc == 0x9e3779b9u) out[0] = acc;
 }
 
+// The skeleton with a fifth, storing wave per block: waves 0-3 do the
+// skeleton's reads for the block's 256 packets (index, windows, stream) and
+// put their records and flows into LDS; after a barrier wave 4, which reads
+// nothing, stores the block's outputs (4 KiB of records, 3 x 2 KiB of flows,
+// non-temporal). Whether stores cost less from a wave that does not stream.
+__global__ __launch_bounds__(320) void probe_skeleton_storer_kernel(const uint8_t* data, const uint64_t* offsets,
+                                                                   const uint32_t* caplens, uint64_t n, uint8_t* wbuf,
+                                                                   uint32_t wbytes, uint32_t* out) {
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  __shared__ u32x4 win[256 * 6];
+  const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint64_t b0 = (uint64_t)blockIdx.x * 256;
+  uint32_t acc = 0;
+  if (wv < 4) {
+    const uint64_t w0 = b0 + 64 * wv;
+    const uint64_t i = w0 + lane < n ? w0 + lane : n - 1;
+    const uint64_t o = offsets[i];
+    const uint32_t c = caplens[i];
+    acc = c;
+    const uint8_t* h = data + (o & ~15ull);
+    u32x4 w[6];
+#pragma unroll
+    for (int k = 0; k < 6; k++) w[k] = *reinterpret_cast<const u32x4*>(h + 16 * k);
+#pragma unroll
+    for (int k = 0; k < 6; k++) win[threadIdx.x * 6 + k] = w[k];
+    const u32x4 x = win[threadIdx.x * 6 + (lane & 3)];
+    acc = __builtin_amdgcn_udot4(x.x ^ x.y ^ x.z ^ x.w, 0x01010101u, acc, false);
+    const uint64_t lo = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)o) |
+                        (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(o >> 32)) << 32;
+    const uint64_t e = o + c;
+    const uint64_t hi = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)e, 63) |
+                        (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(e >> 32), 63) << 32;
+    const uint64_t b = lo & ~15ull;
+    const uint32_t nv = hi <= b ? 0u : (uint32_t)((hi - b + 15) / 16);
+    const u32x4* v = reinterpret_cast<const u32x4*>(data + b);
+    uint32_t k = lane;
+    for (; k + 7 * 64 < nv; k += 8 * 64) {
+      u32x4 a[8];
+#pragma unroll
+      for (int j = 0; j < 8; j++) a[j] = __builtin_nontemporal_load(v + k + 64 * j);
+#pragma unroll
+      for (int j = 0; j < 8; j++) acc = __builtin_amdgcn_udot4(a[j].x ^ a[j].y ^ a[j].z ^ a[j].w, 0x01010101u, acc, false);
+    }
+    for (; k < nv; k += 64) {
+      const u32x4 a = __builtin_nontemporal_load(v + k);
+      acc = __builtin_amdgcn_udot4(a.x ^ a.y ^ a.z ^ a.w, 0x01010101u, acc, false);
+    }
+  }
+  __syncthreads();  // every wave is past its window reads
+  uint32_t* l = reinterpret_cast<uint32_t*>(win);
+  uint64_t* lf = reinterpret_cast<uint64_t*>(l + 1024);
+  if (wv < 4) {
+    const uint32_t t = threadIdx.x;
+    l[4 * t + 0] = acc;
+    l[4 * t + 1] = lane;
+    l[4 * t + 2] = 0u;
+    l[4 * t + 3] = 1u;
+#pragma unroll
+    for (int j = 0; j < 3; j++) lf[256 * j + t] = (uint64_t)acc * (j + 1);
+  }
+  __syncthreads();
+  if (wv == 4) {
+    u32x4* r = reinterpret_cast<u32x4*>(wbuf) + b0;
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+      if (b0 + 64 * k + lane < n)
+        __builtin_nontemporal_store(reinterpret_cast<const u32x4*>(l)[64 * k + lane], r + 64 * k + lane);
+    if (wbytes >= 40) {
+      uint64_t* f = reinterpret_cast<uint64_t*>(wbuf + 16 * n) + b0;
+#pragma unroll
+      for (int j = 0; j < 3; j++)
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+          if (b0 + 64 * k + lane < n)
+            __builtin_nontemporal_store(lf[256 * j + 64 * k + lane], f + j * n + 64 * k + lane);
+    }
+  }
+  if (acc == 0x9e3779b9u) out[0] = acc;
+}
+
 extern "C" {
+
+int gpk_probe_skeleton_storer(const uint8_t* data, const uint64_t* offsets, const uint32_t* caplens, uint64_t n,
+                              uint8_t* wbuf, uint32_t wbytes, uint32_t* out, void* stream) {
+  const uint64_t blocks = (n + 255) / 256;
+  if (!n || blocks > 0xffffffffull || wbytes < 16) return -1;
+  hipLaunchKernelGGL(probe_skeleton_storer_kernel, dim3((unsigned)blocks), dim3(320), 0, (hipStream_t)stream, data,
+                     offsets, caplens, n, wbuf, wbytes, out);
+  return hipGetLastError() == hipSuccess ? 0 : -3;
+}
 
 int gpk_probe_skeleton_idx(const uint8_t* data, const uint64_t* offsets, const uint32_t* caplens, uint64_t n,
                            uint8_t* wbuf, uint32_t wbytes, int flags, uint32_t* out, void* stream) {

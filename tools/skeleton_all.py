@@ -85,6 +85,10 @@ def main():
             runs["skeleton_writes_first"] = skeleton_flags(32)
             runs["skeleton_writes_ring"] = skeleton_flags(128)
             runs["skeleton_writes_by_wave0"] = skeleton_flags(256)
+            if streamed:  # a fifth wave per block that only stores (the others only read)
+                runs["skeleton_storer_wave"] = lambda: S.gpk_probe_skeleton_storer(
+                    data.data_ptr(), off.data_ptr(), cap.data_ptr(), n, wbuf.data_ptr(), wbytes, sink.data_ptr(),
+                    stream.cuda_stream)
         times = {k: [] for k in runs}
         for rnd in range(a.rounds + 1):
             for k, f in runs.items():
