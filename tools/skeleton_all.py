@@ -84,6 +84,7 @@ def main():
             runs["skeleton_block_writes"] = skeleton_flags(16)
             runs["skeleton_writes_first"] = skeleton_flags(32)
             runs["skeleton_writes_ring"] = skeleton_flags(128)
+            runs["skeleton_writes_ring_temporal"] = skeleton_flags(128 | 8)
             runs["skeleton_writes_by_wave0"] = skeleton_flags(256)
             if streamed:  # a fifth wave per block that only stores (the others only read)
                 runs["skeleton_storer_wave"] = lambda: S.gpk_probe_skeleton_storer(
