@@ -86,6 +86,77 @@ def dist_init(backend="nccl", same_device=False, force=False):
     return rank, world, local
 
 
+def free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_plan(gpus, environ, argv, port=None):
+    """How `bench.py --gpus N` runs (one process per GPU, the contract's
+    launch). Decided before anything touches the GPU:
+    - a launcher set WORLD_SIZE: this process is one rank; WORLD_SIZE must
+      equal N (a mismatch is an error, not a silent world-size-1 run);
+    - no launcher and N == 1: run here;
+    - no launcher and N > 1: start `python -m torch.distributed.run
+      --nproc-per-node N bench.py <same args>` as a CHILD process (never an
+      exec) and relay its output.
+    Returns ("inproc", None) or ("spawn", argv of the child)."""
+    world = environ.get("WORLD_SIZE")
+    if world is not None:
+        if int(world) != gpus:
+            raise SystemExit("bench.py: --gpus %d but WORLD_SIZE=%s (launch one rank per GPU)" % (gpus, world))
+        return "inproc", None
+    if gpus < 1:
+        raise SystemExit("bench.py: --gpus must be >= 1")
+    if gpus == 1:
+        return "inproc", None
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(port or free_port()),
+           os.path.join(ROOT, "bench.py")] + list(argv)
+    return "spawn", cmd
+
+
+def spawn_ranks(cmd):
+    """Run the torchrun child, pass its stdout through line by line (rank 0
+    prints the one JSON line) and return its exit status; a run that ends
+    without a JSON line is a failure."""
+    import subprocess
+    env = dict(os.environ)
+    env.setdefault("OMP_NUM_THREADS", "16")
+    p = subprocess.Popen(cmd, cwd=ROOT, env=env, stdout=subprocess.PIPE, text=True, bufsize=1)
+    lines = 0
+    try:
+        for line in p.stdout:
+            if line.startswith("{"):
+                lines += 1
+            sys.stdout.write(line)
+            sys.stdout.flush()
+        rc = p.wait()
+    except BaseException:
+        p.terminate()
+        p.wait(timeout=30)
+        raise
+    if rc == 0 and lines != 1:
+        sys.stderr.write("bench.py: the multi-rank run printed %d JSON lines, not 1\n" % lines)
+        return 1
+    return rc
+
+
+def gather_ranks(x, world):
+    """Every rank's value of x, in rank order (None at world size 1 without a
+    process group)."""
+    import torch.distributed as dist
+    if world == 1 and not dist.is_initialized():
+        return None
+    out = [None] * world
+    dist.all_gather_object(out, round(float(x), 4))
+    return out
+
+
 def barrier(world):
     import torch
     import torch.distributed as dist
@@ -176,8 +247,11 @@ def run_config(name, n, steps, warmup, rank, world, ctx, check_sample=2048, prob
     e1.record(stream)
     barrier(world)
     wall = time.perf_counter() - t0
-    kernel_ms = e0.elapsed_time(e1) / steps
+    kernel_ms_own = e0.elapsed_time(e1) / steps
     wall_max = shard.max_over_ranks(wall, world, device="cuda")
+    # the slowest rank's kernel time (each rank's own, for the record)
+    kernel_ms = shard.max_over_ranks(kernel_ms_own, world, device="cuda")
+    kernel_ms_ranks = gather_ranks(kernel_ms_own, world)
 
     probe_gbs = probe_read(data, payload_bytes, steps, stream) if probe else None
     skel_ms = skeleton_ms(cfg, data, off, cap, n, steps, stream) if probe and not strong else None
@@ -189,6 +263,7 @@ def run_config(name, n, steps, warmup, rank, world, ctx, check_sample=2048, prob
         full, full_s = full_parity(name, cfg, data, off, cap, rec, fl, err, n, host_cores()[0])
         full = dict(result=full, seconds=round(full_s, 2))
     res = dict(full_parity=full, n=n, payload_bytes=payload_bytes, wall_s=wall_max, kernel_ms=kernel_ms,
+               kernel_ms_ranks=kernel_ms_ranks,
                algo_bytes=payload_bytes + INDEX_BYTES * n, parity=parity, probe_gbs=probe_gbs, skeleton_ms=skel_ms,
                strong=strong,
                kernel=kernel, blocks_per_cu=blocks_per_cu)
@@ -999,9 +1074,15 @@ def main():
                     help="initialise the process group at world size 1 too (barrier / max over ranks through it)")
     args = ap.parse_args()
 
+    mode, cmd = launch_plan(args.gpus, os.environ, sys.argv[1:])
+    if mode == "spawn":  # nothing here has touched the GPU
+        sys.exit(spawn_ranks(cmd))
+
     import torch
     import torch.distributed as dist
     rank, world, local = dist_init(args.dist_backend, args.same_device, args.force_dist)
+    if world != args.gpus:
+        raise SystemExit("bench.py: rank %d sees world size %d, --gpus %d" % (rank, world, args.gpus))
     from gopacket_amd import engine
     ctx = engine.Context(local)
     if args.tables == "global":
@@ -1035,6 +1116,7 @@ def main():
                          "traffic_profile": traffic_profile, "kernel": r["kernel"],
                          "blocks_per_cu": r["blocks_per_cu"],
                          "traffic_unit": "bytes per launch", "kernel_ms": round(r["kernel_ms"], 4),
+                         "kernel_ms_ranks": r["kernel_ms_ranks"],
                          "algo_bytes_per_launch": r["algo_bytes"],
                          "probe_read_GBps": r["probe_gbs"] and round(r["probe_gbs"], 1),
                          "skeleton_ms": r["skeleton_ms"] and round(r["skeleton_ms"], 4),
@@ -1051,14 +1133,16 @@ def main():
             pk = st["total_packets"] if st else s["n"] * world
             row = {"workload": CONFIGS[name]["workload"],
                    "value": round(pk * args.steps / s["wall_s"] / 1e6, 2), "unit": "Mpkts/s",
-                   "kernel": s["kernel"], "blocks_per_cu": s["blocks_per_cu"], "kernel_ms": round(s["kernel_ms"], 4), "achieved_GBps": round(ach, 1),
+                   "kernel": s["kernel"], "blocks_per_cu": s["blocks_per_cu"], "kernel_ms": round(s["kernel_ms"], 4),
+                   "kernel_ms_ranks": s["kernel_ms_ranks"], "achieved_GBps": round(ach, 1),
                    "frac": round(ach / HBM_PEAK_GBS, 4), "parity": s["parity"], "full_parity": s["full_parity"],
                    "probe_read_GBps": s["probe_gbs"] and round(s["probe_gbs"], 1),
                    "skeleton_ms": s["skeleton_ms"] and round(s["skeleton_ms"], 4),
                    "of_skeleton": s["skeleton_ms"] and round(s["skeleton_ms"] / s["kernel_ms"], 4)}
             if st:
                 row.update(scaling="strong", total_packets=st["total_packets"], byte_balance=st["balance"],
-                           note="one batch split at byte-balanced cuts; kernel_ms/achieved are rank 0's shard")
+                           note="one batch split at byte-balanced cuts; kernel_ms/achieved: the slowest rank's "
+                                "shard (kernel_ms_ranks: every rank's)")
             out["configs"][name] = row
         if args.pcie and world == 1:
             out["pcie_inclusive"] = pcie_inclusive(head, ctx)

@@ -101,23 +101,30 @@ def test_two_rank_device_shards_concatenate_to_single_rank_result():
 
 
 def test_bench_two_ranks_strong_and_weak():
-    """bench.py's multi-rank branch (torchrun, 2 ranks, gloo on one GPU)."""
+    """bench.py's multi-rank branch as the driver invokes it: `python bench.py
+    --gpus 2 ...` with no launcher (bench.py starts torch.distributed.run as
+    a child, 2 ranks, gloo, both on the box's one GPU)."""
     env = dict(os.environ, OMP_NUM_THREADS="4")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
-           "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "2", "--dist-backend", "gloo",
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    cmd = [sys.executable, "bench.py", "--gpus", "2", "--dist-backend", "gloo",
            "--same-device", "--configs", "c3,c4s", "--packets", str(1 << 20), "--steps", "2", "--warmup", "1",
            "--no-cpu-baseline", "--c5", "0", "--no-probe"]
     out = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=280)
     assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-3000:]
-    line = [x for x in out.stdout.splitlines() if x.startswith("{")][-1]
-    r = json.loads(line)
+    lines = [x for x in out.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, out.stdout[-2000:]
+    r = json.loads(lines[0])
     assert r["n_gpus"] == 2 and r["steps"] == 2 and r["scaling"] == "weak"
+    assert r["dist_backend"] == "gloo"
     assert r["parity"].startswith("bit-exact")
+    ks = r["roofline"]["kernel_ms_ranks"]
+    assert len(ks) == 2 and abs(r["roofline"]["kernel_ms"] - max(ks)) < 1e-3
     c = r["configs"]["c4s"]
     assert c["scaling"] == "strong" and c["total_packets"] == 1 << 20
     assert c["parity"].startswith("bit-exact") and 1.0 <= c["byte_balance"] < 1.001
+    assert len(c["kernel_ms_ranks"]) == 2 and abs(c["kernel_ms"] - max(c["kernel_ms_ranks"])) < 1e-3
     assert r["roofline"]["kernel"].startswith("gpk::decode_kernel<true,false,true,false,")
-
 
 def test_bench_rccl_world_one():
     """bench.py's RCCL branch on a one-GPU box: torchrun with one rank and
