@@ -291,8 +291,9 @@ def skeleton_ms(cfg, data, off, cap, n, steps, stream, wbytes=None):
     sink = torch.zeros(1, dtype=torch.int32, device="cuda")
 
     def go():
-        assert S.gpk_probe_skeleton_idx(data.data_ptr(), off.data_ptr(), cap.data_ptr(), n, wbuf.data_ptr(), wbytes,
-                                        2 | (0 if streamed else 64), sink.data_ptr(), stream.cuda_stream) == 0
+        assert S.gpk_probe_skeleton_idx(data.data_ptr(), off.data_ptr(), cap.data_ptr(), n, wbuf.data_ptr(),
+                                        wbuf.numel(), wbytes, 2 | (0 if streamed else 64), sink.data_ptr(),
+                                        stream.cuda_stream) == 0
 
     go()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

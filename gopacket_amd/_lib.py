@@ -46,18 +46,18 @@ RECORD_DTYPE = np.dtype([("layers", "<u8"), ("status", "<u4"), ("ip4_csum", "<u2
 LAYOUT_DTYPE = np.dtype([("start", "<u4", (8,)), ("end", "<u4", (8,))])
 # include/gpk.h gpk_fields (128 B): the scalar layer fields (gpk_extract_fields)
 FIELDS_DTYPE = np.dtype({
-    "names": ["present", "eth_type", "eth_length", "eth_dst", "eth_src", "d1q_tci", "d1q_type", "ip4_version",
+    "names": ["present", "hbh_opt_map", "eth_type", "eth_length", "eth_dst", "eth_src", "d1q_tci", "d1q_type", "ip4_version",
               "ip4_ihl", "ip4_tos", "ip4_ttl", "ip4_length", "ip4_id", "ip4_flags_frag", "ip4_protocol",
               "ip6_version", "ip4_checksum", "ip6_traffic_class", "ip6_next_header", "ip6_flow_label", "ip6_length",
               "ip6_hop_limit", "tcp_data_offset", "ip4_src", "ip4_dst", "ip6_src", "ip6_dst", "tcp_src_port",
               "tcp_dst_port", "tcp_seq", "tcp_ack", "tcp_flags", "tcp_window", "tcp_checksum", "tcp_urgent",
               "udp_src_port", "udp_dst_port", "udp_length", "udp_checksum", "ip4_start", "tcp_start",
               "ip4_opt_map", "tcp_opt_map"],
-    "formats": ["<u4", "<u2", "<u2", ("u1", (6,)), ("u1", (6,)), "<u2", "<u2", "u1", "u1", "u1", "u1", "<u2", "<u2",
+    "formats": ["u1", ("u1", (3,)), "<u2", "<u2", ("u1", (6,)), ("u1", (6,)), "<u2", "<u2", "u1", "u1", "u1", "u1", "<u2", "<u2",
                 "<u2", "u1", "u1", "<u2", "u1", "u1", "<u4", "<u2", "u1", "u1", ("u1", (4,)), ("u1", (4,)),
                 ("u1", (16,)), ("u1", (16,)), "<u2", "<u2", "<u4", "<u4", "<u2", "<u2", "<u2", "<u2", "<u2", "<u2",
                 "<u2", "<u2", "u1", "u1", ("u1", (5,)), ("u1", (5,))],
-    "offsets": [0, 4, 6, 8, 14, 20, 22, 24, 25, 26, 27, 28, 30, 32, 34, 35, 36, 38, 39, 40, 44, 46, 47, 48, 52, 56, 72,
+    "offsets": [0, 1, 4, 6, 8, 14, 20, 22, 24, 25, 26, 27, 28, 30, 32, 34, 35, 36, 38, 39, 40, 44, 46, 47, 48, 52, 56, 72,
                 88, 90, 92, 96, 100, 102, 104, 106, 108, 110, 112, 114, 116, 117, 118, 123],
     "itemsize": 128})
 NAME_FIELDS = 2  # gpk_decode_kernel_name / gpk_decode_occupancy: the fused fields launch
@@ -347,11 +347,12 @@ def synth_lib():
                                          ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
         S.gpk_probe_skeleton.restype = ctypes.c_int
         S.gpk_probe_skeleton_idx.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
-                                             ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int, ctypes.c_void_p,
-                                             ctypes.c_void_p]
+                                             ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int,
+                                             ctypes.c_void_p, ctypes.c_void_p]
         S.gpk_probe_skeleton_idx.restype = ctypes.c_int
         S.gpk_probe_skeleton_storer.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
-                                                ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]
+                                                ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_void_p,
+                                                ctypes.c_void_p]
         S.gpk_probe_skeleton_storer.restype = ctypes.c_int
         S.gpk_synth_tpacket_v3.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int,
                                            ctypes.c_uint64, ctypes.c_int32, ctypes.c_uint32, ctypes.c_void_p]

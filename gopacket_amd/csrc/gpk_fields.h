@@ -15,7 +15,7 @@
 //   Dot1Q     layers/dot1q.go:28-41     (the tag control word, Type)
 //   IPv4      layers/ip4.go:178-271     (Length 0 = the slice's length, TSO;
 //                                       option starts, ip4.go:219-256)
-//   IPv6      layers/ip6.go:221-278
+//   IPv6      layers/ip6.go:221-278     (HopByHop option starts, ip6.go:509-526)
 //   TCP       layers/tcp.go:292-313     (option starts, tcp.go:336-549)
 //   UDP       layers/udp.go:30-43
 #ifndef GPK_FIELDS_H
@@ -47,14 +47,42 @@ __device__ __forceinline__ uint64_t option_map(const H& h, uint32_t s, uint32_t 
   return map;
 }
 
+// Where the options of the IPv6 layer's inline HopByHop header start (the
+// header at IPv6 byte 40, ip6.go:244-246): bit k = an option at HopByHop byte
+// 2 + k, walked as IPv6HopByHop.DecodeFromBytes walks them (ip6.go:509-526,
+// TLVs :327-346: Pad1 is one byte, every other option its length byte + 2;
+// the loop runs while the offset is below ActualLength = HeaderLength * 8 +
+// 8). Only for HeaderLength <= 2 (ActualLength <= 26: every start fits the 24
+// bits), else 0. s: the IPv6 start. The IPv6 decode succeeded, so every
+// option it walked was inside the slice.
+template <class H>
+__device__ __forceinline__ uint32_t hbh_map(const H& h, uint32_t s) {
+  const uint32_t hl = h.u8(s + 41);
+  if (hl > 2) return 0;
+  const uint32_t actual = hl * 8 + 8;
+  uint32_t map = 0;
+  for (uint32_t off = 2; off < actual;) {
+    map |= 1u << (off - 2);
+    const uint32_t t = h.u8(s + 40 + off);
+    off += t == 0 ? 1u : h.u8(s + 41 + off) + 2u;
+  }
+  return map;
+}
+
 // present: bit k = layout slot k holds a slice; st[k]: its start (read only
 // when present); ip4_end: the end of the IPv4 slice.
 template <class H>
 __device__ __forceinline__ void fields_words(const H& h, uint32_t present, const uint32_t (&st)[8], uint32_t ip4_end,
                                              uint32_t (&w)[32]) {
+  // the HopByHop walk first, while no record word is live (no scratch in the fused kernel)
+  uint32_t hmap = 0;
+  if (present >> (GPK_DEC_IPV6 - 1) & 1u) {
+    const uint32_t d = st[GPK_DEC_IPV6 - 1];
+    if (h.u8(d + 6) == 0) hmap = hbh_map(h, d);  // NextHeader 0: the inline HopByHop, ip6.go:244-246
+  }
 #pragma unroll
   for (int k = 0; k < 32; k++) w[k] = 0;
-  w[0] = present;
+  w[0] = present | hmap << 8;  // bytes 1-3: the HopByHop option map
   uint32_t ip4s = 0xFFu, tcps = 0xFFu;
   uint64_t ip4m = 0, tcpm = 0;
   if (present >> (GPK_DEC_ETHERNET - 1) & 1u) {  // ethernet.go:46-55

@@ -114,6 +114,9 @@ struct gpk_ctx {
     uint64_t last_use = 0;
   };
   std::unordered_map<hipStream_t, Agg> aggs;
+  // retired aggregation streams whose marks may still be pending: destroyed
+  // once their work has completed (agg_of polls them; never waits)
+  std::vector<Agg> retired;
   std::mutex mu;
   // gpk_replay_file's staging buffers, kept for the next call (gpk_walk.h)
   void* replay_cache = nullptr;
@@ -274,12 +277,14 @@ static void free_slots(gpk_ctx* c) {
     t.dctab = nullptr;
     t.staging = nullptr;
   }
-  for (auto& kv : c->aggs) {
-    (void)hipStreamSynchronize(kv.second.agg);
-    (void)hipStreamDestroy(kv.second.agg);
-    (void)hipEventDestroy(kv.second.ev);
-  }
+  for (auto& kv : c->aggs) c->retired.push_back(kv.second);
   c->aggs.clear();
+  for (auto& a : c->retired) {  // context teardown: the one place that waits
+    (void)hipStreamSynchronize(a.agg);
+    (void)hipStreamDestroy(a.agg);
+    (void)hipEventDestroy(a.ev);
+  }
+  c->retired.clear();
 }
 
 // The first C++ exception a process throws initialises the unwinder's
@@ -450,22 +455,36 @@ static uint32_t fast_flags(const gpk_parser* p) {
   return f;
 }
 
-constexpr size_t kAggStreams = 8;
+// Caller streams with an aggregation stream of their own: enough for
+// gpk_replay_file's one stream per staging slot plus the caller's (its slots
+// option stays far below), so steady launches never create or retire one.
+constexpr size_t kAggStreams = 32;
 
 // The aggregation stream and reusable event of caller stream s (created on
 // first use; beyond kAggStreams callers the least recently used one is
-// drained and retired: the marks recorded on it have completed by then, and
-// a completed event stays complete).
+// retired WITHOUT waiting: it moves to c->retired, and is destroyed by a later
+// call once hipStreamQuery reports its marks complete. Nothing here blocks
+// while c->mu is held, so a caller stream that waits on host progress cannot
+// deadlock another caller.
 static int agg_of(gpk_ctx* c, hipStream_t s, gpk_ctx::Agg** out) {
+  for (size_t k = 0; k < c->retired.size();) {
+    const hipError_t q = hipStreamQuery(c->retired[k].agg);
+    if (q == hipErrorNotReady) {
+      k++;
+      continue;
+    }
+    (void)hipStreamDestroy(c->retired[k].agg);
+    (void)hipEventDestroy(c->retired[k].ev);
+    c->retired[k] = c->retired.back();
+    c->retired.pop_back();
+  }
   auto it = c->aggs.find(s);
   if (it == c->aggs.end()) {
     if (c->aggs.size() >= kAggStreams) {
       auto lru = c->aggs.begin();
       for (auto j = c->aggs.begin(); j != c->aggs.end(); ++j)
         if (j->second.last_use < lru->second.last_use) lru = j;
-      HIPCHK(hipStreamSynchronize(lru->second.agg));
-      HIPCHK(hipStreamDestroy(lru->second.agg));
-      HIPCHK(hipEventDestroy(lru->second.ev));
+      c->retired.push_back(lru->second);  // its marks may be pending: a completed event stays complete
       c->aggs.erase(lru);
     }
     gpk_ctx::Agg a;

@@ -269,7 +269,8 @@ __global__ __launch_bounds__(256) void probe_skeleton_kernel(const uint8_t* data
 #pragma unroll
     for (int k = 0; k < 6; k++) win[threadIdx.x * 6 + k] = w[k];
     __syncthreads();
-    const u32x4 x = win[((threadIdx.x + 1) & 255) * 6 + (lane & 3)];
+    // (the interleaved-store form reuses the wave's own slots: no lane reads another wave's window)
+    const u32x4 x = win[(flags & 512 ? threadIdx.x : (threadIdx.x + 1) & 255) * 6 + (lane & 3)];
     acc = __builtin_amdgcn_udot4(x.x ^ x.y ^ x.z ^ x.w, 0x01010101u, acc, false);
   }
   const u32x4* v = reinterpret_cast<const u32x4*>(data + base + dep);
@@ -333,7 +334,8 @@ __global__ __launch_bounds__(256) void probe_skeleton_idx_kernel(const uint8_t* 
 #pragma unroll
     for (int k = 0; k < 6; k++) win[threadIdx.x * 6 + k] = w[k];
     __syncthreads();
-    const u32x4 x = win[((threadIdx.x + 1) & 255) * 6 + (lane & 3)];
+    // (the interleaved-store form reuses the wave's own slots: no lane reads another wave's window)
+    const u32x4 x = win[(flags & 512 ? threadIdx.x : (threadIdx.x + 1) & 255) * 6 + (lane & 3)];
     acc = __builtin_amdgcn_udot4(x.x ^ x.y ^ x.z ^ x.w, 0x01010101u, acc, false);
   }
   auto store_out = [&]() {
@@ -359,6 +361,25 @@ __global__ __launch_bounds__(256) void probe_skeleton_idx_kernel(const uint8_t* 
 #pragma unroll
         for (int j = 0; j < 8; j++) __builtin_nontemporal_store(u32x4{acc, (uint32_t)j, lane, 0u}, fl + 64 * j + lane);
       }
+    }
+  };
+  // flags & 512: the packet's 40 bytes (record + three flows) interleaved at wbuf + 40 i: each wave's outputs
+  // as ONE contiguous 2560-byte run, staged through its own window slots (read above by its own lanes only)
+  auto store_aos = [&]() {
+    uint32_t* l = reinterpret_cast<uint32_t*>(win) + (threadIdx.x & ~63u) * 24;
+    asm volatile("" ::: "memory");
+    const uint64_t a = acc;
+    *reinterpret_cast<uint64_t*>(l + 10 * lane) = (uint64_t)lane << 32 | acc;
+    *reinterpret_cast<uint64_t*>(l + 10 * lane + 2) = 1ull << 32;
+#pragma unroll
+    for (int j = 0; j < 3; j++) *reinterpret_cast<uint64_t*>(l + 10 * lane + 4 + 2 * j) = a * (j + 1);
+    asm volatile("" ::: "memory");
+    const uint64_t lim = (n - w0) * 40;  // bytes of this wave's run
+    u32x4* r = reinterpret_cast<u32x4*>(wbuf + w0 * 40);
+#pragma unroll
+    for (uint32_t k = 0; k < 3; k++) {
+      const uint32_t c = 64 * k + lane;
+      if (c < 160 && 16ull * c < lim) __builtin_nontemporal_store(reinterpret_cast<const u32x4*>(l)[c], r + c);
     }
   };
   if (flags & 32) store_out();  // the outputs before the stream (their values are whatever acc holds then)
@@ -414,6 +435,7 @@ __global__ __launch_bounds__(256) void probe_skeleton_idx_kernel(const uint8_t* 
     acc = __builtin_amdgcn_udot4(a.x ^ a.y ^ a.z ^ a.w, 0x01010101u, acc, false);
   }
   if (flags & 256) store_by_wave0();
+  else if (flags & 512) store_aos();
   else if (!(flags & 32)) store_out();
   if (acc == 0x9e3779b9u) out[0] = acc;
 }
@@ -500,19 +522,31 @@ __global__ __launch_bounds__(320) void probe_skeleton_storer_kernel(const uint8_
 
 extern "C" {
 
+// wbuf_bytes: the size of wbuf. Every form stores at most wbytes bytes per
+// packet inside [wbuf, wbuf + wbytes * n) (the ring form inside the first
+// 2^20 packets' share); a call whose buffer is smaller, or whose wbytes is not
+// one of the forms (0, 16, 40, 168), is rejected before launch (-1). Round 4's
+// fault: the wave-0 form stored flows into a 16-byte-per-packet buffer.
+static bool skeleton_args_ok(uint64_t n, uint32_t wbytes, int flags, uint64_t wbuf_bytes, bool storer) {
+  if (wbytes != 0 && wbytes != 16 && wbytes != 40 && wbytes != 168) return false;
+  if (storer && wbytes != 16 && wbytes != 40) return false;
+  if ((flags & 512) && wbytes != 40) return false;
+  return wbuf_bytes >= (uint64_t)wbytes * n;
+}
+
 int gpk_probe_skeleton_storer(const uint8_t* data, const uint64_t* offsets, const uint32_t* caplens, uint64_t n,
-                              uint8_t* wbuf, uint32_t wbytes, uint32_t* out, void* stream) {
+                              uint8_t* wbuf, uint64_t wbuf_bytes, uint32_t wbytes, uint32_t* out, void* stream) {
   const uint64_t blocks = (n + 255) / 256;
-  if (!n || blocks > 0xffffffffull || wbytes < 16) return -1;
+  if (!n || blocks > 0xffffffffull || !skeleton_args_ok(n, wbytes, 0, wbuf_bytes, true)) return -1;
   hipLaunchKernelGGL(probe_skeleton_storer_kernel, dim3((unsigned)blocks), dim3(320), 0, (hipStream_t)stream, data,
                      offsets, caplens, n, wbuf, wbytes, out);
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
 int gpk_probe_skeleton_idx(const uint8_t* data, const uint64_t* offsets, const uint32_t* caplens, uint64_t n,
-                           uint8_t* wbuf, uint32_t wbytes, int flags, uint32_t* out, void* stream) {
+                           uint8_t* wbuf, uint64_t wbuf_bytes, uint32_t wbytes, int flags, uint32_t* out, void* stream) {
   const uint64_t blocks = (n + 255) / 256;
-  if (!n || blocks > 0xffffffffull) return -1;
+  if (!n || blocks > 0xffffffffull || !skeleton_args_ok(n, wbytes, flags, wbuf_bytes, false)) return -1;
   hipLaunchKernelGGL(probe_skeleton_idx_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, data,
                      offsets, caplens, n, wbuf, wbytes, flags, out);
   return hipGetLastError() == hipSuccess ? 0 : -3;

@@ -211,6 +211,10 @@ class Payload:
 
     def _hydrate(self, d):
         self.data = d
+        self._poff = len(d)
+
+    def _fill(self, pkt, s, e, f):
+        self._hydrate(pkt[s:e])
 
 
 class Fragment(Payload):
@@ -329,6 +333,11 @@ def NewDecodingLayerParser(first, *decoders):
     return DecodingLayerParser(first, *decoders)
 
 
+def _slot(kind):
+    """gpk_layout / gpk_fields.present slot of a decoder kind (Payload and Fragment share 7)."""
+    return min(kind, _lib.DEC_PAYLOAD) - 1
+
+
 class BatchResult:
     """Device results of DecodeBatch, with per-packet gopacket views."""
 
@@ -398,8 +407,8 @@ class BatchResult:
         f = self._fields_of(i)
         if not int(f["present"]) & (1 << (_lib.DEC_IPV4 - 1)):
             return None
-        return IPv4OptionsFromMap(self._packet_for(i, int(f["ip4_start"]), "ip4"), int(f["ip4_start"]),
-                                  int(f["ip4_ihl"]) * 4, f["ip4_opt_map"])
+        pkt, s = self._start_of(i, f, _lib.DEC_IPV4, "ip4_start")
+        return IPv4OptionsFromMap(pkt, s, int(f["ip4_ihl"]) * 4, f["ip4_opt_map"])
 
     def TCPOptions(self, i):
         """(Options, Padding, Multipath) of packet i's TCP layer from the
@@ -408,22 +417,36 @@ class BatchResult:
         f = self._fields_of(i)
         if not int(f["present"]) & (1 << (_lib.DEC_TCP - 1)):
             return None
-        return TCPOptionsFromMap(self._packet_for(i, int(f["tcp_start"]), "tcp"), int(f["tcp_start"]),
-                                 int(f["tcp_data_offset"]) * 4, f["tcp_opt_map"])
+        pkt, s = self._start_of(i, f, _lib.DEC_TCP, "tcp_start")
+        return TCPOptionsFromMap(pkt, s, int(f["tcp_data_offset"]) * 4, f["tcp_opt_map"])
 
     def _fields_of(self, i):
         if self.fields is None:
             raise ValueError("option maps need fields=True results")
         return self.fields[i]
 
-    def _packet_for(self, i, start, what):
-        if start == 0xFF:  # the header starts at byte 255 or later: the map's offsets are not in the record
-            raise ValueError("packet %d: %s header beyond byte 254, use Hydrate" % (i, what))
-        return self.batch.packet(i)
+    def _start_of(self, i, f, kind, name):
+        """(packet bytes, start of the decoder's header): the record's start,
+        or, for a header at byte 255 or later (0xFF), the start of its slice
+        derived from the decoded list (as Hydrate derives it)."""
+        pkt = self.batch.packet(i)
+        s = int(f[name])
+        if s == 0xFF:
+            sl = self._slices(pkt, self.Decoded(i), f) or self._slices_host(pkt, self.Decoded(i))
+            s = sl[kind][0]
+        return pkt, s
 
     def Hydrate(self, i, decoded):
         """Make the parser's layer structs and `decoded` look exactly as after
-        DecodeLayers(packet i, decoded); returns its error value."""
+        DecodeLayers(packet i, decoded); returns its error value.
+
+        From layouts=True results each struct is read from its decoder's
+        slice. From fields=True results without layouts (the one-launch
+        gpk_decode_batch_fields) each struct is filled from the packet's
+        gpk_fields record (layers.*._fill), at slices derived from the decoded
+        list (_slices); only what the record cannot describe (a stacked IPv4,
+        IPv6, Ethernet or UDP, a HopByHop header longer than its option map)
+        is read from the packet bytes (counted in host_decodes)."""
         p = self.parser
         if p.first.__int__() not in [int(t) for d in p._decoders.values() for t in d.CanDecode()]:
             # LayersDecoder (layers_decoder.go:12-16): decoded is not truncated
@@ -432,30 +455,119 @@ class BatchResult:
         decoded[:] = self.Decoded(i)
         p.Truncated = self.Truncated(i)
         err = self.Err(i)
-        if self.layouts is None:
-            raise ValueError("Hydrate needs layouts=True results")
         pkt = self.batch.packet(i)
-        lay = self.layouts[i]
-        st = self.status(i)
-        lh, nh, th = self.FlowHashes(i)
-        for slot, kind in enumerate(_lib.LAYOUT_SLOTS):
-            s = int(lay["start"][slot])
-            if s == _lib.LAYOUT_ABSENT:
-                continue
-            e = int(lay["end"][slot])
-            if slot == 7:
-                kind = _lib.DEC_PAYLOAD if _lib.DEC_PAYLOAD in p._decoders and \
-                    LayerTypePayload in decoded else _lib.DEC_FRAGMENT
-            inst = p._decoders.get(kind)
-            if inst is None:
-                continue
-            inst._hydrate(pkt[s:e])
-            if kind == _lib.DEC_ETHERNET and lh is not None:
-                inst._link_hash = lh
-            if kind == _lib.DEC_IPV4 and st & _lib.ST_IP4_CSUM:
-                inst._csum = (None, ChecksumVerificationResult(bool(st & _lib.ST_IP4_VALID),
-                                                               int(self.records[i]["ip4_csum"]), inst.Checksum))
-            if kind in (_lib.DEC_TCP, _lib.DEC_UDP) and st & _lib.ST_L4_CSUM:
-                inst._csum = (None, ChecksumVerificationResult(bool(st & _lib.ST_L4_VALID),
-                                                               int(self.records[i]["l4_csum"]), inst.Checksum))
+        if self.layouts is not None:
+            lay = self.layouts[i]
+            for slot, kind in enumerate(_lib.LAYOUT_SLOTS):
+                s = int(lay["start"][slot])
+                if s == _lib.LAYOUT_ABSENT:
+                    continue
+                e = int(lay["end"][slot])
+                if slot == 7:
+                    kind = _lib.DEC_PAYLOAD if _lib.DEC_PAYLOAD in p._decoders and \
+                        LayerTypePayload in decoded else _lib.DEC_FRAGMENT
+                inst = p._decoders.get(kind)
+                if inst is None:
+                    continue
+                inst._hydrate(pkt[s:e])
+                self._attach(i, kind, inst)
+        elif self.fields is not None:
+            f = self.fields[i]
+            sl = self._slices(pkt, decoded, f)
+            fill = True
+            if sl is None:  # the record does not describe this stack: read the slices' headers
+                self.host_decodes += 1
+                sl, fill = self._slices_host(pkt, decoded), False
+            pres = int(f["present"])
+            for kind, (s, e) in sl.items():
+                if not pres >> (_slot(kind)) & 1:
+                    continue  # a later DecodeFromBytes of this instance failed: not in the layout either
+                if fill:
+                    p._decoders[kind]._fill(pkt, s, e, f)
+                else:
+                    p._decoders[kind]._hydrate(pkt[s:e])
+                self._attach(i, kind, p._decoders[kind])
+        else:
+            raise ValueError("Hydrate needs layouts=True or fields=True results")
         return err
+
+    host_decodes = 0  # packets Hydrate read headers for on the host (fields=True results only)
+
+    def _attach(self, i, kind, inst):
+        """The device's flow hash and checksum results on the hydrated struct."""
+        st = self.status(i)
+        if kind == _lib.DEC_ETHERNET and st & _lib.ST_LINK_FLOW:
+            inst._link_hash = int(self.flows[i])
+        if kind == _lib.DEC_IPV4 and st & _lib.ST_IP4_CSUM:
+            inst._csum = (None, ChecksumVerificationResult(bool(st & _lib.ST_IP4_VALID),
+                                                           int(self.records[i]["ip4_csum"]), inst.Checksum))
+        if kind in (_lib.DEC_TCP, _lib.DEC_UDP) and st & _lib.ST_L4_CSUM:
+            inst._csum = (None, ChecksumVerificationResult(bool(st & _lib.ST_L4_VALID),
+                                                           int(self.records[i]["l4_csum"]), inst.Checksum))
+
+    def _kinds(self, decoded):
+        """The decoder kind of each decoded LayerType (the parser's container:
+        one instance per type, parser.go:74-169)."""
+        by_type = {int(t): k for k, d in self.parser._decoders.items() for t in d.CanDecode()}
+        return [by_type[int(t)] for t in decoded]
+
+    def _slices(self, pkt, decoded, f):
+        """{kind: (start, end)} of the slice each decoder's LAST DecodeFromBytes
+        was handed (what gpk_layout records), derived from the decoded list:
+        the first decoder gets the whole packet, each next one its
+        predecessor's Payload, whose start and end follow from the
+        predecessor's fields in the record (layers.payload_end,
+        layers.ipv6_payload_start). None when the record cannot give them: a
+        decoder whose header length or trim depends on its own fields appears
+        twice (the record holds the last instance only), or an inline
+        HopByHop is longer than the record's option map."""
+        from . import layers as L
+        kinds = self._kinds(decoded)
+        pres = int(f["present"])
+        for k in kinds:
+            if not pres >> _slot(k) & 1:  # decoded, then a later instance failed: its fields are gone
+                return None
+        for k in (_lib.DEC_ETHERNET, _lib.DEC_IPV4, _lib.DEC_IPV6, _lib.DEC_TCP, _lib.DEC_UDP):
+            if kinds.count(k) > 1:
+                return None
+        out, s, e = {}, 0, len(pkt)
+        for k in kinds:
+            out[k] = (s, e)
+            if k == _lib.DEC_ETHERNET:
+                s, e = s + 14, L.payload_end(k, pkt, s, e, f)
+            elif k == _lib.DEC_DOT1Q:
+                s = s + 4
+            elif k == _lib.DEC_IPV4:
+                s, e = s + int(f["ip4_ihl"]) * 4, L.payload_end(k, pkt, s, e, f)
+            elif k == _lib.DEC_IPV6:
+                if int(f["ip6_next_header"]) == L.IPProtocolIPv6HopByHop and not L.hbh_map_covers(pkt, s + 40):
+                    return None
+                s, e = L.ipv6_payload_start(pkt, s, f), L.payload_end(k, pkt, s, e, f)
+            elif k == _lib.DEC_IPV6_EXT:
+                s = s + pkt[s + 1] * 8 + 8
+            elif k == _lib.DEC_TCP:
+                s = s + int(f["tcp_data_offset"]) * 4
+            elif k == _lib.DEC_UDP:
+                s, e = s + 8, L.payload_end(k, pkt, s, e, f)
+        # the record's own view of the same decode: presence and the starts it keeps
+        got = 0
+        for k in out:
+            got |= 1 << _slot(k)
+        assert got == pres, "record presence %#x, decoded list %#x" % (pres, got)
+        for k, name in ((_lib.DEC_IPV4, "ip4_start"), (_lib.DEC_TCP, "tcp_start")):
+            if k in out and out[k][0] < 0xFF:
+                assert out[k][0] == int(f[name]), name
+        return out
+
+    def _slices_host(self, pkt, decoded):
+        """The same slices, each predecessor's Payload read from its header
+        bytes on the host (layers.*._hydrate); the fallback of _slices."""
+        out, s, e = {}, 0, len(pkt)
+        scratch = {}
+        for k in self._kinds(decoded):
+            out[k] = (s, e)
+            inst = scratch.setdefault(k, type(self.parser._decoders[k])())
+            inst._hydrate(pkt[s:e])
+            s = s + inst._poff
+            e = s + len(inst.LayerPayload() if hasattr(inst, "LayerPayload") else b"")
+        return out

@@ -2,12 +2,18 @@
 the DecodingLayer structs Ethernet, Dot1Q, IPv4, IPv6, IPv6ExtensionSkipper,
 TCP, UDP (layers/{ethernet,dot1q,ip4,ip6,tcp,udp}.go).
 
-These structs are filled from device results: the GPU runs DecodeLayers and
-reports, per decoder instance, the byte range its DecodeFromBytes was handed
-(gpk_layout). Every field below is then a pure read of those packet bytes,
-following the field assignments of the reference decoder it names. Option
-lists are walked from bytes whose validity the device already established
-(the device reports any option error as the packet's error instead).
+These structs are filled from device results, in one of two ways:
+- _fill(pkt, s, e, f): from the gpk_fields record the device wrote for the
+  packet (gpk_decode_batch_fields) and the slice [s, e) its DecodeFromBytes
+  was handed (derived from the decoded list, gopacket.BatchResult.Hydrate):
+  every scalar field is the record's, option lists come from the record's
+  option start maps, and Contents/Payload are slices at the header length and
+  payload end the record's fields give. No header is decoded on the host.
+- _hydrate(d): from the slice alone (a gpk_layout range), every field a pure
+  read of those packet bytes, following the field assignments of the
+  reference decoder it names; the fallback for what the record does not hold.
+Option lists are walked from bytes whose validity the device already
+established (the device reports any option error as the packet's error).
 """
 import json
 import os
@@ -115,12 +121,19 @@ class Ethernet(BaseLayer):
         self.SrcMAC = d[6:12]
         self.EthernetType = _be16(d, 12)
         self.Contents, self.Payload = d[:14], d[14:]
+        self._poff = 14
         self.Length = 0
         if self.EthernetType < 0x0600:
             self.Length = self.EthernetType
             self.EthernetType = EthernetTypeLLC
             if len(self.Payload) > self.Length:
                 self.Payload = self.Payload[:self.Length]
+
+    def _fill(self, pkt, s, e, f):
+        self.DstMAC, self.SrcMAC = bytes(f["eth_dst"]), bytes(f["eth_src"])
+        self.EthernetType, self.Length = int(f["eth_type"]), int(f["eth_length"])
+        self.Contents, self.Payload = pkt[s:s + 14], pkt[s + 14:payload_end(_lib.DEC_ETHERNET, pkt, s, e, f)]
+        self._poff = 14
 
     def LinkFlow(self):
         return NewFlow(EndpointMAC, self.SrcMAC, self.DstMAC)
@@ -148,6 +161,14 @@ class Dot1Q(BaseLayer):
         self.VLANIdentifier = _be16(d, 0) & 0x0FFF
         self.Type = _be16(d, 2)
         self.Contents, self.Payload = d[:4], d[4:]
+        self._poff = 4
+
+    def _fill(self, pkt, s, e, f):
+        tci = int(f["d1q_tci"])
+        self.Priority, self.DropEligible, self.VLANIdentifier = tci >> 13, bool(tci >> 12 & 1), tci & 0x0FFF
+        self.Type = int(f["d1q_type"])
+        self.Contents, self.Payload = pkt[s:s + 4], pkt[s + 4:e]
+        self._poff = 4
 
 
 @dataclass
@@ -221,6 +242,21 @@ class IPv4(BaseLayer, _Checksummed):
         self.Checksum = _be16(d, 10)
         self.SrcIP = d[12:16]
         self.DstIP = d[16:20]
+        self._poff = hl
+
+    def _fill(self, pkt, s, e, f):
+        self.Version, self.IHL, self.TOS = int(f["ip4_version"]), int(f["ip4_ihl"]), int(f["ip4_tos"])
+        self.Length, self.Id = int(f["ip4_length"]), int(f["ip4_id"])
+        ff = int(f["ip4_flags_frag"])
+        self.Flags, self.FragOffset = ff >> 13, ff & 0x1FFF
+        self.TTL, self.Protocol, self.Checksum = int(f["ip4_ttl"]), int(f["ip4_protocol"]), int(f["ip4_checksum"])
+        self.SrcIP, self.DstIP = bytes(f["ip4_src"]), bytes(f["ip4_dst"])
+        hl = self.IHL * 4
+        self.Contents, self.Payload = pkt[s:s + hl], pkt[s + hl:payload_end(_lib.DEC_IPV4, pkt, s, e, f)]
+        self.Options, padding = IPv4OptionsFromMap(pkt, s, hl, f["ip4_opt_map"])
+        if padding is not None:  # set only by an End of options (ip4.go:231), else kept
+            self.Padding = padding
+        self._poff = hl
 
     def NetworkFlow(self):
         return NewFlow(EndpointIPv4, self.SrcIP, self.DstIP)
@@ -291,9 +327,24 @@ class IPv6(BaseLayer, _Checksummed):
             jumbo = next((o for o in h.Options if o.OptionType == IPv6HopByHopOptionJumbogram), None)
             if jumbo is not None and self.Length == 0:
                 self.Payload = self.Payload[:min(_be32(jumbo.OptionData, 0), len(self.Payload))]
+                self._poff = 40
                 return
             self.Payload = self.Payload[h.ActualLength:]
         self.Payload = self.Payload[:min(self.Length, len(self.Payload))]
+        self._poff = 40 + (self.hbh.ActualLength if self.HopByHop is not None else 0)
+
+    def _fill(self, pkt, s, e, f):
+        self.Version, self.TrafficClass = int(f["ip6_version"]), int(f["ip6_traffic_class"])
+        self.FlowLabel, self.Length = int(f["ip6_flow_label"]), int(f["ip6_length"])
+        self.NextHeader, self.HopLimit = int(f["ip6_next_header"]), int(f["ip6_hop_limit"])
+        self.SrcIP, self.DstIP = bytes(f["ip6_src"]), bytes(f["ip6_dst"])
+        self.HopByHop = None
+        self.Contents = pkt[s:s + 40]
+        if self.NextHeader == IPProtocolIPv6HopByHop:
+            HopByHopFromMap(self.hbh, pkt, s + 40, e, f["hbh_opt_map"])
+            self.HopByHop = self.hbh
+        self._poff = ipv6_payload_start(pkt, s, f) - s
+        self.Payload = pkt[s + self._poff:payload_end(_lib.DEC_IPV6, pkt, s, e, f)]
 
     def NetworkFlow(self):
         return NewFlow(EndpointIPv6, self.SrcIP, self.DstIP)
@@ -329,6 +380,70 @@ def IPv4OptionsFromMap(pkt, start, hlen, opt_map):
     return opts, padding
 
 
+def hbh_map_covers(pkt, hbh_start):
+    """Whether a gpk_fields hbh_opt_map holds the HopByHop header at
+    pkt[hbh_start]: HeaderLength <= 2 (include/gpk.h)."""
+    return pkt[hbh_start + 1] <= 2
+
+
+def HopByHopFromMap(h, pkt, b0, e, opt_map):
+    """IPv6HopByHop (ip6.go:418-432 base, :509-526 options, TLVs :327-346) of
+    the header at pkt[b0] inside the IPv6 slice ending at e, from its
+    gpk_fields option map: NextHeader and HeaderLength are the header's two
+    bytes, each option read at its start."""
+    h.NextHeader, h.HeaderLength = pkt[b0], pkt[b0 + 1]
+    h.ActualLength = h.HeaderLength * 8 + 8
+    h.Contents, h.Payload = pkt[b0:b0 + h.ActualLength], pkt[b0 + h.ActualLength:e]
+    h.Options = []
+    for k in _map_bits(opt_map):
+        b = b0 + 2 + k
+        if pkt[b] == 0:  # Pad1
+            h.Options.append(IPv6HopByHopOption(0, 0, 1, None))
+        else:
+            al = pkt[b + 1] + 2
+            h.Options.append(IPv6HopByHopOption(pkt[b], pkt[b + 1], al, pkt[b + 2:b + al]))
+    return h
+
+
+def _hbh_jumbo(pkt, b0, opt_map):
+    """The jumbogram length of the HopByHop header at pkt[b0] (ip6.go:54-76:
+    the first option of type 0xC2), or None."""
+    for k in _map_bits(opt_map):
+        b = b0 + 2 + k
+        if pkt[b] == IPv6HopByHopOptionJumbogram:
+            return _be32(pkt, b + 2)
+    return None
+
+
+def ipv6_payload_start(pkt, s, f):
+    """Where the IPv6 layer at pkt[s]'s Payload starts (ip6.go:235-262): after
+    the 40-byte header, and after an inline HopByHop header unless it is a
+    jumbogram (P4: its payload is not advanced past the HopByHop header)."""
+    if int(f["ip6_next_header"]) != IPProtocolIPv6HopByHop:
+        return s + 40
+    if int(f["ip6_length"]) == 0 and _hbh_jumbo(pkt, s + 40, f["hbh_opt_map"]) is not None:
+        return s + 40
+    return s + 40 + pkt[s + 41] * 8 + 8
+
+
+def payload_end(kind, pkt, s, e, f):
+    """The end of the Payload of the decoder `kind` whose DecodeFromBytes was
+    handed pkt[s:e], from its gpk_fields values (each decoder's trim rule)."""
+    if kind == _lib.DEC_ETHERNET:  # ethernet.go:50-55: 802.3 length trims, never grows
+        return s + 14 + int(f["eth_length"]) if int(f["eth_type"]) == 0 and e - s - 14 > int(f["eth_length"]) else e
+    if kind == _lib.DEC_IPV4:  # ip4.go:189-205 (Length already the slice's uint16 length when 0, P9)
+        return s + int(f["ip4_length"]) if e - s > int(f["ip4_length"]) else e
+    if kind == _lib.DEC_IPV6:  # ip6.go:244-277 (P3 / P4)
+        p0, length = ipv6_payload_start(pkt, s, f), int(f["ip6_length"])
+        if int(f["ip6_next_header"]) == IPProtocolIPv6HopByHop and length == 0:
+            length = _hbh_jumbo(pkt, s + 40, f["hbh_opt_map"])
+        return min(e, p0 + length) if p0 <= e else p0
+    if kind == _lib.DEC_UDP:  # udp.go:46-55
+        ln = int(f["udp_length"])
+        return s + min(ln, e - s) if ln >= 8 else e
+    return e
+
+
 # ---- layers/ip6.go:434-461 ---------------------------------------------------
 class IPv6ExtensionSkipper(BaseLayer):
     kind = _lib.DEC_IPV6_EXT
@@ -343,6 +458,14 @@ class IPv6ExtensionSkipper(BaseLayer):
         actual = d[1] * 8 + 8
         self.NextHeader = d[0]
         self.Contents, self.Payload = d[:actual], d[actual:]
+        self._poff = actual
+
+    def _fill(self, pkt, s, e, f):
+        # no record fields: NextHeader and HeaderLength are the header's first two bytes (ip6.go:418-461)
+        actual = pkt[s + 1] * 8 + 8
+        self.NextHeader = pkt[s]
+        self.Contents, self.Payload = pkt[s:s + actual], pkt[s + actual:e]
+        self._poff = actual
 
 
 TCPOptionKindEndList, TCPOptionKindNop, TCPOptionKindMSS, TCPOptionKindTimestamps = 0, 1, 2, 8
@@ -407,6 +530,23 @@ class TCP(BaseLayer, _Checksummed):
                 o = TCPOption(t, opts[1], opts[2:opts[1]])
             self.Options.append(o)
             opts = opts[o.OptionLength:]
+        self._poff = ds
+
+    def _fill(self, pkt, s, e, f):
+        self.SrcPort, self.DstPort = int(f["tcp_src_port"]), int(f["tcp_dst_port"])
+        self.sPort, self.dPort = struct.pack(">H", self.SrcPort), struct.pack(">H", self.DstPort)
+        self.Seq, self.Ack, self.DataOffset = int(f["tcp_seq"]), int(f["tcp_ack"]), int(f["tcp_data_offset"])
+        fl = int(f["tcp_flags"])
+        self.FIN, self.SYN, self.RST, self.PSH = bool(fl & 1), bool(fl & 2), bool(fl & 4), bool(fl & 8)
+        self.ACK, self.URG, self.ECE, self.CWR = bool(fl & 0x10), bool(fl & 0x20), bool(fl & 0x40), bool(fl & 0x80)
+        self.NS = bool(fl & 0x100)
+        self.Window, self.Checksum, self.Urgent = int(f["tcp_window"]), int(f["tcp_checksum"]), int(f["tcp_urgent"])
+        ds = self.DataOffset * 4
+        self.Contents, self.Payload = pkt[s:s + ds], pkt[s + ds:e]
+        self.Options, self.Padding, mp = TCPOptionsFromMap(pkt, s, ds, f["tcp_opt_map"])
+        if mp:  # tcp.go:348: set by an MPTCP option, never reset (P6)
+            self.Multipath = True
+        self._poff = ds
 
     def TransportFlow(self):
         return NewFlow(EndpointTCPPort, self.sPort, self.dPort)
@@ -456,6 +596,14 @@ class UDP(BaseLayer, _Checksummed):
             self.Payload = d[8:min(self.Length, len(d))]
         else:
             self.Payload = d[8:]
+        self._poff = 8
+
+    def _fill(self, pkt, s, e, f):
+        self.SrcPort, self.DstPort = int(f["udp_src_port"]), int(f["udp_dst_port"])
+        self.sPort, self.dPort = struct.pack(">H", self.SrcPort), struct.pack(">H", self.DstPort)
+        self.Length, self.Checksum = int(f["udp_length"]), int(f["udp_checksum"])
+        self.Contents, self.Payload = pkt[s:s + 8], pkt[s + 8:payload_end(_lib.DEC_UDP, pkt, s, e, f)]
+        self._poff = 8
 
     def TransportFlow(self):
         return NewFlow(EndpointUDPPort, self.sPort, self.dPort)

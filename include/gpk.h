@@ -54,7 +54,10 @@
 extern "C" {
 #endif
 
-#define GPK_ABI_VERSION 1
+/* 2: gpk_fields bytes 1-3 carry the HopByHop option map (present is a u8);
+ *    gpk_replay_stats gained alloc_wait_s. A caller compiled against another
+ *    version must not call in: check gpk_abi_version() == GPK_ABI_VERSION. */
+#define GPK_ABI_VERSION 2
 
 /* ---- status codes -------------------------------------------------------- */
 #define GPK_OK 0
@@ -208,10 +211,19 @@ typedef struct gpk_layout {
  * present: bit k set = layout slot k holds a slice (k = GPK_DEC_* - 1; Payload
  * and Fragment share slot 7); every field of an absent layer is 0. Integers in
  * host byte order; MACs and addresses as their bytes. Variable-length parts
- * (HopByHop options, Payload) stay in the packet bytes at the layout's range;
- * IPv4 and TCP option lists are described by their option start maps.        */
+ * (Payload, option data) stay in the packet bytes; the IPv4, TCP and IPv6
+ * HopByHop option lists are described by their option start maps.
+ * Stacked layers (QinQ, IP in IP, 6in6): the fields are the LAST instance's,
+ * as the reference's one struct per type holds them (parser.go:21-28, last
+ * writer wins); ip4_start / tcp_start are 0xFF when that header starts at
+ * packet byte 255 or later (the record has one byte each; Hydrate derives the
+ * starts from the decoded list instead).                                     */
 typedef struct gpk_fields {
-  uint32_t present;          /*   0                                                       */
+  uint8_t present;           /*   0                                                       */
+  uint8_t hbh_opt_map[3];    /*   1 IPv6.HopByHop.Options (the last IPv6's inline HopByHop,
+                                    ip6.go:244-256, 509-526): bit k (byte k/8, bit k%8) set =
+                                    an option starts at HopByHop byte 2 + k; covers headers of
+                                    up to 26 bytes (HeaderLength <= 2), 0 for longer ones     */
   uint16_t eth_type;         /*   4 Ethernet.EthernetType (EthernetTypeLLC = 0 below 0x0600) */
   uint16_t eth_length;       /*   6 Ethernet.Length (802.3 frames, else 0)               */
   uint8_t eth_dst[6];        /*   8 Ethernet.DstMAC                                       */
@@ -262,7 +274,13 @@ typedef struct gpk_fields {
  * pkt[b+1]; OptionData = pkt[b+2 : b+OptionLength] (IPv4 and TCP kinds other
  * than 0, 1 and 30). A list that ends with kind 0 has Padding = the header's
  * bytes after it (ip4.go:231, tcp.go:343). Every option lies inside the
- * header the layer decoded (the decode checked each length). */
+ * header the layer decoded (the decode checked each length).
+ * HopByHop (IPv6 NextHeader 0, header at the IPv6 start + 40): option j at the
+ * j-th set bit k of hbh_opt_map, HopByHop byte b = 2 + k; OptionType = hbh[b];
+ * type 0 (Pad1): ActualLength 1, no length or data; else OptionLength =
+ * hbh[b+1], ActualLength = OptionLength + 2, OptionData = hbh[b+2 :
+ * b+ActualLength] (ip6.go:327-346; the last option may extend past the
+ * header's ActualLength, as the reference's loop allows). */
 
 /* ---- outputs -------------------------------------------------------------- */
 #define GPK_OUT_IP4_CSUM 0x1u  /* IPv4.VerifyChecksum for the last IPv4 in decoded        */

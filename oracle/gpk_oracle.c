@@ -858,6 +858,20 @@ static void fields_of(const uint8_t* pkt, const gpk_layout* lay, gpk_fields* f) 
     f->ip6_hop_limit = d[7];
     memcpy(f->ip6_src, d + 8, 16);
     memcpy(f->ip6_dst, d + 24, 16);
+    /* ip6.go:244-246: NextHeader 0 is decoded inline as IPv6HopByHop from
+     * data[40:]; its options (ip6.go:509-526 loop, TLVs :327-346), for
+     * HeaderLength <= 2 (the map's 24 bits hold every start) */
+    if (f->ip6_next_header == 0 && d[41] <= 2) {
+      const uint32_t actual = (uint32_t)d[41] * 8 + 8;
+      uint32_t map = 0;
+      for (uint32_t off = 2; off < actual;) {
+        map |= 1u << (off - 2);
+        off += d[40 + off] == 0 ? 1u : (uint32_t)d[41 + off] + 2u; /* Pad1 | OptionLength + 2 */
+      }
+      f->hbh_opt_map[0] = (uint8_t)map;
+      f->hbh_opt_map[1] = (uint8_t)(map >> 8);
+      f->hbh_opt_map[2] = (uint8_t)(map >> 16);
+    }
   }
   if (lay->start[GPK_DEC_TCP - 1] != GPK_LAYOUT_ABSENT) { /* tcp.go:296-313 */
     const uint8_t* d = pkt + lay->start[GPK_DEC_TCP - 1];

@@ -213,3 +213,20 @@ def test_decode_batch_fused_options(gpu_ctx):
             assert opts == v.Options and pad == v.Padding and mp == v.Multipath, i
             nt += len(opts) > 0
     assert n4 > 20 and nt > 20
+
+
+def test_fields_hopbyhop_maps(gpu_ctx):
+    """The HopByHop option map (gpk_fields bytes 1-3, ip6.go:509-526) of
+    Pad1 / PadN / Router Alert / Jumbo Payload mixes in headers of 8 to 32
+    bytes, behind 0-2 tags: both device paths against the oracle, and the
+    map set wherever the header fits it."""
+    import hydrate_cases as H
+    for cfg_name in ("statsassembly", "raw_ip6"):
+        if cfg_name not in CONFIGS:
+            continue
+        pkts = H.hbh_packets(17, 3000)
+        if cfg_name == "raw_ip6":
+            pkts = [H.strip_ethernet(p) for p in pkts]
+        f = check(gpu_ctx, cfg_name, pkts)
+        m = f["hbh_opt_map"].astype(np.uint32)
+        assert ((m[:, 0] | m[:, 1] << 8 | m[:, 2] << 16) != 0).mean() > 0.5, cfg_name

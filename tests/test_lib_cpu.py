@@ -28,7 +28,7 @@ def test_exports_every_declared_symbol():
     for n in names:
         assert hasattr(L, n), n
     assert set(names) == set(_lib.EXPORTS)
-    assert L.gpk_abi_version() == 1
+    assert L.gpk_abi_version() == 2
 
 
 def test_parser_config_container_semantics():

@@ -123,3 +123,57 @@ def test_slot_eviction_across_three_streams(gpu_ctx):
         e = (got["status"] & 0x7F) != 0
         assert np.array_equal(err.cpu().numpy().view(np.uint32).reshape(n, 2)[e],
                               np.tile(ref["err_args"].reshape(n1, 2), (reps, 1))[e]), i
+
+
+def test_many_caller_streams_one_context(gpu_ctx):
+    """More caller streams than the context keeps aggregation streams for
+    (40 > kAggStreams = 32, gpk_host.cpp agg_of), three parsers cycled over
+    them with no synchronisation, the first stream held behind ~1 s of device
+    work: retiring its aggregation stream must not wait for that work (ADVICE
+    r04: it held the context lock while it waited), so the 80 launches are
+    enqueued in a fraction of the hold; every launch matches its parser's
+    oracle."""
+    import time
+    import torch
+    from gopacket_amd import _lib
+    base = pktutil.fuzz_packets(93, 3000) + pktutil.read_pcap(pktutil.GOLDEN + "/test_ethernet.pcap")[1]
+    data, off, cap = pktutil.pack(base)
+    n = len(base)
+    names = ("overrides", "eth_ip4_udp_payload", "statsassembly")
+    refs = {k: oracle_parser(CONFIGS[k]).decode(data, off, cap, nthreads=8) for k in names}
+    parsers = {k: device_parser(CONFIGS[k]) for k in names}
+    d = torch.from_numpy(data).cuda()
+    o = torch.from_numpy(off.astype(np.int64)).cuda()
+    c = torch.from_numpy(cap.astype(np.int32)).cuda()
+    streams = [torch.cuda.Stream() for _ in range(40)]
+    # calibrate the spin kernel, then hold stream 0 for ~1 s
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    torch.cuda._sleep(10_000_000)
+    e1.record()
+    torch.cuda.synchronize()
+    cycles = int(10_000_000 * 1000.0 / max(e0.elapsed_time(e1), 1e-3))
+    h0, h1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    h0.record(streams[0])
+    with torch.cuda.stream(streams[0]):
+        torch.cuda._sleep(cycles)
+    h1.record(streams[0])
+    outs = []
+    t0 = time.perf_counter()
+    for rnd in range(2):
+        for j, st in enumerate(streams):
+            k = names[(j + rnd) % 3]
+            with torch.cuda.stream(st):
+                rec = torch.empty(n * 16, dtype=torch.uint8, device="cuda")
+                err = torch.zeros(2 * n, dtype=torch.int32, device="cuda")
+                fl = torch.empty(3 * n, dtype=torch.int64, device="cuda")
+                gpu_ctx.decode_device(parsers[k], d, o, c, rec, err, fl, stream=st)
+            outs.append((k, rec, err, fl))
+    enqueue_ms = (time.perf_counter() - t0) * 1e3
+    torch.cuda.synchronize()
+    hold_ms = h0.elapsed_time(h1)
+    assert hold_ms > 300 and enqueue_ms < hold_ms / 2, (enqueue_ms, hold_ms)
+    for k, rec, err, fl in outs:
+        ref = refs[k]
+        assert np.array_equal(rec.cpu().numpy().view(_lib.RECORD_DTYPE), ref["records"]), k
+        assert np.array_equal(fl.cpu().numpy().view(np.uint64), ref["flows"]), k

@@ -59,8 +59,8 @@ def main():
         flags = 2 | (0 if streamed else 64)
 
         def skeleton():
-            assert S.gpk_probe_skeleton_idx(data.data_ptr(), off.data_ptr(), cap.data_ptr(), n, wbuf.data_ptr(), wbytes,
-                                            flags, sink.data_ptr(), stream.cuda_stream) == 0
+            assert S.gpk_probe_skeleton_idx(data.data_ptr(), off.data_ptr(), cap.data_ptr(), n, wbuf.data_ptr(),
+                                            wbuf.numel(), wbytes, flags, sink.data_ptr(), stream.cuda_stream) == 0
 
         def decode():
             if fields:
@@ -69,12 +69,15 @@ def main():
                 ctx.decode_device(parser, data, off, cap, rec, err, fl, stream=stream)
 
         def skeleton_nowrite():
-            assert S.gpk_probe_skeleton_idx(data.data_ptr(), off.data_ptr(), cap.data_ptr(), n, wbuf.data_ptr(), 0,
-                                            flags, sink.data_ptr(), stream.cuda_stream) == 0
+            assert S.gpk_probe_skeleton_idx(data.data_ptr(), off.data_ptr(), cap.data_ptr(), n, wbuf.data_ptr(),
+                                            wbuf.numel(), 0, flags, sink.data_ptr(), stream.cuda_stream) == 0
 
         def skeleton_flags(extra):
-            return lambda: S.gpk_probe_skeleton_idx(data.data_ptr(), off.data_ptr(), cap.data_ptr(), n, wbuf.data_ptr(),
-                                                    wbytes, flags | extra, sink.data_ptr(), stream.cuda_stream)
+            def go():
+                rc = S.gpk_probe_skeleton_idx(data.data_ptr(), off.data_ptr(), cap.data_ptr(), n, wbuf.data_ptr(),
+                                              wbuf.numel(), wbytes, flags | extra, sink.data_ptr(), stream.cuda_stream)
+                assert rc == 0, "skeleton form %d rejected for %d-byte outputs" % (extra, wbytes)
+            return go
 
         runs = {"skeleton": skeleton, "decode": decode}
         if a.no_write:
@@ -86,10 +89,15 @@ def main():
             runs["skeleton_writes_ring"] = skeleton_flags(128)
             runs["skeleton_writes_ring_temporal"] = skeleton_flags(128 | 8)
             runs["skeleton_writes_by_wave0"] = skeleton_flags(256)
+            if wbytes == 40:  # record + flows interleaved, one 2560-byte run per wave; and the records alone
+                runs["skeleton_writes_interleaved"] = skeleton_flags(512)
+                runs["skeleton_records_only"] = lambda: S.gpk_probe_skeleton_idx(
+                    data.data_ptr(), off.data_ptr(), cap.data_ptr(), n, wbuf.data_ptr(), wbuf.numel(), 16, flags,
+                    sink.data_ptr(), stream.cuda_stream)
             if streamed:  # a fifth wave per block that only stores (the others only read)
                 runs["skeleton_storer_wave"] = lambda: S.gpk_probe_skeleton_storer(
-                    data.data_ptr(), off.data_ptr(), cap.data_ptr(), n, wbuf.data_ptr(), wbytes, sink.data_ptr(),
-                    stream.cuda_stream)
+                    data.data_ptr(), off.data_ptr(), cap.data_ptr(), n, wbuf.data_ptr(), wbuf.numel(), wbytes,
+                    sink.data_ptr(), stream.cuda_stream)
         times = {k: [] for k in runs}
         for rnd in range(a.rounds + 1):
             for k, f in runs.items():
