@@ -886,12 +886,32 @@ std::mutex g_pin_mu;
 std::unordered_map<void*, size_t> g_pinned;  // mapped (huge-page) buffers -> their mapping length
 }  // namespace
 
+// Bytes the host can still back (MemAvailable of /proc/meminfo), or SIZE_MAX
+// when unknown.
+static size_t mem_available() {
+  FILE* f = fopen("/proc/meminfo", "r");
+  if (!f) return SIZE_MAX;
+  char line[256];
+  size_t kb = 0;
+  bool found = false;
+  while (fgets(line, sizeof line, f))
+    if (sscanf(line, "MemAvailable: %zu kB", &kb) == 1) {
+      found = true;
+      break;
+    }
+  fclose(f);
+  return found ? kb * 1024 : SIZE_MAX;
+}
+
 hipError_t gpk_pin_alloc(void** out, size_t bytes) {
   *out = nullptr;
   if (bytes >= 2 * kHuge) {
     const size_t len = (bytes + kHuge - 1) & ~(kHuge - 1);
-    // (no MAP_NORESERVE: a request the host cannot back fails here, not as a
-    // fault while it is touched)
+    // Under the default overcommit policy an anonymous mapping the host cannot
+    // back still succeeds, and touching it below would get the process
+    // OOM-killed instead of returning an error: refuse a request larger than
+    // what the host has available first.
+    if (len > mem_available()) return hipErrorOutOfMemory;
     void* m = mmap(nullptr, len + kHuge, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
     if (m != MAP_FAILED) {
       // 2 MiB-aligned, so transparent huge pages can back all of it

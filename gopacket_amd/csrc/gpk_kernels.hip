@@ -1412,7 +1412,10 @@ __device__ __forceinline__ void window_dma(const KParams& P, const WinGeo& g, ui
 
 template <bool kCompact, int O, int W = 6, bool kFields = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(O, 8))) void decode_sb_kernel(KParams P) {
-  static_assert(!kFields || 64 * 4 * W >= 1024, "the fused fields stage a half record per lane in the wave's slots");
+  // fields_store stages 48 whole 128-byte records (GPK_FIELDS_STAGE 2: 1536 dwords) or a half record per lane
+  // (1: 1024 dwords) in the wave's window slots, 4 W dwords per lane
+  static_assert(!kFields || 64 * 4 * W >= (GPK_FIELDS_STAGE == 2 ? 1536 : 1024),
+                "the fused fields' staging does not fit the wave's window slots");
   constexpr int D = GPK_SB_DEPTH;
   constexpr int kSbStride = 4 * W;  // one 16-byte cell per window chunk, no pad
   const uint32_t tid = threadIdx.x, lane = tid & 63;

@@ -428,6 +428,19 @@ static int replay_file(gpk_ctx* ctx, const gpk_parser* parser, const char* path,
       if (on) (void)pthread_setaffinity_np(pthread_self(), sizeof(*set), set);
     }
   } restore{caller_pinned, &caller_cpus};
+  // the file, its gzip stream and the record reader are released on every
+  // return, an exception's included (declared before the pipeline, whose
+  // destructor waits for the read threads that use them)
+  gpk_capreader* rd = nullptr;
+  struct Release {
+    Src* src;
+    gpk_capreader** rd;
+    ~Release() {
+      if (*rd) gpk_capreader_destroy(*rd);
+      if (src->gz) gzclose(src->gz);
+      if (src->fd >= 0) close(src->fd);
+    }
+  } release{&src, &rd};
   src.fd = open(path, O_RDONLY);
   if (src.fd < 0) {
     snprintf(stats->error, sizeof(stats->error), "open %s failed", path);
@@ -441,16 +454,12 @@ static int replay_file(gpk_ctx* ctx, const gpk_parser* parser, const char* path,
   ssize_t mk = pread(src.fd, magic, 4, 0);
   if (mk >= 2 && magic[0] == 0x1f && magic[1] == 0x8b) {  // read.go:74-84, ngread.go:80-95
     if (src.size < 10) {  // gzip.NewReader: the header read hits EOF
-      close(src.fd);
       snprintf(stats->error, sizeof(stats->error), "unexpected EOF");
       stats->reader_status = 1;
       return GPK_OK;
     }
     src.gz = gzdopen(dup(src.fd), "rb");
-    if (!src.gz) {
-      close(src.fd);
-      return GPK_ENOMEM;
-    }
+    if (!src.gz) return GPK_ENOMEM;
     gzbuffer(src.gz, 1u << 20);
     if (gzread(src.gz, magic, 4) < 4) memset(magic, 0, 4);
     gzrewind(src.gz);
@@ -460,13 +469,8 @@ static int replay_file(gpk_ctx* ctx, const gpk_parser* parser, const char* path,
     const uint32_t m = (uint32_t)magic[0] | (uint32_t)magic[1] << 8 | (uint32_t)magic[2] << 16 | (uint32_t)magic[3] << 24;
     format = m == 0x0A0D0D0Au ? GPK_CAP_PCAPNG : GPK_CAP_PCAP;
   }
-  gpk_capreader* rd = nullptr;
   int rc = gpk_capreader_create(&rd, format, opt.ng_flags);
-  if (rc) {
-    if (src.gz) gzclose(src.gz);
-    close(src.fd);
-    return rc;
-  }
+  if (rc) return rc;
 
   // ---- buffers ---------------------------------------------------------------
   // (kept in the context between calls: the pinned staging slots are ~GBs and
@@ -543,9 +547,6 @@ static int replay_file(gpk_ctx* ctx, const gpk_parser* parser, const char* path,
   }
   for (size_t i = 0; i < pl.bats.size(); i++) pl.free_bats.push_back((int)i);
   if (!good) {
-    gpk_capreader_destroy(rd);
-    if (src.gz) gzclose(src.gz);
-    close(src.fd);
     snprintf(stats->error, sizeof(stats->error), "%s", pl.herr.c_str());
     return GPK_ENOMEM;
   }
@@ -916,14 +917,10 @@ static int replay_file(gpk_ctx* ctx, const gpk_parser* parser, const char* path,
     }
   const double t_fills = now_s();
   stats->packets = packet_index;
-  {
-    const std::string e = pl.settle();  // allocations the call did not reach
-    if (!e.empty() && good) {
-      good = false;
-      pl.herr = e;
-      rc = GPK_ENOMEM;
-    }
-  }
+  // allocations the call did not reach: one that failed has cost the call
+  // nothing (every packet was delivered), so the call succeeds and only the
+  // buffers are not kept for the next one
+  const bool keep = pl.settle().empty();
   if (trace && trace[0] == '2')
     fprintf(stderr, "gpk_replay tail: delivered %.2f ms, fills %.2f, settled %.2f (from the last launch)\n",
             (t_delivered - t_tail) * 1e3, (t_fills - t_tail) * 1e3, (now_s() - t_tail) * 1e3);
@@ -932,15 +929,13 @@ static int replay_file(gpk_ctx* ctx, const gpk_parser* parser, const char* path,
   if (trace && trace[0] == '1')
     fprintf(stderr, "gpk_replay: setup %.4f s, loop %.4f s, %llu slots\n", t_loop - t_start, now_s() - t_loop,
             (unsigned long long)stats->slots);
-  gpk_capreader_destroy(rd);
-  if (src.gz) gzclose(src.gz);
-  close(src.fd);
   if (!good) {
     snprintf(stats->error, sizeof(stats->error), "%s", pl.herr.c_str());
     return rc ? rc : GPK_EHIP;
   }
-  for (auto& s : pl.slots) good = good && pl.ok(hipStreamSynchronize(s.stream), "hipStreamSynchronize");
-  if (good)  // idle buffers for the next call
+  for (auto& s : pl.slots)
+    if (s.stream) good = good && pl.ok(hipStreamSynchronize(s.stream), "hipStreamSynchronize");
+  if (good && keep)  // idle buffers for the next call
     gpk_ctx_replay_put(ctx, new Cached{C, R, P, dev_walk, std::move(pl.slots), std::move(pl.bats)}, free_cached);
   return rc;
 }

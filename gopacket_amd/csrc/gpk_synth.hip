@@ -341,8 +341,11 @@ __global__ __launch_bounds__(256) void probe_skeleton_idx_kernel(const uint8_t* 
   auto store_out = [&]() {
     if (flags & 16) __syncthreads();  // the block's four waves store together
     if (w0 + lane < n) {
-      // flags & 128: the outputs of packet i at i mod 2^20 (a 40 MiB ring that stays on chip) instead of i
-      const uint64_t q = (flags & 128) ? ((w0 + lane) & ((1u << 20) - 1)) : w0 + lane;
+      // flags & 128: the outputs of packet i at i mod 2^20 (a 40 MiB ring that stays on chip) instead of i;
+      // flags & 1024: at i mod 2^14 (640 KiB: a ring that stays in each XCD's L2)
+      const uint64_t q = (flags & 1024)  ? ((w0 + lane) & ((1u << 14) - 1))
+                         : (flags & 128) ? ((w0 + lane) & ((1u << 20) - 1))
+                                         : w0 + lane;
       uint8_t* r = wbuf + q * 16;
       uint64_t* f = reinterpret_cast<uint64_t*>(wbuf + 16 * n) + (q - (w0 + lane));
       if (flags & 8) {  // default (temporal) store policy

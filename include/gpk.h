@@ -414,7 +414,13 @@ int gpk_decoded_list(gpk_ctx* ctx, const gpk_parser* p, const gpk_batch* batch,
 int gpk_decoded_list_host(gpk_ctx* ctx, const gpk_parser* p, const uint8_t* pkt, uint32_t caplen,
                           int64_t* out_types, uint32_t cap, uint32_t* out_n);
 
-/* Pinned host memory for gpk_decode_batch_host (hipHostMalloc). */
+/* Page-locked host memory for gpk_decode_batch_host and the replay paths:
+ * below 4 MiB hipHostMalloc; from 4 MiB an anonymous 2 MiB-aligned mapping
+ * (transparent huge pages) faulted in on up to 8 threads and registered with
+ * hipHostRegister. Either way it is ordinary host memory for HIP copies, not a
+ * device-mapped (zero-copy) pointer, and it must be released with
+ * gpk_host_free (never hipHostFree / free). A request larger than the host's
+ * MemAvailable fails with GPK_EHIP (hipErrorOutOfMemory) instead of faulting. */
 int gpk_host_alloc(void** out, size_t bytes);
 int gpk_host_free(void* p);
 

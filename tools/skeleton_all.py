@@ -88,6 +88,8 @@ def main():
             runs["skeleton_writes_first"] = skeleton_flags(32)
             runs["skeleton_writes_ring"] = skeleton_flags(128)
             runs["skeleton_writes_ring_temporal"] = skeleton_flags(128 | 8)
+            runs["skeleton_writes_l2ring_temporal"] = skeleton_flags(1024 | 8)
+            runs["skeleton_writes_l2ring"] = skeleton_flags(1024)
             runs["skeleton_writes_by_wave0"] = skeleton_flags(256)
             if wbytes == 40:  # record + flows interleaved, one 2560-byte run per wave; and the records alone
                 runs["skeleton_writes_interleaved"] = skeleton_flags(512)
