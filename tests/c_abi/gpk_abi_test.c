@@ -27,6 +27,9 @@ _Static_assert(sizeof(gpk_layout) == 64, "gpk_layout is 64 bytes");
 _Static_assert(sizeof(gpk_batch) == 40, "gpk_batch is 5 words");
 _Static_assert(sizeof(gpk_results) == 32, "gpk_results is 4 pointers");
 _Static_assert(sizeof(gpk_fields) == 128, "gpk_fields is 128 bytes");
+_Static_assert(offsetof(gpk_fields, present) == 0 && sizeof(((gpk_fields*)0)->present) == 1 &&
+                   offsetof(gpk_fields, hbh_opt_map) == 1,
+               "gpk_fields presence byte and HopByHop option map (ABI 2)");
 _Static_assert(offsetof(gpk_fields, eth_dst) == 8 && offsetof(gpk_fields, d1q_tci) == 20, "gpk_fields link part");
 _Static_assert(offsetof(gpk_fields, ip4_length) == 28 && offsetof(gpk_fields, ip6_flow_label) == 40 &&
                    offsetof(gpk_fields, ip4_src) == 48 && offsetof(gpk_fields, ip6_dst) == 72,

@@ -26,7 +26,7 @@ def fields_of(first, decoders, pkts):
 
 def test_fields_record_layout():
     assert _lib.FIELDS_DTYPE.itemsize == 128
-    for name, off in (("eth_type", 4), ("eth_dst", 8), ("d1q_tci", 20), ("ip4_length", 28), ("ip6_flow_label", 40),
+    for name, off in (("present", 0), ("hbh_opt_map", 1), ("eth_type", 4), ("eth_dst", 8), ("d1q_tci", 20), ("ip4_length", 28), ("ip6_flow_label", 40),
                       ("ip4_src", 48), ("ip6_src", 56), ("ip6_dst", 72), ("tcp_seq", 92), ("tcp_flags", 100),
                       ("udp_checksum", 114), ("ip4_start", 116), ("tcp_start", 117), ("ip4_opt_map", 118),
                       ("tcp_opt_map", 123)):
