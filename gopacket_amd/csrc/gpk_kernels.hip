@@ -130,9 +130,6 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 #ifndef GPK_DIAG_FIELDS
 #define GPK_DIAG_FIELDS 0  // timing only: 1 = fused fields computed, not stored; 2 = stored, not read
 #endif
-#ifndef GPK_STORE_BLOCK
-#define GPK_STORE_BLOCK 0  // records and flows staged in LDS per block and stored by its first wave (A/B)
-#endif
 #ifndef GPK_PB_NULL
 #define GPK_PB_NULL 0  // timing only: phase-B stream loads read nothing (zero-record descriptors)
 #endif
@@ -1009,57 +1006,6 @@ __device__ __forceinline__ void fields_store(const KParams& P, const uint32_t (&
   asm volatile("" ::: "memory");
 }
 
-// GPK_STORE_BLOCK: the block's outputs leave from its first wave. Each lane
-// puts its record and flows into its wave's window slots once the wave has
-// read its windows for the last time (records at dword 4 l, flow j of lane l
-// at dword 256 + 128 j + 2 l of the wave's slots); after a block barrier wave
-// 0 stores the block's 256 records as four 1 KiB runs (4 KiB contiguous) and
-// each flow array's 2 KiB as two 16-byte-per-lane stores (four 8-byte ones
-// when the array is not 16-byte aligned). All lanes of the block call it.
-template <int kSlotStride>
-__device__ __forceinline__ void block_store(const KParams& P, uint32_t region_dw, uint32_t lane, bool active,
-                                            const u32x4& rec, bool flows, uint64_t lf, uint64_t nf, uint64_t tf) {
-  asm volatile("" ::: "memory");
-  *reinterpret_cast<u32x4*>(gpk_smem + region_dw + 4 * lane) = rec;
-  if (flows) {
-    *reinterpret_cast<uint64_t*>(gpk_smem + region_dw + 256 + 2 * lane) = lf;
-    *reinterpret_cast<uint64_t*>(gpk_smem + region_dw + 384 + 2 * lane) = nf;
-    *reinterpret_cast<uint64_t*>(gpk_smem + region_dw + 512 + 2 * lane) = tf;
-  }
-  (void)active;
-  __syncthreads();
-  if (threadIdx.x >= 64) return;
-  constexpr uint32_t kWaveDw = 64u * kSlotStride;
-  const uint64_t b0 = (uint64_t)blockIdx.x * kBlock;
-  u32x4* R = reinterpret_cast<u32x4*>(P.records) + b0;
-#pragma unroll
-  for (uint32_t k = 0; k < kWaves; k++)
-    if (b0 + 64 * k + lane < P.n)
-      __builtin_nontemporal_store(*reinterpret_cast<const u32x4*>(gpk_smem + k * kWaveDw + 4 * lane), R + 64 * k + lane);
-  if (!flows) return;
-#pragma unroll
-  for (uint32_t j = 0; j < 3; j++) {
-    uint64_t* F = P.flows + j * P.n + b0;
-    if (((uintptr_t)F & 15) == 0) {  // two flows per lane, 16-byte stores
-#pragma unroll
-      for (uint32_t h = 0; h < 2; h++) {
-        const uint32_t q = 128 * h + 2 * lane, w = q >> 6, i = q & 63;
-        const u32x4 v = *reinterpret_cast<const u32x4*>(gpk_smem + w * kWaveDw + 256 + 128 * j + 2 * i);
-        if (b0 + q + 1 < P.n)
-          __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(F + q));
-        else if (b0 + q < P.n)
-          __builtin_nontemporal_store((uint64_t)v.x | (uint64_t)v.y << 32, F + q);
-      }
-    } else {
-#pragma unroll
-      for (uint32_t k = 0; k < kWaves; k++)
-        if (b0 + 64 * k + lane < P.n)
-          __builtin_nontemporal_store(
-              *reinterpret_cast<const uint64_t*>(gpk_smem + k * kWaveDw + 256 + 128 * j + 2 * lane), F + 64 * k + lane);
-    }
-  }
-}
-
 template <bool kL4, bool kLayout, class TT, bool kKeys, int W, int O, int AL, int kSlotStride = slot_dw_of<W, AL>(),
           int kEarly = -1, bool kSB = false, bool kFields = false>
 __device__ __forceinline__ void decode_packet(const KParams& P, const TT& T, uint64_t i, bool active, uint64_t off,
@@ -1124,9 +1070,6 @@ __device__ __forceinline__ void decode_packet(const KParams& P, const TT& T, uin
                 ((q.nlayers > GPK_ST_NLAYERS_MASK ? GPK_ST_NLAYERS_MASK : q.nlayers) << GPK_ST_NLAYERS_SHIFT);
   uint32_t ip4c = 0, l4c = 0;
 
-  // the block stores the outputs (GPK_STORE_BLOCK): the flows stay in registers until then
-  constexpr bool kBlockStore = GPK_STORE_BLOCK && !kLayout && !kKeys && !kFields;
-  uint64_t bl_lf = 0, bl_nf = 0, bl_tf = 0;
   // L4 checksum job: segment [js, je) of the batch, pseudo-header sum jinit
   uint64_t js = 0, je = 0;
   uint32_t jinit = 0, jexist = 0;
@@ -1171,11 +1114,7 @@ __device__ __forceinline__ void decode_packet(const KParams& P, const TT& T, uin
       tflow = ft ? tflow : 0;
       st |= (fl ? GPK_ST_LINK_FLOW : 0u) | (fn ? GPK_ST_NET_FLOW : 0u) |
             (fn && nk == GPK_DEC_IPV6 ? GPK_ST_NET_IPV6 : 0u) | (ft ? GPK_ST_TRANSPORT_FLOW : 0u);
-      if (kBlockStore) {
-        bl_lf = lflow;
-        bl_nf = nflow;
-        bl_tf = tflow;
-      } else if (P.flows) {
+      if (P.flows) {
         __builtin_nontemporal_store(lflow, P.flows + i);
         __builtin_nontemporal_store(nflow, P.flows + P.n + i);
         __builtin_nontemporal_store(tflow, P.flows + 2 * P.n + i);
@@ -1351,11 +1290,6 @@ __device__ __forceinline__ void decode_packet(const KParams& P, const TT& T, uin
       const bool udp = (st & GPK_ST_L4_UDP) != 0;
       if (l4c == jexist || (udp && jexist == 0)) st |= GPK_ST_L4_VALID;
     }
-  }
-  if (kBlockStore) {
-    block_store<kSlotStride>(P, slot_dw - lane * kSlotStride, lane, active, u32x4{lay_lo, lay_hi, st, ip4c | (l4c << 16)},
-                             P.flows && (P.outputs & GPK_OUT_FLOWS), bl_lf, bl_nf, bl_tf);
-    return;
   }
   if (active)  // written once, never read back here: non-temporal
     __builtin_nontemporal_store(u32x4{lay_lo, lay_hi, st, ip4c | (l4c << 16)}, reinterpret_cast<u32x4*>(P.records) + i);

@@ -23,6 +23,9 @@ def main():
     ap.add_argument("--seeds", type=int, default=20)
     ap.add_argument("--first-seed", type=int, default=5000)
     ap.add_argument("--packets", type=int, default=30000)
+    ap.add_argument("--hydrate", type=int, default=0, metavar="K",
+                    help="every K-th seed also: Hydrate from the one-launch fields result against Hydrate from "
+                         "layouts, struct by struct (tests/hydrate_cases.compare), over the seed's first 4000 packets")
     ap.add_argument("--layouts", default="", type=lambda x: [y for y in x.split(",") if y],
                     help="placements to cycle through: packed, shuffled, reversed, wave_shuffled, gapped, sparse_mix")
     a = ap.parse_args()
@@ -53,6 +56,16 @@ def main():
             if seed % 3 == 0 and layout == "packed":
                 fields_check(ctx, name, packets, align=align)
                 n_batches += 2
+        if a.hydrate and seed % a.hydrate == 0:
+            import hydrate_cases as H
+            from gopacket_amd import gopacket as G
+            sub = packets[:4000] + H.hbh_packets(seed, 500)
+            batch = G.PacketBatch.from_packets(sub)
+            pa, pb = H.parser(), H.parser()
+            pa._ctx = pb._ctx = ctx
+            ra, rb = pa.DecodeBatch(batch, layouts=True), pb.DecodeBatch(batch, fields=True)
+            H.compare(ra, rb, pa, pb, range(len(sub)))
+            n_batches += 1
         print("seed %d (%s, align %d): %d parsers x 2 bit-exact, %.0f s" % (seed, layout, align, len(CONFIGS),
                                                                           time.time() - t0),
               flush=True)
