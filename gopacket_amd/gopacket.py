@@ -37,6 +37,17 @@ class LayerType(int):
         return "LayerType(%s)" % self.String()
 
 
+class LayerClass(list):
+    """layerclass.go:11-107: the LayerTypes a DecodingLayer can decode
+    (CanDecode); a single LayerType or a LayerClassSlice in Go."""
+
+    def Contains(self, t):
+        return int(t) in [int(x) for x in self]
+
+    def LayerTypes(self):
+        return list(self)
+
+
 LayerTypeZero = LayerType(0)
 LayerTypeDecodeFailure = LayerType(1)
 LayerTypePayload = LayerType(2)
@@ -192,7 +203,7 @@ class Payload:
         self.data = b""
 
     def CanDecode(self):
-        return [LayerTypePayload]
+        return LayerClass([LayerTypePayload])
 
     def LayerType(self):
         return LayerTypePayload
@@ -222,7 +233,7 @@ class Fragment(Payload):
     kind = _lib.DEC_FRAGMENT
 
     def CanDecode(self):
-        return [LayerTypeFragment]
+        return LayerClass([LayerTypeFragment])
 
     def LayerType(self):
         return LayerTypeFragment
@@ -269,36 +280,190 @@ def _default_ctx():
     return _DEFAULT_CTX
 
 
+# ---- decoding layer containers (parser.go:48-169) ------------------------------
+
+
+class DecodingLayerContainer:
+    """parser.go:56-67: LayerType -> DecodingLayer. Put registers every type of
+    the layer's CanDecode() (a later Put overrides); Decoder looks one up;
+    LayersDecoder returns the DecodingLayerFunc of the container. The three
+    forms differ in their lookup structure only; the device decodes with
+    the container's contents either way (layers_decoder.go:18-100)."""
+
+    def LayersDecoder(self, first, df):
+        """parser.go:96-99 / 138-141 / 166-169: a DecodingLayerFunc over this
+        container starting at `first`, reporting Truncated to df."""
+        return _LayersDecoder(self, LayerType(first), df)
+
+    def _instances(self):
+        """Each registered DecodingLayer once, by its device decoder kind
+        (_types: the subclass's (LayerType, layer) pairs)."""
+        out = {}
+        for _, d in self._types():
+            if d is not None:
+                out[d.kind] = d
+        return out
+
+
+class DecodingLayerSparse(DecodingLayerContainer):
+    """parser.go:74-107: a slice indexed by the LayerType value."""
+
+    def __init__(self, layers=None):
+        self._slots = list(layers or [])
+
+    def Put(self, d):
+        types = [int(t) for t in d.CanDecode().LayerTypes()]
+        slots = self._slots + [None] * max(0, max(types) + 1 - len(self._slots))
+        for t in types:
+            slots[t] = d
+        return DecodingLayerSparse(slots)
+
+    def Decoder(self, typ):
+        t = int(typ)
+        d = self._slots[t] if 0 <= t < len(self._slots) else None
+        return d, d is not None
+
+    def _types(self):
+        return [(t, d) for t, d in enumerate(self._slots) if d is not None]
+
+
+class DecodingLayerArray(DecodingLayerContainer):
+    """parser.go:112-142: (type, layer) pairs searched linearly."""
+
+    def __init__(self, elems=None):
+        self._elems = list(elems or [])
+
+    def Put(self, d):
+        elems = list(self._elems)
+        for t in d.CanDecode().LayerTypes():
+            for k, (typ, _) in enumerate(elems):
+                if typ == int(t):
+                    elems[k] = (typ, d)
+                    break
+            else:
+                elems.append((int(t), d))
+        return DecodingLayerArray(elems)
+
+    def Decoder(self, typ):
+        for t, d in self._elems:
+            if t == int(typ):
+                return d, True
+        return None, False
+
+    def _types(self):
+        return list(self._elems)
+
+
+class DecodingLayerMap(DecodingLayerContainer):
+    """parser.go:147-169: a map keyed by LayerType (the parser's default)."""
+
+    def __init__(self, m=None):
+        self._m = dict(m or {})
+
+    def Put(self, d):
+        m = dict(self._m)
+        for t in d.CanDecode().LayerTypes():
+            m[int(t)] = d
+        return DecodingLayerMap(m)
+
+    def Decoder(self, typ):
+        d = self._m.get(int(typ))
+        return d, d is not None
+
+    def _types(self):
+        return list(self._m.items())
+
+
+class _NilDecodeFeedback:
+    """decode.go:21-26"""
+
+    def SetTruncated(self):
+        pass
+
+
+NilDecodeFeedback = _NilDecodeFeedback()
+
+
+class _LayersDecoder:
+    """LayersDecoder (layers_decoder.go:11-101) for one packet on the device:
+    returns (LayerTypeZero, None) on success, (the first LayerType with no
+    decoder, None), or (LayerTypeZero, the decoder's error). A decoder's panic
+    is not recovered here (DecodeLayers recovers it, parser.go:329-333): it
+    raises GoPanic. `decoded` is truncated and refilled, except when `first`
+    has no decoder (returned at once, layers_decoder.go:12-16)."""
+
+    def __init__(self, dlc, first, df):
+        self.dlc, self.first, self.df = dlc, first, df
+        self._p = DecodingLayerParser(first)
+        self._p.SetDecodingLayerContainer(dlc)
+        self._p.IgnorePanic = True  # panics raise (GoPanic) instead of becoming errors
+
+    def __call__(self, data, decoded):
+        if not self.dlc.Decoder(self.first)[1]:
+            return self.first, None
+        if self.df is not None and hasattr(self.df, "_ctx"):
+            self._p._ctx = self._p._ctx or self.df._ctx
+        res = self._p.DecodeBatch(PacketBatch.from_packets([data]), layouts=True)
+        err = res.Hydrate(0, decoded)
+        if res.Truncated(0) and self.df is not None:
+            self.df.SetTruncated()
+        if isinstance(err, UnsupportedLayerType):
+            return err.typ, None
+        return LayerTypeZero, err
+
+
 class DecodingLayerParser:
     """parser.go:182-317 over the GPU engine.
 
-    Differences that are not semantic: the container is always the Map form
-    (Sparse/Array/Map decode identically, layers_decoder.go:18-100); layer
-    structs are refreshed from device results, so per-packet state that the
-    reference leaves stale across calls (TCP.Multipath, IPv4.Padding) is
-    per packet here (parity notes P6)."""
+    Differences that are not semantic: the device decodes the container's
+    layers whichever container form holds them (Sparse/Array/Map decode
+    identically, layers_decoder.go:18-100); layer structs are refreshed from
+    device results, so per-packet state that the reference leaves stale
+    across calls (TCP.Multipath, IPv4.Padding) is per packet here
+    (parity notes P6)."""
 
     def __init__(self, first, *decoders, ctx=None):
         self.first = LayerType(first)
         self.IgnorePanic = False
         self.IgnoreUnsupported = False
         self.Truncated = False
-        self._decoders = {}  # kind -> instance (last Put wins)
         self._ctx = ctx
-        self._cfg = None
+        dlc = DecodingLayerMap()  # NewDecodingLayerParser's default container (parser.go:226)
         for d in decoders:
-            self.AddDecodingLayer(d)
+            dlc = dlc.Put(d)
+        self.SetDecodingLayerContainer(dlc)
+
+    def SetDecodingLayerContainer(self, dlc):
+        """parser.go:238-241: replaces every registered decoder."""
+        self._dlc = dlc
+        self._decoders = dlc._instances()  # kind -> instance
+        self._cfg = None
 
     def AddDecodingLayer(self, d):
-        self._decoders[d.kind] = d
-        self._cfg = None
+        """parser.go:200-202"""
+        self.SetDecodingLayerContainer(self._dlc.Put(d))
+
+    def SetTruncated(self):
+        """parser.go:207-209 (the parser is its decoders' DecodeFeedback)"""
+        self.Truncated = True
 
     def _config(self, outputs=_lib.OUT_ALL):
         from .engine import ParserConfig
-        key = (tuple(sorted(self._decoders)), self.IgnorePanic, self.IgnoreUnsupported, outputs)
+        from . import layers
+        key = (tuple(sorted(self._decoders)), self.IgnorePanic, self.IgnoreUnsupported, outputs,
+               layers._registry_version[0])
         if self._cfg is None or self._cfg[0] != key:
             p = ParserConfig(int(self.first), sorted(self._decoders), ignore_panic=self.IgnorePanic,
                              ignore_unsupported=self.IgnoreUnsupported, outputs=outputs)
+            ed = layers._registry_edits()  # EthernetTypeMetadata / IPProtocolMetadata edits, Register*PortLayerType
+            for v, lt in ed["ethertype"]:
+                p.set_ethertype(v, lt)
+            for v, lt in ed["ipprotocol"]:
+                p.set_ipprotocol(v, lt)
+            for v, lt in ed["tcp_port"]:
+                p.set_tcp_port(v, lt)
+            for v, lt in ed["udp_port"]:
+                p.set_udp_port(v, lt)
             self._cfg = (key, p)
         return self._cfg[1]
 
@@ -569,5 +734,5 @@ class BatchResult:
             inst = scratch.setdefault(k, type(self.parser._decoders[k])())
             inst._hydrate(pkt[s:e])
             s = s + inst._poff
-            e = s + len(inst.LayerPayload() if hasattr(inst, "LayerPayload") else b"")
+            e = s + len(inst.LayerPayload())
         return out

@@ -22,8 +22,8 @@ from dataclasses import dataclass, field
 from typing import List, Optional
 
 from . import _lib
-from .gopacket import (ChecksumVerificationResult, Flow, LayerType, NewFlow, EndpointIPv4, EndpointIPv6,
-                       EndpointMAC, EndpointTCPPort, EndpointUDPPort, LayerTypePayload)
+from .gopacket import (ChecksumVerificationResult, Flow, LayerClass, LayerType, NewFlow, EndpointIPv4, EndpointIPv6,
+                       EndpointMAC, EndpointTCPPort, EndpointUDPPort, LayerTypeFragment, LayerTypePayload)
 
 _REG = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "registry_gen.json")))
 
@@ -54,6 +54,9 @@ LayerTypeDNS = _lt("DNS")
 LayerTypeTLS = _lt("TLS")
 LayerTypeModbus = _lt("Modbus")
 LayerTypeENIP = _lt("ENIP")
+# layertypes.go:200-206
+LayerClassIPv6Extension = LayerClass([LayerTypeIPv6HopByHop, LayerTypeIPv6Routing, LayerTypeIPv6Fragment,
+                                      LayerTypeIPv6Destination])
 
 # ---- enums (layers/enums.go) -------------------------------------------------
 EthernetTypeLLC = 0x0000
@@ -75,11 +78,128 @@ _ETHERTYPE_NAMES = {v: n for v, lt, n in _REG["ethertype"]}
 
 
 def IPProtocolString(p):
-    return _IPPROTO_NAMES.get(p, "UnknownIPProtocol")
+    return IPProtocolMetadata[p].Name
 
 
 def EthernetTypeString(t):
-    return _ETHERTYPE_NAMES.get(t, "UnknownEthernetType")
+    return EthernetTypeMetadata[t].Name
+
+
+# ---- next-layer tables (layers/enums.go:294-390, ports.go:54-183) -----------
+# The registry the reference's NextLayerType methods consult, as the host
+# mirror: EthernetTypeMetadata / IPProtocolMetadata (EnumMetadata per value,
+# enums.go:294-353, editable as in Go) and the TCP/UDP port overrides of
+# RegisterTCPPortLayerType / RegisterUDPPortLayerType (ports.go:95-104,
+# 174-183) over the port switches. Every DecodingLayerParser built after an
+# edit sends the edited entries to its device parser (gpk_parser_set_*), so
+# the device's NextLayerType lookups and the structs' NextLayerType() agree.
+_registry_version = [0]
+
+
+class EnumMetadata:
+    """enums.go EnumMetadata: the LayerType a value decodes as, and its name."""
+
+    def __init__(self, LayerType=0, Name=""):
+        self.LayerType, self.Name = LayerType, Name
+
+    def __repr__(self):
+        return "EnumMetadata(LayerType=%d, Name=%r)" % (int(self.LayerType), self.Name)
+
+
+class _EnumTable:
+    """A [n]EnumMetadata array: reads the generated defaults, keeps edits."""
+
+    def __init__(self, rows, n, unknown):
+        self._default = {v: (LayerType(lt), name) for v, lt, name in rows}
+        self._n, self._unknown, self._edits = n, unknown, {}
+
+    def __getitem__(self, v):
+        v = int(v)
+        if not 0 <= v < self._n:
+            raise IndexError(v)
+        if v in self._edits:
+            return self._edits[v]
+        lt, name = self._default.get(v, (LayerType(0), self._unknown))
+        return EnumMetadata(lt, name)
+
+    def __setitem__(self, v, meta):
+        v = int(v)
+        if not 0 <= v < self._n:
+            raise IndexError(v)
+        self._edits[v] = meta
+        _registry_version[0] += 1
+
+    def _changed(self):
+        """(value, LayerType) of every edited entry."""
+        return [(v, int(m.LayerType)) for v, m in sorted(self._edits.items())]
+
+
+EthernetTypeMetadata = _EnumTable(_REG["ethertype"], 65536, "UnknownEthernetType")
+IPProtocolMetadata = _EnumTable(_REG["ipprotocol"], 256, "UnknownIPProtocol")
+
+_TCP_SWITCH = {p: LayerType(lt) for p, lt in _REG["tcp_port_switch"]}
+_UDP_SWITCH = {p: LayerType(lt) for p, lt in _REG["udp_port_switch"]}
+_tcp_override = {p: LayerType(lt) for p, lt in _REG["tcp_port_override"]}  # init() registrations
+_udp_override = {p: LayerType(lt) for p, lt in _REG["udp_port_override"]}
+_tcp_user, _udp_user = {}, {}
+
+
+def RegisterTCPPortLayerType(port, layerType):
+    """ports.go:99-104"""
+    _tcp_override[int(port)] = _tcp_user[int(port)] = LayerType(layerType)
+    _registry_version[0] += 1
+
+
+def RegisterUDPPortLayerType(port, layerType):
+    """ports.go:178-183"""
+    _udp_override[int(port)] = _udp_user[int(port)] = LayerType(layerType)
+    _registry_version[0] += 1
+
+
+def EthernetTypeLayerType(t):
+    """EthernetType.LayerType() (enums_generated.go:76-86)."""
+    return LayerType(EthernetTypeMetadata[t].LayerType)
+
+
+def IPProtocolLayerType(p):
+    """IPProtocol.LayerType() (enums_generated.go:146-156)."""
+    return LayerType(IPProtocolMetadata[p].LayerType)
+
+
+def TCPPortLayerType(port):
+    """TCPPort.LayerType() (ports.go:54-93): the override, else the switch, else Payload."""
+    port = int(port)
+    if port in _tcp_override:
+        return _tcp_override[port]
+    return _TCP_SWITCH.get(port, LayerTypePayload)
+
+
+def UDPPortLayerType(port):
+    """UDPPort.LayerType() (ports.go:121-172)."""
+    port = int(port)
+    if port in _udp_override:
+        return _udp_override[port]
+    return _UDP_SWITCH.get(port, LayerTypePayload)
+
+
+def _reset_registry():
+    """Back to the reference's registry after init() (tests)."""
+    EthernetTypeMetadata._edits.clear()
+    IPProtocolMetadata._edits.clear()
+    _tcp_user.clear()
+    _udp_user.clear()
+    _tcp_override.clear()
+    _tcp_override.update({p: LayerType(lt) for p, lt in _REG["tcp_port_override"]})
+    _udp_override.clear()
+    _udp_override.update({p: LayerType(lt) for p, lt in _REG["udp_port_override"]})
+    _registry_version[0] += 1
+
+
+def _registry_edits():
+    """What a device parser must be told beyond its default tables."""
+    return dict(ethertype=EthernetTypeMetadata._changed(), ipprotocol=IPProtocolMetadata._changed(),
+                tcp_port=sorted((p, int(lt)) for p, lt in _tcp_user.items()),
+                udp_port=sorted((p, int(lt)) for p, lt in _udp_user.items()))
 
 
 def _be16(b, o):
@@ -114,7 +234,7 @@ class Ethernet(BaseLayer):
         return LayerTypeEthernet
 
     def CanDecode(self):
-        return [LayerTypeEthernet]
+        return LayerClass([LayerTypeEthernet])
 
     def _hydrate(self, d):
         self.DstMAC = d[0:6]
@@ -135,6 +255,10 @@ class Ethernet(BaseLayer):
         self.Contents, self.Payload = pkt[s:s + 14], pkt[s + 14:payload_end(_lib.DEC_ETHERNET, pkt, s, e, f)]
         self._poff = 14
 
+    def NextLayerType(self):
+        """ethernet.go:111-113"""
+        return EthernetTypeLayerType(self.EthernetType)
+
     def LinkFlow(self):
         return NewFlow(EndpointMAC, self.SrcMAC, self.DstMAC)
 
@@ -153,7 +277,7 @@ class Dot1Q(BaseLayer):
         return LayerTypeDot1Q
 
     def CanDecode(self):
-        return [LayerTypeDot1Q]
+        return LayerClass([LayerTypeDot1Q])
 
     def _hydrate(self, d):
         self.Priority = (d[0] & 0xE0) >> 5
@@ -169,6 +293,10 @@ class Dot1Q(BaseLayer):
         self.Type = int(f["d1q_type"])
         self.Contents, self.Payload = pkt[s:s + 4], pkt[s + 4:e]
         self._poff = 4
+
+    def NextLayerType(self):
+        """dot1q.go:49-51"""
+        return EthernetTypeLayerType(self.Type)
 
 
 @dataclass
@@ -205,7 +333,7 @@ class IPv4(BaseLayer, _Checksummed):
         return LayerTypeIPv4
 
     def CanDecode(self):
-        return [LayerTypeIPv4]
+        return LayerClass([LayerTypeIPv4])
 
     def _hydrate(self, d):
         self.Length = _be16(d, 2)
@@ -258,6 +386,12 @@ class IPv4(BaseLayer, _Checksummed):
             self.Padding = padding
         self._poff = hl
 
+    def NextLayerType(self):
+        """ip4.go:277-282: a fragment (MoreFragments or an offset) decodes as Fragment"""
+        if self.Flags & 1 or self.FragOffset != 0:
+            return LayerTypeFragment
+        return IPProtocolLayerType(self.Protocol)
+
     def NetworkFlow(self):
         return NewFlow(EndpointIPv4, self.SrcIP, self.DstIP)
 
@@ -296,7 +430,7 @@ class IPv6(BaseLayer, _Checksummed):
         return LayerTypeIPv6
 
     def CanDecode(self):
-        return [LayerTypeIPv6]
+        return LayerClass([LayerTypeIPv6])
 
     def _hydrate(self, d):
         self.Version = d[0] >> 4
@@ -345,6 +479,12 @@ class IPv6(BaseLayer, _Checksummed):
             self.HopByHop = self.hbh
         self._poff = ipv6_payload_start(pkt, s, f) - s
         self.Payload = pkt[s + self._poff:payload_end(_lib.DEC_IPV6, pkt, s, e, f)]
+
+    def NextLayerType(self):
+        """ip6.go:286-291"""
+        if self.HopByHop is not None:
+            return IPProtocolLayerType(self.HopByHop.NextHeader)
+        return IPProtocolLayerType(self.NextHeader)
 
     def NetworkFlow(self):
         return NewFlow(EndpointIPv6, self.SrcIP, self.DstIP)
@@ -452,7 +592,11 @@ class IPv6ExtensionSkipper(BaseLayer):
         self.NextHeader = 0
 
     def CanDecode(self):
-        return [LayerTypeIPv6HopByHop, LayerTypeIPv6Routing, LayerTypeIPv6Fragment, LayerTypeIPv6Destination]
+        return LayerClassIPv6Extension
+
+    def NextLayerType(self):
+        """ip6.go:458-461"""
+        return IPProtocolLayerType(self.NextHeader)
 
     def _hydrate(self, d):
         actual = d[1] * 8 + 8
@@ -499,7 +643,7 @@ class TCP(BaseLayer, _Checksummed):
         return LayerTypeTCP
 
     def CanDecode(self):
-        return [LayerTypeTCP]
+        return LayerClass([LayerTypeTCP])
 
     def _hydrate(self, d):
         self.SrcPort, self.DstPort = _be16(d, 0), _be16(d, 2)
@@ -548,6 +692,11 @@ class TCP(BaseLayer, _Checksummed):
             self.Multipath = True
         self._poff = ds
 
+    def NextLayerType(self):
+        """tcp.go:591-597: the destination port's type, else the source port's"""
+        lt = TCPPortLayerType(self.DstPort)
+        return TCPPortLayerType(self.SrcPort) if lt == LayerTypePayload else lt
+
     def TransportFlow(self):
         return NewFlow(EndpointTCPPort, self.sPort, self.dPort)
 
@@ -585,7 +734,7 @@ class UDP(BaseLayer, _Checksummed):
         return LayerTypeUDP
 
     def CanDecode(self):
-        return [LayerTypeUDP]
+        return LayerClass([LayerTypeUDP])
 
     def _hydrate(self, d):
         self.SrcPort, self.DstPort = _be16(d, 0), _be16(d, 2)
@@ -604,6 +753,11 @@ class UDP(BaseLayer, _Checksummed):
         self.Length, self.Checksum = int(f["udp_length"]), int(f["udp_checksum"])
         self.Contents, self.Payload = pkt[s:s + 8], pkt[s + 8:payload_end(_lib.DEC_UDP, pkt, s, e, f)]
         self._poff = 8
+
+    def NextLayerType(self):
+        """udp.go:114-119"""
+        lt = UDPPortLayerType(self.DstPort)
+        return lt if lt != LayerTypePayload else UDPPortLayerType(self.SrcPort)
 
     def TransportFlow(self):
         return NewFlow(EndpointUDPPort, self.sPort, self.dPort)

@@ -129,3 +129,77 @@ def test_decode_batch_matches_decode_layers(gp):
         assert h == (eth.LinkFlow().FastHash(), ip4.NetworkFlow().FastHash(), tcp.TransportFlow().FastHash())
     assert res.FlowHashes(0) == res.FlowHashes(1)  # opposite directions, symmetric hash
     assert np.count_nonzero([gopacket.LayerTypePayload in res.Decoded(i) for i in range(10)]) == 3
+
+
+# layers/decode_test.go:1045-1077 testDecodingLayerContainer over Map / Sparse / Array,
+# and decode_test.go:1033-1043 TestDecodingLayerParserFullTCPPacket
+@pytest.mark.parametrize("form", ["DecodingLayerMap", "DecodingLayerSparse", "DecodingLayerArray"])
+def test_decoding_layer_container(gp, form):
+    gopacket, L, ctx = gp
+    dlc = getattr(gopacket, form)(None)
+    dlc = dlc.Put(L.Ethernet())
+    dlc = dlc.Put(L.IPv4())
+    dlc = dlc.Put(L.TCP())
+    dlc = dlc.Put(gopacket.Payload())
+    decoded = [gopacket.LayerTypeZero]
+    df = gopacket.DecodingLayerParser(L.LayerTypeEthernet, ctx=ctx)  # just as a DecodeFeedback
+    decoder = dlc.LayersDecoder(L.LayerTypeEthernet, df)
+    typ, err = decoder(pktutil.golden_bytes("simple_tcp"), decoded)
+    assert err is None and typ == gopacket.LayerTypeZero
+    assert len(decoded) == 4
+    # the same container behind a parser (decode_test.go:219-232), both panic modes
+    for ignore in (True, False):
+        p = gopacket.DecodingLayerParser(L.LayerTypeEthernet, ctx=ctx)
+        p.SetDecodingLayerContainer(dlc)
+        p.IgnorePanic = ignore
+        decoded = []
+        assert p.DecodeLayers(pktutil.golden_bytes("simple_tcp"), decoded) is None and len(decoded) == 4
+
+
+def test_layers_decoder_unsupported_and_errors(gp):
+    """LayersDecoder's own results (layers_decoder.go:11-101): the first type
+    with no decoder comes back without an error (DecodeLayers turns it into
+    UnsupportedLayerType), a decoder error with LayerTypeZero, Truncated
+    through the feedback, and a first type with no decoder leaves `decoded`
+    untouched."""
+    gopacket, L, ctx = gp
+    dlc = gopacket.DecodingLayerMap().Put(L.Ethernet()).Put(L.IPv4()).Put(L.UDP())
+    df = gopacket.DecodingLayerParser(L.LayerTypeEthernet, ctx=ctx)
+    dns = pktutil.read_pcap(pktutil.GOLDEN + "/test_dns.pcap")[1][0]
+    decoded = []
+    typ, err = dlc.LayersDecoder(L.LayerTypeEthernet, df)(dns, decoded)
+    assert (typ, err) == (L.LayerTypeDNS, None) and decoded == [L.LayerTypeEthernet, L.LayerTypeIPv4, L.LayerTypeUDP]
+    decoded = []
+    typ, err = dlc.LayersDecoder(L.LayerTypeEthernet, df)(pktutil.golden_bytes("udp_too_small"), decoded)
+    assert typ == gopacket.LayerTypeZero and err is not None and df.Truncated
+    decoded = [L.LayerTypeTCP]
+    typ, err = dlc.LayersDecoder(L.LayerTypeTCP, df)(dns, decoded)
+    assert (typ, err, decoded) == (L.LayerTypeTCP, None, [L.LayerTypeTCP])
+
+
+def test_register_port_layer_type_on_device(gp):
+    """RegisterTCPPortLayerType (ports.go:99-104) reaches the device parser:
+    with port 80 registered as DNS, the simple TCP packet (to port 80) stops
+    after TCP with UnsupportedLayerType(DNS), and TCP.NextLayerType() says
+    the same; an EthernetTypeMetadata edit (enums.go:310-329) makes an
+    unknown EtherType decode as IPv4."""
+    gopacket, L, ctx = gp
+    L._reset_registry()
+    try:
+        eth, ip4, tcp = L.Ethernet(), L.IPv4(), L.TCP()
+        p = _parser(gp, L.LayerTypeEthernet, eth, ip4, tcp, gopacket.Payload())
+        pkt = pktutil.golden_bytes("simple_tcp")
+        decoded = []
+        assert p.DecodeLayers(pkt, decoded) is None and len(decoded) == 4
+        L.RegisterTCPPortLayerType(80, L.LayerTypeDNS)
+        err = p.DecodeLayers(pkt, decoded)
+        assert err == gopacket.UnsupportedLayerType(L.LayerTypeDNS)
+        assert decoded == [L.LayerTypeEthernet, L.LayerTypeIPv4, L.LayerTypeTCP]
+        assert tcp.NextLayerType() == L.LayerTypeDNS
+        odd = pkt[:12] + b"\x88\xb5" + pkt[14:]
+        assert p.DecodeLayers(odd, decoded) is None and decoded == [L.LayerTypeEthernet]  # unknown: success (P1)
+        L.EthernetTypeMetadata[0x88B5] = L.EnumMetadata(LayerType=L.LayerTypeIPv4, Name="Local experimental")
+        assert p.DecodeLayers(odd, decoded) == gopacket.UnsupportedLayerType(L.LayerTypeDNS)
+        assert decoded == [L.LayerTypeEthernet, L.LayerTypeIPv4, L.LayerTypeTCP] and eth.NextLayerType() == 20
+    finally:
+        L._reset_registry()
