@@ -169,9 +169,16 @@ def test_layers_decoder_unsupported_and_errors(gp):
     decoded = []
     typ, err = dlc.LayersDecoder(L.LayerTypeEthernet, df)(dns, decoded)
     assert (typ, err) == (L.LayerTypeDNS, None) and decoded == [L.LayerTypeEthernet, L.LayerTypeIPv4, L.LayerTypeUDP]
-    decoded = []
-    typ, err = dlc.LayersDecoder(L.LayerTypeEthernet, df)(pktutil.golden_bytes("udp_too_small"), decoded)
-    assert typ == gopacket.LayerTypeZero and err is not None and df.Truncated
+    # decode_test.go:1018-1031: a UDP Length past the packet is Truncated, not an error
+    full = dlc.Put(L.Dot1Q()).Put(gopacket.Payload())
+    decoded, df.Truncated = [], False
+    typ, err = full.LayersDecoder(L.LayerTypeEthernet, df)(pktutil.golden_bytes("udp_too_small"), decoded)
+    assert (typ, err) == (gopacket.LayerTypeZero, None) and df.Truncated and len(decoded) == 5
+    # a decoder error (ip4.go:180-182): LayerTypeZero, the error, the layers before it
+    decoded, df.Truncated = [], False
+    typ, err = full.LayersDecoder(L.LayerTypeEthernet, df)(pktutil.golden_bytes("simple_tcp")[:20], decoded)
+    assert typ == gopacket.LayerTypeZero and err.Error() == "Invalid ip4 header. Length 6 less than 20"
+    assert decoded == [L.LayerTypeEthernet] and df.Truncated
     decoded = [L.LayerTypeTCP]
     typ, err = dlc.LayersDecoder(L.LayerTypeTCP, df)(dns, decoded)
     assert (typ, err, decoded) == (L.LayerTypeTCP, None, [L.LayerTypeTCP])
