@@ -450,12 +450,12 @@ class DecodingLayerParser:
     def _config(self, outputs=_lib.OUT_ALL):
         from .engine import ParserConfig
         from . import layers
+        ed = layers._registry_edits()  # EthernetTypeMetadata / IPProtocolMetadata edits, Register*PortLayerType
         key = (tuple(sorted(self._decoders)), self.IgnorePanic, self.IgnoreUnsupported, outputs,
-               layers._registry_version[0])
+               tuple((k, tuple(v)) for k, v in sorted(ed.items())))
         if self._cfg is None or self._cfg[0] != key:
             p = ParserConfig(int(self.first), sorted(self._decoders), ignore_panic=self.IgnorePanic,
                              ignore_unsupported=self.IgnoreUnsupported, outputs=outputs)
-            ed = layers._registry_edits()  # EthernetTypeMetadata / IPProtocolMetadata edits, Register*PortLayerType
             for v, lt in ed["ethertype"]:
                 p.set_ethertype(v, lt)
             for v, lt in ed["ipprotocol"]:

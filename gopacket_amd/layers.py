@@ -93,7 +93,6 @@ def EthernetTypeString(t):
 # 174-183) over the port switches. Every DecodingLayerParser built after an
 # edit sends the edited entries to its device parser (gpk_parser_set_*), so
 # the device's NextLayerType lookups and the structs' NextLayerType() agree.
-_registry_version = [0]
 
 
 class EnumMetadata:
@@ -107,31 +106,37 @@ class EnumMetadata:
 
 
 class _EnumTable:
-    """A [n]EnumMetadata array: reads the generated defaults, keeps edits."""
+    """A [n]EnumMetadata array: the generated defaults, and every entry a
+    caller has touched kept as its own object, so both forms of Go's edit
+    work: `T[v] = EnumMetadata(...)` and `T[v].LayerType = ...`."""
 
     def __init__(self, rows, n, unknown):
         self._default = {v: (LayerType(lt), name) for v, lt, name in rows}
         self._n, self._unknown, self._edits = n, unknown, {}
 
-    def __getitem__(self, v):
+    def _check(self, v):
         v = int(v)
         if not 0 <= v < self._n:
             raise IndexError(v)
-        if v in self._edits:
-            return self._edits[v]
-        lt, name = self._default.get(v, (LayerType(0), self._unknown))
-        return EnumMetadata(lt, name)
+        return v
+
+    def __getitem__(self, v):
+        v = self._check(v)
+        if v not in self._edits:
+            lt, name = self._default.get(v, (LayerType(0), self._unknown))
+            self._edits[v] = EnumMetadata(lt, name)
+        return self._edits[v]
 
     def __setitem__(self, v, meta):
-        v = int(v)
-        if not 0 <= v < self._n:
-            raise IndexError(v)
-        self._edits[v] = meta
-        _registry_version[0] += 1
+        self._edits[self._check(v)] = meta
 
     def _changed(self):
-        """(value, LayerType) of every edited entry."""
-        return [(v, int(m.LayerType)) for v, m in sorted(self._edits.items())]
+        """(value, LayerType) of every entry whose LayerType differs from the default."""
+        out = []
+        for v, m in sorted(self._edits.items()):
+            if int(m.LayerType) != int(self._default.get(v, (0, ""))[0]):
+                out.append((v, int(m.LayerType)))
+        return out
 
 
 EthernetTypeMetadata = _EnumTable(_REG["ethertype"], 65536, "UnknownEthernetType")
@@ -147,13 +152,11 @@ _tcp_user, _udp_user = {}, {}
 def RegisterTCPPortLayerType(port, layerType):
     """ports.go:99-104"""
     _tcp_override[int(port)] = _tcp_user[int(port)] = LayerType(layerType)
-    _registry_version[0] += 1
 
 
 def RegisterUDPPortLayerType(port, layerType):
     """ports.go:178-183"""
     _udp_override[int(port)] = _udp_user[int(port)] = LayerType(layerType)
-    _registry_version[0] += 1
 
 
 def EthernetTypeLayerType(t):
@@ -192,7 +195,6 @@ def _reset_registry():
     _tcp_override.update({p: LayerType(lt) for p, lt in _REG["tcp_port_override"]})
     _udp_override.clear()
     _udp_override.update({p: LayerType(lt) for p, lt in _REG["udp_port_override"]})
-    _registry_version[0] += 1
 
 
 def _registry_edits():

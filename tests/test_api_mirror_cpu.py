@@ -46,7 +46,12 @@ def test_registry_edits_reach_parser_config():
     cfg = p._config()
     assert cfg.decoder_for(L.LayerTypeIPv4) == _lib.DEC_IPV4
     L.RegisterUDPPortLayerType(9999, L.LayerTypeDNS)
-    assert p._config() is not cfg  # an edit rebuilds the device parser
+    cfg2 = p._config()
+    assert cfg2 is not cfg  # an edit rebuilds the device parser
+    assert p._config() is cfg2  # ... once
+    L.IPProtocolMetadata[254].LayerType = L.LayerTypeTCP  # Go's in-place form
+    assert L._registry_edits()["ipprotocol"] == [(253, 45), (254, 44)] and p._config() is not cfg2
+    assert L.IPProtocolString(254) == "UnknownIPProtocol"
 
 
 @pytest.mark.parametrize("form", [G.DecodingLayerMap, G.DecodingLayerSparse, G.DecodingLayerArray])
