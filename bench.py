@@ -126,7 +126,7 @@ def spawn_ranks(cmd):
     without a JSON line is a failure."""
     import subprocess
     env = dict(os.environ)
-    env.setdefault("OMP_NUM_THREADS", "16")
+    env.setdefault("OMP_NUM_THREADS", "16")  # (torchrun would set 1 and warn; the ranks' host work is the parity check)
     p = subprocess.Popen(cmd, cwd=ROOT, env=env, stdout=subprocess.PIPE, text=True, bufsize=1)
     lines = 0
     try:

@@ -47,7 +47,8 @@
 #include "../../include/gpk_afpacket.h"
 
 extern "C" int gpk_decode_batch_ex(gpk_ctx* c, const gpk_parser* p, const gpk_batch* b, const gpk_results* o,
-                                   void* stream, uint64_t packet_bytes, char* kname, size_t kcap);
+                                   void* stream, uint64_t packet_bytes, char* kname, size_t kcap,
+                                   gpk_fields* fields);
 
 namespace {
 
@@ -1212,7 +1213,7 @@ static int tpacket_pump(gpk_ctx* ctx, const gpk_parser* parser, gpk_tpacket* t, 
     gpk_batch db{dev, b.d_off, b.d_cap, n, ring_bytes + NB * side_cap + 64};
     gpk_results dr{b.d_rec, b.d_err, b.d_flow, nullptr};
     int drc = gpk_decode_batch_ex(ctx, parser, &db, &dr, b.stream, pk_bytes ? pk_bytes : 1, st->kernel,
-                                  sizeof(st->kernel));
+                                  sizeof(st->kernel), nullptr);
     if (drc) {
       rc = drc;
       good = false;

@@ -684,22 +684,33 @@ int gpk_decode_batch_fields(gpk_ctx* c, const gpk_parser* p, const gpk_batch* b,
 // readable end of data: data_bytes is the readable end only, packet_bytes the
 // mean-size hint; the name of the kernel launched goes to kname when given.
 // Library-internal, not part of the C ABI.
+// fields: the fused decode + layer fields launch (gpk_decode_batch_fields,
+// no layouts), else NULL.
 extern "C" __attribute__((visibility("hidden"))) int gpk_decode_batch_ex(gpk_ctx* c, const gpk_parser* p,
                                                                          const gpk_batch* b, const gpk_results* o,
                                                                          void* stream, uint64_t packet_bytes,
-                                                                         char* kname, size_t kcap) {
-  if (!o) return GPK_EINVAL;
+                                                                         char* kname, size_t kcap, gpk_fields* fields) {
+  if (!o || (fields && o->layouts)) return GPK_EINVAL;
   gpk::KParams P;
   int rc = make_params(c, p, b, o, P, packet_bytes);
   if (rc) return rc;
+  P.fields = fields;
   hipStream_t s = (hipStream_t)stream;
   std::lock_guard<std::mutex> g(c->mu);
   HIPCHK(hipSetDevice(c->device));
   int slot = 0;
   rc = upload(c, p, P, &slot, s);
   if (rc) return rc;
-  if (kname && kcap) gpk_launch_describe(&P, (p->outputs & GPK_OUT_L4_CSUM) != 0, o->layouts != nullptr, kname, kcap);
-  HIPCHK(gpk_launch_decode(&P, (p->outputs & GPK_OUT_L4_CSUM) != 0, o->layouts != nullptr, s));
+  if (kname && kcap) {
+    if (fields)
+      gpk_launch_describe_fields(&P, kname, kcap);
+    else
+      gpk_launch_describe(&P, (p->outputs & GPK_OUT_L4_CSUM) != 0, o->layouts != nullptr, kname, kcap);
+  }
+  if (fields)
+    HIPCHK(gpk_launch_decode_fields(&P, s, nullptr));
+  else
+    HIPCHK(gpk_launch_decode(&P, (p->outputs & GPK_OUT_L4_CSUM) != 0, o->layouts != nullptr, s));
   return note_launch(c, slot, s);
 }
 

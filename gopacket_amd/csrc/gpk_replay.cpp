@@ -52,7 +52,8 @@
 #include "gpk_walk.h"
 
 extern "C" int gpk_decode_batch_ex(gpk_ctx* c, const gpk_parser* p, const gpk_batch* b, const gpk_results* o,
-                                   void* stream, uint64_t packet_bytes, char* kname, size_t kcap);
+                                   void* stream, uint64_t packet_bytes, char* kname, size_t kcap,
+                                   gpk_fields* fields);
 
 namespace {
 
@@ -196,8 +197,11 @@ struct Bat {
   gpk_record* d_rec = nullptr;
   uint32_t* d_err = nullptr;
   uint64_t* d_flow = nullptr;
+  gpk_fields* h_fields = nullptr;  // opts.fields_cb: the layer fields (allocated on the first call that asks)
+  gpk_fields* d_fields = nullptr;
   hipEvent_t e0 = nullptr, k0 = nullptr, k1 = nullptr, done = nullptr;
   uint64_t first = 0, n = 0, flows_n = 0;
+  bool with_fields = false;  // this launch wrote fields
 };
 
 struct Pipeline {
@@ -206,6 +210,7 @@ struct Pipeline {
   std::deque<int> free_bats, inflight;
   uint64_t P = 0;
   gpk_replay_cb cb = nullptr;
+  gpk_replay_fields_cb fields_cb = nullptr;
   void* user = nullptr;
   gpk_replay_stats* st = nullptr;
   std::string herr;
@@ -232,6 +237,7 @@ struct Pipeline {
     if (hipEventElapsedTime(&kms, B.k0, B.k1) == hipSuccess) st->kernel_s += kms * 1e-3;
     double t = now_s();
     for (uint64_t i = 0; i < B.n; i++) st->packet_bytes += B.h_cap[i];
+    if (fields_cb && B.with_fields) fields_cb(user, B.first, B.n, B.h_fields);  // before the batch's results
     if (cb) cb(user, B.first, B.n, B.h_rec, B.h_err, B.h_flow, B.h_ci, B.h_cap);
     st->deliver_s += now_s() - t;
     free_bats.push_back(b);
@@ -287,9 +293,10 @@ struct Pipeline {
     }
     for (auto& B : bats) {
       for (void* p : {(void*)B.h_off, (void*)B.h_cap, (void*)B.h_ci, (void*)B.h_rec, (void*)B.h_err,
-                      (void*)B.h_flow})
+                      (void*)B.h_flow, (void*)B.h_fields})
         if (p) (void)gpk_pin_free(p);
-      for (void* p : {(void*)B.d_off, (void*)B.d_cap, (void*)B.d_rec, (void*)B.d_err, (void*)B.d_flow})
+      for (void* p : {(void*)B.d_off, (void*)B.d_cap, (void*)B.d_rec, (void*)B.d_err, (void*)B.d_flow,
+                      (void*)B.d_fields})
         if (p) (void)hipFree(p);
       for (hipEvent_t e : {B.e0, B.k0, B.k1, B.done})
         if (e) (void)hipEventDestroy(e);
@@ -398,8 +405,9 @@ void free_cached(void* p) {
 static int replay_file(gpk_ctx* ctx, const gpk_parser* parser, const char* path, const gpk_replay_opts* o,
                        gpk_replay_cb cb, void* user, gpk_replay_stats* stats) {
   const double t_start = now_s();
-  gpk_replay_opts opt{0, 0, 256ull << 20, 4, 1ull << 20, 8};
+  gpk_replay_opts opt{0, 0, 256ull << 20, 4, 1ull << 20, 8, nullptr};
   if (o) {
+    opt.fields_cb = o->fields_cb;
     opt.format = o->format;
     opt.ng_flags = o->ng_flags;
     if (o->slot_bytes) opt.slot_bytes = o->slot_bytes;
@@ -485,6 +493,7 @@ static int replay_file(gpk_ctx* ctx, const gpk_parser* parser, const char* path,
   const uint64_t R = opt.slot_bytes, C = R <= (1ull << 20) ? R : std::max<uint64_t>(1ull << 20, R / 16);
   Pipeline pl;
   pl.cb = cb;
+  pl.fields_cb = opt.fields_cb;
   pl.user = user;
   pl.st = stats;
   pl.P = opt.batch_pkts;
@@ -826,6 +835,17 @@ static int replay_file(gpk_ctx* ctx, const gpk_parser* parser, const char* path,
         break;
       }
       Bat& B = pl.bats[b];
+      B.with_fields = opt.fields_cb != nullptr;
+      if (B.with_fields && !B.d_fields) {  // first call that asks for fields: this batch's buffers
+        if (gpk_pin_alloc((void**)&B.h_fields, P * sizeof(gpk_fields)) != hipSuccess ||
+            hipMalloc((void**)&B.d_fields, P * sizeof(gpk_fields)) != hipSuccess) {
+          (void)pl.ok(hipErrorOutOfMemory, "fields buffers");
+          rc = GPK_ENOMEM;
+          pl.free_bats.push_back(b);
+          good = false;
+          break;
+        }
+      }
       if (!dwalk) {
         memcpy(B.h_off, xi.offsets + first, n * 8);  // relative to the slot's device copy (start)
         memcpy(B.h_cap, xi.caplens + first, n * 4);
@@ -864,7 +884,7 @@ static int replay_file(gpk_ctx* ctx, const gpk_parser* parser, const char* path,
                    dwalk ? S.d_cap + first : B.d_cap, n, dwalk ? C + R + 16 - base_off : len + 16};
       gpk_results dr{B.d_rec, B.d_err, B.d_flow, nullptr};
       int drc = gpk_decode_batch_ex(ctx, parser, &db, &dr, S.stream, pk_bytes ? pk_bytes : 1, stats->kernel,
-                                    sizeof(stats->kernel));
+                                    sizeof(stats->kernel), B.with_fields ? B.d_fields : nullptr);
       if (drc) {
         rc = drc;
         finished = true;
@@ -876,6 +896,9 @@ static int replay_file(gpk_ctx* ctx, const gpk_parser* parser, const char* path,
              pl.ok(hipMemcpyAsync(B.h_rec, B.d_rec, n * sizeof(gpk_record), hipMemcpyDeviceToHost, S.stream), "DtoH") &&
              pl.ok(hipMemcpyAsync(B.h_err, B.d_err, n * 8, hipMemcpyDeviceToHost, S.stream), "DtoH") &&
              pl.ok(hipMemcpyAsync(B.h_flow, B.d_flow, n * 24, hipMemcpyDeviceToHost, S.stream), "DtoH");
+      if (B.with_fields)
+        good = good && pl.ok(hipMemcpyAsync(B.h_fields, B.d_fields, n * sizeof(gpk_fields), hipMemcpyDeviceToHost,
+                                            S.stream), "DtoH fields");
       if (dwalk)
         good = good &&
                pl.ok(hipMemcpyAsync(B.h_cap, S.d_cap + first, n * 4, hipMemcpyDeviceToHost, S.stream), "DtoH caplens") &&

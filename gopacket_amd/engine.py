@@ -194,13 +194,21 @@ class Context:
         return out.value
 
     def replay_file(self, parser, path, fmt=0, ng_flags=0, slot_bytes=0, slots=0, batch_pkts=0, read_threads=0,
-                    collect=True, on_batch=None):
+                    collect=True, on_batch=None, fields=False):
         """gpk_replay_file: the whole capture through HBM (BASELINE config C5).
         collect=True gathers every result (records, err_args, flows SoA, ci,
         caplens) in packet order; on_batch(first, n, records, err_args, flows,
         ci, caplens) sees each launch's numpy views instead (valid during the
-        call). Returns (results-or-None, stats dict)."""
+        call). fields=True: every launch is the fused decode + layer fields
+        (gpk_replay_opts.fields_cb): the results gain "fields" (FIELDS_DTYPE
+        per packet), and on_batch a last argument, the launch's fields.
+        Returns (results-or-None, stats dict)."""
         parts = []
+        got_fields = []  # the current launch's fields (fields_cb runs right before cb)
+
+        def fcb(user, first, n, f):
+            got_fields[:] = [np.ctypeslib.as_array(ctypes.cast(f, ctypes.POINTER(ctypes.c_uint8)), (n * 128,)).view(
+                _lib.FIELDS_DTYPE) if n else np.zeros(0, _lib.FIELDS_DTYPE)]
 
         def cb(user, first, n, rec, err, fl, ci, cap):
             if not n:
@@ -212,13 +220,16 @@ class Context:
                      np.ctypeslib.as_array(ctypes.cast(ci, ctypes.POINTER(ctypes.c_uint8)), (n * 24,)).view(
                          _lib.CAPINFO_DTYPE),
                      np.ctypeslib.as_array(ctypes.cast(cap, ctypes.POINTER(ctypes.c_uint32)), (n,)))
+            if fields:
+                views = views + (got_fields[0],)
             if on_batch is not None:
                 on_batch(first, n, *views)
             if collect:
                 parts.append(tuple(v.copy() for v in views))
 
         c_cb = _lib.REPLAY_CB(cb)
-        o = _lib.ReplayOpts(fmt, ng_flags, slot_bytes, slots, batch_pkts, read_threads)
+        c_fcb = _lib.REPLAY_FIELDS_CB(fcb) if fields else _lib.REPLAY_FIELDS_CB()
+        o = _lib.ReplayOpts(fmt, ng_flags, slot_bytes, slots, batch_pkts, read_threads, c_fcb)
         st = _lib.ReplayStats()
         rc = lib().gpk_replay_file(self.h, parser.h, path.encode() if isinstance(path, str) else path,
                                    ctypes.byref(o), c_cb, None, ctypes.byref(st))
@@ -234,10 +245,14 @@ class Context:
                 fl = np.concatenate([p[2].reshape(3, -1) for p in parts], axis=1).reshape(-1)
                 res = dict(records=np.concatenate([p[0] for p in parts]), err_args=np.concatenate([p[1] for p in parts]),
                            flows=fl, ci=np.concatenate([p[3] for p in parts]), caplens=np.concatenate([p[4] for p in parts]))
+                if fields:
+                    res["fields"] = np.concatenate([p[5] for p in parts])
             else:
                 res = dict(records=np.zeros(0, _lib.RECORD_DTYPE), err_args=np.zeros(0, np.uint32),
                            flows=np.zeros(0, np.uint64), ci=np.zeros(0, _lib.CAPINFO_DTYPE),
                            caplens=np.zeros(0, np.uint32))
+                if fields:
+                    res["fields"] = np.zeros(0, _lib.FIELDS_DTYPE)
         return res, stats
 
     def decoded_list_host(self, parser, pkt, cap=65536):

@@ -143,6 +143,12 @@ int gpk_capreader_interface(const gpk_capreader* r, int section, int index, gpk_
 int gpk_capreader_interface_str(const gpk_capreader* r, int section, int index, int field, char* buf, size_t cap);
 
 /* ---- whole-file replay through the GPU (BASELINE config C5) -------------- */
+/* The layer fields of one device launch's packets (gpk_replay_opts.fields_cb):
+ * gpk_fields as gpk_decode_batch_fields writes them, in packet order, host
+ * memory valid during the call only; called on the calling thread right
+ * before gpk_replay_cb for the same packets. */
+typedef void (*gpk_replay_fields_cb)(void* user, uint64_t first_packet, uint64_t n, const gpk_fields* fields);
+
 typedef struct gpk_replay_opts {
   int format;            /* GPK_CAP_PCAP / GPK_CAP_PCAPNG, 0 = from the magic */
   uint32_t ng_flags;     /* GPK_NG_* */
@@ -153,6 +159,9 @@ typedef struct gpk_replay_opts {
   int slots;             /* staging slots in flight (default 4)                 */
   uint64_t batch_pkts;   /* packets per device launch (default 1 Mi)            */
   int read_threads;      /* pread threads per slot (default 8)                  */
+  gpk_replay_fields_cb fields_cb; /* non-NULL: each launch is the fused decode + layer fields
+                            (gpk_decode_batch_fields) and the fields come back too, 128 B per
+                            packet more DtoH; NULL: the decode alone */
 } gpk_replay_opts;
 
 typedef struct gpk_replay_stats {

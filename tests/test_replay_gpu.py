@@ -206,3 +206,32 @@ def test_replay_device_walk_resumes(gpu_ctx, tmp_path):
     assert st["error"] == "EOF"
     assert n_big >= 10
     assert st["device_walk_packets"] >= 0.9 * st["packets"], (st["device_walk_packets"], st["packets"])
+
+
+@pytest.mark.parametrize("cfg_name,slot_bytes,slots,batch", [("statsassembly", 65536, 3, 1000),
+                                                             ("statsassembly", 0, 0, 0), ("fragment_no_payload", 1 << 20, 2, 4097)])
+def test_replay_fields(gpu_ctx, capture, cfg_name, slot_bytes, slots, batch):
+    """fields=True: every launch is the fused decode + layer fields; the
+    gpk_fields records reach the host through fields_cb (called before the
+    batch's results callback) and equal the oracle's field extraction over the
+    oracle's layouts, packet for packet; the decode results are unchanged."""
+    from oracle import oracle as O
+    import pktutil
+    path, raw = capture
+    res, pk = packets_and_expect(raw)
+    seen = []
+
+    def on_batch(first, n, rec, err, fl, ci, cap, fields):
+        assert len(fields) == n
+        seen.append((first, n))
+
+    got, st = gpu_ctx.replay_file(device_parser(CONFIGS[cfg_name]), path, slot_bytes=slot_bytes, slots=slots,
+                                  batch_pkts=batch, fields=True, on_batch=on_batch)
+    assert st["packets"] == len(pk) and st["error"] == res["err"]
+    assert sum(n for _, n in seen) == len(pk)
+    assert [f for f, _ in seen] == sorted(f for f, _ in seen)
+    data, off, cap = pktutil.pack(pk)
+    ref = oracle_parser(CONFIGS[cfg_name]).decode(data, off, cap, nthreads=8, layouts=True)
+    assert_same(got, ref, "replay+fields")
+    want = O.extract_fields(data, off, ref["layouts"])
+    assert np.array_equal(got["fields"].view(np.uint8).reshape(-1, 128), want)
