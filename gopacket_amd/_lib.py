@@ -119,9 +119,13 @@ class TpOpts(ctypes.Structure):
                 ("protocol", ctypes.c_uint16), ("_pad", ctypes.c_uint16 * 3), ("iface", ctypes.c_char * 64)]
 
 
+# gpk_tp_pump_fields_cb(user, first_packet, n, const gpk_fields*)
+PUMP_FIELDS_CB = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p)
+
+
 class PumpOpts(ctypes.Structure):
     _fields_ = [("batch_pkts", ctypes.c_uint64), ("max_packets", ctypes.c_uint64), ("wait", ctypes.c_int),
-                ("inflight", ctypes.c_int)]
+                ("inflight", ctypes.c_int), ("fields_cb", PUMP_FIELDS_CB)]
 
 
 class PumpStats(ctypes.Structure):

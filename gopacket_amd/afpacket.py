@@ -224,11 +224,19 @@ class TPacket:
     def SetFanout(self, t, id_):
         _lib.check(_lib.lib().gpk_tpacket_set_fanout(self.h, int(t), int(id_)))
 
-    def Pump(self, ctx, parser, batch_pkts=0, max_packets=0, wait=False, inflight=0, collect=True, on_batch=None):
+    def Pump(self, ctx, parser, batch_pkts=0, max_packets=0, wait=False, inflight=0, collect=True, on_batch=None,
+             fields=False):
         """gpk_tpacket_pump: drain the ring through HBM and the decoder. Returns
         (results-or-None, stats dict); results as Context.replay_file's, with
-        ci of TPINFO_DTYPE."""
+        ci of TPINFO_DTYPE. fields=True: every launch is the fused decode +
+        layer fields (gpk_tp_pump_opts.fields_cb); results gain "fields" and
+        on_batch a last argument, as in replay_file."""
         parts = []
+        got_fields = []
+
+        def fcb(user, first, n, f):
+            got_fields[:] = [np.ctypeslib.as_array(ctypes.cast(f, ctypes.POINTER(ctypes.c_uint8)), (n * 128,)).view(
+                _lib.FIELDS_DTYPE) if n else np.zeros(0, _lib.FIELDS_DTYPE)]
 
         def cb(user, first, n, rec, err, fl, ci, cap):
             if not n:
@@ -240,13 +248,16 @@ class TPacket:
                      np.ctypeslib.as_array(ctypes.cast(ci, ctypes.POINTER(ctypes.c_uint8)), (n * 24,)).view(
                          _lib.TPINFO_DTYPE),
                      np.ctypeslib.as_array(ctypes.cast(cap, ctypes.POINTER(ctypes.c_uint32)), (n,)))
+            if fields:
+                views = views + (got_fields[0],)
             if on_batch is not None:
                 on_batch(first, n, *views)
             if collect:
                 parts.append(tuple(v.copy() for v in views))
 
         c_cb = _lib.PUMP_CB(cb)
-        o = _lib.PumpOpts(batch_pkts, max_packets, 1 if wait else 0, inflight)
+        c_fcb = _lib.PUMP_FIELDS_CB(fcb) if fields else _lib.PUMP_FIELDS_CB()
+        o = _lib.PumpOpts(batch_pkts, max_packets, 1 if wait else 0, inflight, c_fcb)
         st = _lib.PumpStats()
         rc = _lib.lib().gpk_tpacket_pump(ctx.h, parser.h, self.h, ctypes.byref(o), c_cb, None, ctypes.byref(st))
         if rc != _lib.GPK_OK:
@@ -261,10 +272,14 @@ class TPacket:
                 fl = np.concatenate([p[2].reshape(3, -1) for p in parts], axis=1).reshape(-1)
                 res = dict(records=np.concatenate([p[0] for p in parts]), err_args=np.concatenate([p[1] for p in parts]),
                            flows=fl, ci=np.concatenate([p[3] for p in parts]), caplens=np.concatenate([p[4] for p in parts]))
+                if fields:
+                    res["fields"] = np.concatenate([p[5] for p in parts])
             else:
                 res = dict(records=np.zeros(0, _lib.RECORD_DTYPE), err_args=np.zeros(0, np.uint32),
                            flows=np.zeros(0, np.uint64), ci=np.zeros(0, _lib.TPINFO_DTYPE),
                            caplens=np.zeros(0, np.uint32))
+                if fields:
+                    res["fields"] = np.zeros(0, _lib.FIELDS_DTYPE)
         return res, stats
 
     def Close(self):

@@ -1008,6 +1008,7 @@ struct PBat {
   gpk_record *h_rec = nullptr, *d_rec = nullptr;
   uint32_t *h_err = nullptr, *d_err = nullptr;
   uint64_t *h_flow = nullptr, *d_flow = nullptr;
+  gpk_fields *h_fields = nullptr, *d_fields = nullptr;
   uint8_t* h_side = nullptr;
   hipStream_t stream = nullptr;
   hipEvent_t e0 = nullptr, h2d = nullptr, k0 = nullptr, k1 = nullptr, done = nullptr;
@@ -1019,13 +1020,15 @@ struct PBat {
 
 static int tpacket_pump(gpk_ctx* ctx, const gpk_parser* parser, gpk_tpacket* t, const gpk_tp_pump_opts* o,
                         gpk_tp_pump_cb cb, void* user, gpk_tp_pump_stats* st) {
-  gpk_tp_pump_opts opt{1ull << 20, 0, 0, 4};
+  gpk_tp_pump_opts opt{1ull << 20, 0, 0, 4, nullptr};
   if (o) {
     if (o->batch_pkts) opt.batch_pkts = o->batch_pkts;
     opt.max_packets = o->max_packets;
     opt.wait = o->wait;
     if (o->inflight > 0) opt.inflight = o->inflight;
+    opt.fields_cb = o->fields_cb;
   }
+  const bool with_fields = opt.fields_cb != nullptr;
   const uint64_t P = opt.batch_pkts;
   const int NB = std::max(2, opt.inflight);
   const uint64_t side_cap = std::min<uint64_t>(64ull << 20, std::max<uint64_t>(1ull << 20, P * 256));
@@ -1054,6 +1057,9 @@ static int tpacket_pump(gpk_ctx* ctx, const gpk_parser* parser, gpk_tpacket* t, 
            ok(hipEventCreateWithFlags(&b.h2d, hipEventDisableTiming), "hipEventCreate") &&
            ok(hipEventCreate(&b.k0), "hipEventCreate") && ok(hipEventCreate(&b.k1), "hipEventCreate") &&
            ok(hipEventCreate(&b.done), "hipEventCreate");
+    if (with_fields)
+      good = good && ok(gpk_pin_alloc((void**)&b.h_fields, P * sizeof(gpk_fields)), "pinned batch") &&
+             ok(hipMalloc((void**)&b.d_fields, P * sizeof(gpk_fields)), "hipMalloc");
   }
   // the ring itself is DMA'd from: pin it where the memory allows (an AF_PACKET
   // mapping may refuse; then the copies go through the runtime's staging)
@@ -1098,6 +1104,7 @@ static int tpacket_pump(gpk_ctx* ctx, const gpk_parser* parser, gpk_tpacket* t, 
     float ms = 0, kms = 0;
     if (hipEventElapsedTime(&ms, b.e0, b.done) == hipSuccess) st->gpu_s += ms * 1e-3;
     if (hipEventElapsedTime(&kms, b.k0, b.k1) == hipSuccess) st->kernel_s += kms * 1e-3;
+    if (with_fields) opt.fields_cb(user, b.first, b.n, b.h_fields);
     if (cb) cb(user, b.first, b.n, b.h_rec, b.h_err, b.h_flow, b.h_ci, b.h_cap);
     b.inflight = false;
     return true;
@@ -1213,7 +1220,7 @@ static int tpacket_pump(gpk_ctx* ctx, const gpk_parser* parser, gpk_tpacket* t, 
     gpk_batch db{dev, b.d_off, b.d_cap, n, ring_bytes + NB * side_cap + 64};
     gpk_results dr{b.d_rec, b.d_err, b.d_flow, nullptr};
     int drc = gpk_decode_batch_ex(ctx, parser, &db, &dr, b.stream, pk_bytes ? pk_bytes : 1, st->kernel,
-                                  sizeof(st->kernel), nullptr);
+                                  sizeof(st->kernel), with_fields ? b.d_fields : nullptr);
     if (drc) {
       rc = drc;
       good = false;
@@ -1223,6 +1230,8 @@ static int tpacket_pump(gpk_ctx* ctx, const gpk_parser* parser, gpk_tpacket* t, 
            ok(hipMemcpyAsync(b.h_rec, b.d_rec, n * sizeof(gpk_record), hipMemcpyDeviceToHost, b.stream), "DtoH") &&
            ok(hipMemcpyAsync(b.h_err, b.d_err, n * 8, hipMemcpyDeviceToHost, b.stream), "DtoH") &&
            ok(hipMemcpyAsync(b.h_flow, b.d_flow, n * 24, hipMemcpyDeviceToHost, b.stream), "DtoH") &&
+           (!with_fields ||
+            ok(hipMemcpyAsync(b.h_fields, b.d_fields, n * sizeof(gpk_fields), hipMemcpyDeviceToHost, b.stream), "DtoH")) &&
            ok(hipEventRecord(b.done, b.stream), "hipEventRecord");
     b.inflight = true;
     order.push_back(slot);
@@ -1253,9 +1262,9 @@ static int tpacket_pump(gpk_ctx* ctx, const gpk_parser* parser, gpk_tpacket* t, 
   for (auto& b : B) {
     if (b.stream) (void)hipStreamSynchronize(b.stream);
     for (void* p : {(void*)b.h_off, (void*)b.h_cap, (void*)b.h_ci, (void*)b.h_rec, (void*)b.h_err, (void*)b.h_flow,
-                    (void*)b.h_side})
+                    (void*)b.h_side, (void*)b.h_fields})
       if (p) (void)gpk_pin_free(p);
-    for (void* p : {(void*)b.d_off, (void*)b.d_cap, (void*)b.d_rec, (void*)b.d_err, (void*)b.d_flow})
+    for (void* p : {(void*)b.d_off, (void*)b.d_cap, (void*)b.d_rec, (void*)b.d_err, (void*)b.d_flow, (void*)b.d_fields})
       if (p) (void)hipFree(p);
     for (hipEvent_t e : {b.e0, b.h2d, b.k0, b.k1, b.done})
       if (e) (void)hipEventDestroy(e);

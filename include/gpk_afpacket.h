@@ -137,11 +137,17 @@ int gpk_tpacket_set_bpf(gpk_tpacket* t, const void* insns, uint32_t n);
 int gpk_tpacket_set_fanout(gpk_tpacket* t, int type, uint16_t id);
 
 /* ---- the capture loop through the GPU ------------------------------------ */
+/* Per batch, before its gpk_tp_pump_cb: the layer fields of its n packets
+ * (gpk_fields, include/gpk.h), valid during the call. */
+typedef void (*gpk_tp_pump_fields_cb)(void* user, uint64_t first_packet, uint64_t n, const gpk_fields* fields);
+
 typedef struct gpk_tp_pump_opts {
   uint64_t batch_pkts;  /* packets per device launch (default 1 Mi)              */
   uint64_t max_packets; /* stop after this many (0 = until the ring runs dry)     */
   int wait;             /* socket readers: poll when the ring is dry             */
   int inflight;         /* batches in flight (default 4)                          */
+  gpk_tp_pump_fields_cb fields_cb; /* non-null: every launch is the fused decode +
+                                      layer fields, delivered through it     */
 } gpk_tp_pump_opts;
 
 typedef struct gpk_tp_pump_stats {

@@ -125,3 +125,31 @@ def test_pump_stops_at_a_corrupt_chain_and_at_max_packets(gpu_ctx):
     # block 0 was finished and handed back; block 1 is still current, so still the reader's
     assert struct.unpack_from("<I", ring2, 8)[0] == 0
     tp.Close()
+
+
+@pytest.mark.parametrize("vlan,batch", [(False, 1000), (True, 97)])
+def test_pump_fields(gpu_ctx, vlan, batch):
+    """fields=True: the fused decode + layer fields per batch (the packets with
+    an inserted VLAN tag decoded from the side regions); the gpk_fields records
+    equal the oracle's extraction over its layouts, and the results are
+    unchanged."""
+    from oracle import oracle as O
+    S = _lib.synth_lib()
+    bs, nb = 65536, 16
+    ring = np.zeros(bs * nb, np.uint8)
+    S.gpk_synth_tpacket_v3(ring.ctypes.data, bs, nb, synth.C4_IMIX, 99, 7, 3, None)
+    opts = dict(frame_size=4096, block_size=bs, num_blocks=nb, add_vlan_header=vlan)
+    pk, exp = expect(ring.tobytes(), AO.V3, opts)
+    args = [afpacket.OptFrameSize(4096), afpacket.OptBlockSize(bs), afpacket.OptNumBlocks(nb)]
+    if vlan:
+        args.append(afpacket.OptAddVLANHeader(True))
+    tp = afpacket.AttachRing(ring, afpacket.TPacketVersion3, *args)
+    seen = []
+    got, st = tp.Pump(gpu_ctx, device_parser(CONFIGS["statsassembly"]), batch_pkts=batch, inflight=3, fields=True,
+                      on_batch=lambda first, n, *v: seen.append((first, n, len(v[-1]))))
+    tp.Close()
+    assert st["packets"] == len(pk) and all(n == k for _, n, k in seen)
+    data, off, cap = pktutil.pack(pk)
+    ref = oracle_parser(CONFIGS["statsassembly"]).decode(data, off, cap, nthreads=8, layouts=True)
+    assert_same(got, ref, "pump+fields")
+    assert np.array_equal(got["fields"].view(np.uint8).reshape(-1, 128), O.extract_fields(data, off, ref["layouts"]))
