@@ -837,8 +837,9 @@ static int replay_file(gpk_ctx* ctx, const gpk_parser* parser, const char* path,
       Bat& B = pl.bats[b];
       B.with_fields = opt.fields_cb != nullptr;
       if (B.with_fields && !B.d_fields) {  // first call that asks for fields: this batch's buffers
-        if (gpk_pin_alloc((void**)&B.h_fields, P * sizeof(gpk_fields)) != hipSuccess ||
+        if ((!B.h_fields && gpk_pin_alloc((void**)&B.h_fields, P * sizeof(gpk_fields)) != hipSuccess) ||
             hipMalloc((void**)&B.d_fields, P * sizeof(gpk_fields)) != hipSuccess) {
+          B.d_fields = nullptr;  // h_fields, when it was allocated, is kept for the next call
           (void)pl.ok(hipErrorOutOfMemory, "fields buffers");
           rc = GPK_ENOMEM;
           pl.free_bats.push_back(b);
