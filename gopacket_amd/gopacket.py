@@ -718,10 +718,12 @@ class BatchResult:
         got = 0
         for k in out:
             got |= 1 << _slot(k)
-        assert got == pres, "record presence %#x, decoded list %#x" % (pres, got)
+        if got != pres:
+            raise RuntimeError("fields record presence %#x disagrees with the decoded list (%#x)" % (pres, got))
         for k, name in ((_lib.DEC_IPV4, "ip4_start"), (_lib.DEC_TCP, "tcp_start")):
-            if k in out and out[k][0] < 0xFF:
-                assert out[k][0] == int(f[name]), name
+            if k in out and out[k][0] < 0xFF and out[k][0] != int(f[name]):
+                raise RuntimeError("fields record %s %d disagrees with the decoded list (%d)"
+                                   % (name, int(f[name]), out[k][0]))
         return out
 
     def _slices_host(self, pkt, decoded):
