@@ -146,6 +146,8 @@ class Context:
         layouts returned."""
         import torch
         data = np.ascontiguousarray(data, dtype=np.uint8)
+        if not data.flags.writeable:  # torch.from_numpy wants a writable array (read-only views of bytes)
+            data = data.copy()
         offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
         caplens = np.ascontiguousarray(caplens, dtype=np.uint32)
         n = len(offsets)
