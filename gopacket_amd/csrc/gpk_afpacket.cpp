@@ -298,8 +298,13 @@ struct Call {
     const uint64_t h = s.cur_hdr;
     for (;;) {
       const bool deferred = t->defer && t->pending[h];
-      if (!deferred && (header_status(t, h) & kStatusUser)) break;
-      if (!wait) {
+      // released earlier in this same step (the walk went round the ring over
+      // empty headers): the reference's release has already handed it to the
+      // kernel, so it is not the user's; the release is committed when this
+      // step returns, and the next call polls it
+      const bool released_now = std::find(releases->begin(), releases->end(), h) != releases->end();
+      if (!deferred && !released_now && (header_status(t, h) & kStatusUser)) break;
+      if (!wait || released_now) {
         s.polling = true;
         return 0;
       }

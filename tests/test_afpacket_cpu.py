@@ -218,6 +218,34 @@ def test_empty_block_retry_and_vlan_edge_cases():
     assert len(out) == 1 and kind == AO.ERROR and err == "runtime error: slice bounds out of range [:12] with capacity 8"
 
 
+def test_every_header_empty_goes_round_once():
+    """Every header handed over and empty (tp_len 0): the retry releases each
+    one (afpacket.go:371-385, releaseCurrentPacket hands it to the kernel at
+    once), so the walk comes round to a header the kernel owns and stops there
+    instead of circling the ring (found by tests/asan/fuzz_host.cpp: the
+    native walk committed its releases only after the step, and looped)."""
+    rng = np.random.default_rng(13)
+    for nb in (1, 4):
+        blocks = [dict(status=1, pkts=[dict(data=bytes(60), length=0)]) for _ in range(nb)]
+        compare(ringgen.v3_ring(blocks, 4096, nb), AO.V3, dict(frame_size=4096, block_size=4096, num_blocks=nb), rng,
+                rounds=3)
+    for version in (AO.V1, AO.V2):
+        for nf in (1, 8):
+            frames = [dict(status=1, data=bytes(40), length=0) for _ in range(nf)]
+            fz = 4096 // nf if nf > 1 else 4096
+            compare(ringgen.frame_ring(version, frames, fz, nf), version,
+                    dict(frame_size=fz, block_size=4096, num_blocks=1), rng, rounds=3)
+    # with deferred release the walk stops at the first header it released
+    ring = ringgen.v3_ring([dict(status=1, pkts=[dict(data=bytes(60), length=0)])] * 2, 4096, 2)
+    h, arr = native_reader(ring, AO.V3, dict(frame_size=4096, block_size=4096, num_blocks=2))
+    try:
+        _lib.lib().gpk_tpacket_defer(h, 1)
+        got, _, st = native_index(h, len(ring), 10, np.zeros(64, np.uint8))
+        assert got == [] and st == _lib.TP_WAIT
+    finally:
+        _lib.lib().gpk_tpacket_close(h)
+
+
 def test_deferred_release_holds_headers_until_released():
     rng = np.random.default_rng(5)
     blocks = [dict(status=1, pkts=[dict(data=ringgen.random_packet(rng, 20, 200)) for _ in range(5)])
