@@ -124,10 +124,16 @@ def spawn_ranks(cmd):
     """Run the torchrun child, pass its stdout through line by line (rank 0
     prints the one JSON line) and return its exit status; a run that ends
     without a JSON line is a failure."""
+    import signal
     import subprocess
     env = dict(os.environ)
     env.setdefault("OMP_NUM_THREADS", "16")  # (torchrun would set 1 and warn; the ranks' host work is the parity check)
     p = subprocess.Popen(cmd, cwd=ROOT, env=env, stdout=subprocess.PIPE, text=True, bufsize=1)
+
+    def on_term(signum, frame):  # a driver's timeout: end the ranks too, not just this parent
+        raise SystemExit(128 + signum)
+
+    signal.signal(signal.SIGTERM, on_term)
     lines = 0
     try:
         for line in p.stdout:

@@ -67,3 +67,30 @@ def test_bench_world_mismatch_fails_before_the_gpu():
     out = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--configs", "c2", "--packets", "4096"],
                          cwd=ROOT, env=env, capture_output=True, text=True, timeout=120)
     assert out.returncode != 0 and "WORLD_SIZE" in out.stderr
+
+
+def test_terminating_the_parent_ends_the_ranks(tmp_path):
+    """A driver's timeout sends SIGTERM to `bench.py --gpus N`: the torchrun
+    child (and with it the ranks) is terminated and reaped, not orphaned."""
+    import signal
+    import subprocess
+    import time
+    script = tmp_path / "parent.py"
+    script.write_text(
+        "import importlib.util, sys\n"
+        "spec = importlib.util.spec_from_file_location('b', %r)\n"
+        "b = importlib.util.module_from_spec(spec); spec.loader.exec_module(b)\n"
+        "sys.exit(b.spawn_ranks([sys.executable, '-u', '-c', "
+        "'import os, time; print(os.getpid(), flush=True); time.sleep(120)']))\n" % os.path.join(ROOT, "bench.py"))
+    p = subprocess.Popen([sys.executable, "-u", str(script)], stdout=subprocess.PIPE, text=True)
+    child = int(p.stdout.readline())
+    p.send_signal(signal.SIGTERM)
+    assert p.wait(timeout=60) == 128 + signal.SIGTERM
+    deadline = time.time() + 10
+    while True:
+        try:
+            os.kill(child, 0)
+        except ProcessLookupError:
+            break
+        assert time.time() < deadline, "the child outlived its parent"
+        time.sleep(0.1)
