@@ -363,6 +363,12 @@ def synth_lib():
                                                 ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_void_p,
                                                 ctypes.c_void_p]
         S.gpk_probe_skeleton_storer.restype = ctypes.c_int
+        S.gpk_probe_malloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint64, ctypes.c_uint]
+        S.gpk_probe_malloc.restype = ctypes.c_int
+        S.gpk_probe_free.argtypes = [ctypes.c_void_p]
+        S.gpk_probe_free.restype = ctypes.c_int
+        S.gpk_probe_d2d.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64]
+        S.gpk_probe_d2d.restype = ctypes.c_int
         S.gpk_synth_tpacket_v3.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int,
                                            ctypes.c_uint64, ctypes.c_int32, ctypes.c_uint32, ctypes.c_void_p]
         S.gpk_synth_tpacket_v3.restype = ctypes.c_uint64

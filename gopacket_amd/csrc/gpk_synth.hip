@@ -835,4 +835,15 @@ int gpk_probe_mixed(const uint8_t* data, uint64_t nbytes, uint8_t* wbuf, uint64_
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
+// Device memory of a given kind for placement experiments (tools/alloc_probe.py):
+// hipExtMallocWithFlags flags (hipDeviceMallocDefault 0, Finegrained 1,
+// Uncached 3, Contiguous 4).
+int gpk_probe_malloc(void** p, uint64_t bytes, unsigned flags) {
+  return hipExtMallocWithFlags(p, bytes, flags) == hipSuccess ? 0 : -1;
+}
+int gpk_probe_free(void* p) { return hipFree(p) == hipSuccess ? 0 : -1; }
+int gpk_probe_d2d(void* dst, const void* src, uint64_t bytes) {
+  return hipMemcpy(dst, src, bytes, hipMemcpyDeviceToDevice) == hipSuccess ? 0 : -1;
+}
+
 }  // extern "C"
