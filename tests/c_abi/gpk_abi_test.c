@@ -17,6 +17,7 @@
 #include <string.h>
 
 #include "gpk.h"
+#include "gpk_capture.h"
 
 /* the layouts cgo sees (INTEGRATION.md's Go structs mirror these offsets) */
 _Static_assert(sizeof(gpk_record) == 16, "gpk_record is 16 bytes");
@@ -225,14 +226,134 @@ static int decode_checks(const char* dir) {
   return 0;
 }
 
+/* ---- replay: gpk_replay_file with the fields callback, from C ----------------
+ * What a cgo caller of the C5 loop sees: results in packet order, each batch's
+ * gpk_fields delivered right before its records for the same packets, and for
+ * every packet decoded without error a record whose decoded list names exactly
+ * the decoders the fields record marks present (gpk.h gpk_fields.present). */
+struct replay_state {
+  uint64_t next_first, fields_first, fields_n, packets, checked;
+  int have_fields;
+  uint8_t* present; /* this batch's present bytes (fields valid during the callback only) */
+  uint64_t cap;
+};
+
+static void on_fields(void* user, uint64_t first, uint64_t n, const gpk_fields* f) {
+  struct replay_state* st = (struct replay_state*)user;
+  if (n > st->cap) {
+    free(st->present);
+    st->present = (uint8_t*)malloc(n);
+    st->cap = n;
+  }
+  for (uint64_t i = 0; i < n; i++) st->present[i] = f[i].present;
+  st->fields_first = first;
+  st->fields_n = n;
+  st->have_fields = 1;
+}
+
+static int code_slot(unsigned code) { /* decoded-list code -> gpk_fields.present bit */
+  switch (code) {
+    case GPK_CODE_ETHERNET: return 0;
+    case GPK_CODE_DOT1Q: return 1;
+    case GPK_CODE_IPV4: return 2;
+    case GPK_CODE_IPV6: return 3;
+    case GPK_CODE_IPV6_HOPBYHOP:
+    case GPK_CODE_IPV6_ROUTING:
+    case GPK_CODE_IPV6_FRAGMENT:
+    case GPK_CODE_IPV6_DESTINATION: return 4;
+    case GPK_CODE_TCP: return 5;
+    case GPK_CODE_UDP: return 6;
+    case GPK_CODE_PAYLOAD:
+    case GPK_CODE_FRAGMENT: return 7;
+    default: return -1;
+  }
+}
+
+static void on_results(void* user, uint64_t first, uint64_t n, const gpk_record* rec, const uint32_t* err,
+                       const uint64_t* flows, const gpk_capture_info* ci, const uint32_t* caplens) {
+  struct replay_state* st = (struct replay_state*)user;
+  (void)err;
+  (void)flows;
+  (void)ci;
+  (void)caplens;
+  CHECK(first == st->next_first, "results for packet %llu, expected %llu", (unsigned long long)first,
+        (unsigned long long)st->next_first);
+  CHECK(st->have_fields && st->fields_first == first && st->fields_n == n, "fields not delivered before results");
+  for (uint64_t i = 0; i < n && st->have_fields; i++) {
+    const unsigned nl = gpk_record_nlayers(&rec[i]);
+    if (gpk_record_err(&rec[i]) || nl > 16) continue;
+    unsigned want = 0;
+    for (unsigned k = 0; k < nl; k++) {
+      const int sl = code_slot((unsigned)(rec[i].layers >> (4 * k)) & 0xF);
+      if (sl >= 0) want |= 1u << sl;
+    }
+    CHECK(st->present[i] == want, "packet %llu: present %#x, decoded list %#x", (unsigned long long)(first + i),
+          st->present[i], want);
+    st->checked++;
+  }
+  st->have_fields = 0;
+  st->next_first = first + n;
+  st->packets += n;
+}
+
+static int replay_checks(int nfiles, char** files) {
+  gpk_ctx* ctx = NULL;
+  int rc = gpk_ctx_create(&ctx, 0);
+  if (rc) {
+    fprintf(stderr, "gpk_ctx_create: %s %s\n", gpk_strerror(rc), gpk_last_hip_error());
+    return 2;
+  }
+  gpk_parser* p = make_parser(0);
+  for (int f = 0; f < nfiles; f++) {
+    /* the packets the capture holds, by the reader alone */
+    size_t len = 0;
+    uint8_t* raw = (uint8_t*)slurp(files[f][0] == '/' ? "" : ".", files[f], &len);
+    const int fmt = len >= 4 && raw[0] == 0x0A && raw[1] == 0x0D && raw[2] == 0x0D && raw[3] == 0x0A ? GPK_CAP_PCAPNG
+                                                                                                   : GPK_CAP_PCAP;
+    gpk_capreader* r = NULL;
+    gpk_capindex x = {0, NULL, NULL, NULL};
+    uint64_t used = 0;
+    CHECK(gpk_capreader_create(&r, fmt, 0) == GPK_OK, "capreader_create");
+    CHECK(gpk_capreader_index_all(r, raw, len, 1, 4, &x, &used) >= 0, "index_all");
+    gpk_capreader_destroy(r);
+    /* the same file through the GPU, small slots and batches: many launches */
+    struct replay_state st;
+    memset(&st, 0, sizeof(st));
+    gpk_replay_opts o;
+    memset(&o, 0, sizeof(o));
+    o.format = fmt;
+    o.slot_bytes = 1 << 20;
+    o.slots = 3;
+    o.batch_pkts = 777;
+    o.fields_cb = on_fields;
+    gpk_replay_stats s;
+    rc = gpk_replay_file(ctx, p, files[f], &o, on_results, &st, &s);
+    CHECK(rc == GPK_OK, "replay %s: %s %s", files[f], gpk_strerror(rc), s.error);
+    CHECK(st.packets == s.packets && s.packets == x.n, "%s: %llu delivered, stats %llu, reader %llu", files[f],
+          (unsigned long long)st.packets, (unsigned long long)s.packets, (unsigned long long)x.n);
+    const char* base = strrchr(files[f], '/') ? strrchr(files[f], '/') + 1 : files[f];
+    printf("replay %s: %llu packets, %llu checked against their fields\n", base,
+           (unsigned long long)st.packets, (unsigned long long)st.checked);
+    gpk_capindex_free(&x);
+    free(st.present);
+    free(raw);
+  }
+  gpk_parser_destroy(p);
+  gpk_ctx_destroy(ctx);
+  return 0;
+}
+
 int main(int argc, char** argv) {
   if (argc < 3) {
-    fprintf(stderr, "usage: %s host|decode <golden dir>\n", argv[0]);
+    fprintf(stderr, "usage: %s host|decode <golden dir> | replay <capture>...\n", argv[0]);
     return 2;
   }
   host_checks();
   if (strcmp(argv[1], "decode") == 0) {
     int rc = decode_checks(argv[2]);
+    if (rc) return rc;
+  } else if (strcmp(argv[1], "replay") == 0) {
+    int rc = replay_checks(argc - 2, argv + 2);
     if (rc) return rc;
   }
   if (failures) {
