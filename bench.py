@@ -679,11 +679,41 @@ def c5_replay(ctx, gib=10.0, reps=2, threads=8, cpu_threads=16):
             ok = np.array_equal(gfl, ref["flows"])
         return "%s (%d sampled packets vs oracle)" % ("bit-exact" if ok else "MISMATCH", len(idx))
 
+    fpicked = {}
+
+    def on_batch_fields(first, k, rec, err, fl, ci, cap, fields):
+        lo, hi = np.searchsorted(sample, first), np.searchsorted(sample, first + k)
+        for i in sample[lo:hi]:
+            fpicked[i] = fields[i - first:i - first + 1].copy()
+
+    def replay_fields(p):  # the fused decode + layer fields per launch (gpk_replay_opts.fields_cb)
+        rs = []
+        for _ in range(reps):
+            fpicked.clear()
+            _, r = ctx.replay_file(p, path, collect=False, on_batch=on_batch_fields, read_threads=threads,
+                                   fields=True)
+            rs.append(r)
+        return rs, dict(fpicked)
+
+    def check_fields(st, got_f):  # the sampled packets' fields against the oracle's extraction
+        idx = sorted(got_f)
+        pk = [synth.packet(4, i) for i in idx]
+        cap = np.array([len(x) for x in pk], np.uint32)
+        off = np.concatenate([[0], np.cumsum(cap[:-1], dtype=np.uint64)]).astype(np.uint64)
+        data = np.frombuffer(b"".join(pk) + bytes(16), np.uint8)
+        ref = O.OracleParser(17, ["ETHERNET", "DOT1Q", "IPV4", "IPV6", "IPV6_EXT", "TCP", "UDP", "PAYLOAD"],
+                             outputs=7).decode(data, off, cap, layouts=True)
+        want = O.extract_fields(data, off, ref["layouts"])
+        got = np.stack([got_f[i].view(np.uint8).reshape(-1) for i in idx])
+        ok = st["packets"] == n and len(idx) == len(sample) and np.array_equal(got, want)
+        return "%s (%d sampled packets' fields vs oracle)" % ("bit-exact" if ok else "MISMATCH", len(idx))
+
     cpu = None
     c1 = None
     try:
         runs, got4 = replay(parser)
         valid4 = valid[0]
+        runsf, gotf = replay_fields(parser)
         # the same file through C1's parser (Ethernet/IPv4/TCP/Payload, IPv4+TCP checksums): the
         # small-packet dword-aligned kernel on replay batches
         c1cfg = CONFIGS["c1"]
@@ -702,6 +732,13 @@ def c5_replay(ctx, gib=10.0, reps=2, threads=8, cpu_threads=16):
               runs_wall_s=[round(r["wall_s"], 4) for r in runs1], kernel=st1["kernel"],
               kernel_s=round(st1["kernel_s"], 4),
               parity=check(st1, got1, ["ETHERNET", "IPV4", "TCP", "PAYLOAD"], c1cfg["outputs"]))
+    stf = min(runsf, key=lambda x: x["wall_s"])
+    fields = dict(what="the same replay with gpk_replay_opts.fields_cb: every launch the fused decode + layer "
+                       "fields, 128 more bytes per packet copied back",
+                  value=round(stf["packets"] / stf["wall_s"] / 1e6, 2), unit="Mpkts/s",
+                  GBps=round(stf["file_bytes"] / stf["wall_s"] / 1e9, 2), wall_s=round(stf["wall_s"], 4),
+                  runs_wall_s=[round(r["wall_s"], 4) for r in runsf], kernel=stf["kernel"],
+                  kernel_s=round(stf["kernel_s"], 4), parity=check_fields(stf, gotf))
     w = st["wall_s"]
     w0 = runs[0]["wall_s"]
     return dict(workload="C5: pcapng replay of the C4 IMIX mix, end to end incl. HtoD/DtoH",
@@ -718,7 +755,7 @@ def c5_replay(ctx, gib=10.0, reps=2, threads=8, cpu_threads=16):
                 batches=st["batches"], slots=st["slots"], l4_valid=valid4, write_s=round(gen_s, 2),
                 kernel=st["kernel"], **probe,
                 frac_of_htod_probe=round(st["file_bytes"] / w / 1e9 / probe["htod_probe_GBps"], 4),
-                parity=parity, c1_parser=c1,
+                parity=parity, c1_parser=c1, fields=fields,
                 source="page-cached file in %s" % os.path.dirname(path), cpu_baseline=cpu)
 
 

@@ -369,6 +369,8 @@ def synth_lib():
         S.gpk_probe_free.restype = ctypes.c_int
         S.gpk_probe_d2d.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64]
         S.gpk_probe_d2d.restype = ctypes.c_int
+        S.gpk_probe_hostwrite.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_void_p]
+        S.gpk_probe_hostwrite.restype = ctypes.c_int
         S.gpk_synth_tpacket_v3.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int,
                                            ctypes.c_uint64, ctypes.c_int32, ctypes.c_uint32, ctypes.c_void_p]
         S.gpk_synth_tpacket_v3.restype = ctypes.c_uint64

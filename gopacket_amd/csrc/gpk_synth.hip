@@ -111,6 +111,20 @@ __global__ __launch_bounds__(256) void probe_read_kernel(const uint8_t* data, ui
   if (acc == 0x9e3779b9u) out[0] = acc;  // keep the loads live; practically never stores
 }
 
+// Host-write probe: 16-byte vector stores from the CUs straight into pinned
+// host memory (dst is a host pointer the device can address), grid-stride:
+// results written over the link by the kernel instead of a DtoH copy
+// (tools/duplex_probe.py).
+__global__ __launch_bounds__(256) void probe_hostwrite_kernel(uint8_t* dst, uint64_t nvec) {
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  u32x4* v = reinterpret_cast<u32x4*>(dst);
+  const uint64_t stride = (uint64_t)gridDim.x * 256;
+  for (uint64_t k = (uint64_t)blockIdx.x * 256 + threadIdx.x; k < nvec; k += stride) {
+    const uint32_t x = (uint32_t)k;
+    __builtin_nontemporal_store(u32x4{x, x ^ 1u, x ^ 2u, x ^ 3u}, v + k);
+  }
+}
+
 // Mixed probe: the streaming read of probe_read_kernel over data[0, nbytes)
 // and, at the same time, non-temporal 16-byte stores over wbuf[0, wbytes) (the
 // records / flows / fields a decode writes): the first `writers` blocks store,
@@ -832,6 +846,11 @@ int gpk_probe_mixed(const uint8_t* data, uint64_t nbytes, uint8_t* wbuf, uint64_
   if (writers < 0 || writers >= blocks) return -1;
   hipLaunchKernelGGL(probe_mixed_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, data, nbytes / 16, wbuf,
                      wbytes / 16, (uint32_t)writers, out);
+  return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+int gpk_probe_hostwrite(uint8_t* dst, uint64_t nbytes, int blocks, void* stream) {
+  hipLaunchKernelGGL(probe_hostwrite_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, dst, nbytes / 16);
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
