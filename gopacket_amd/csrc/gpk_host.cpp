@@ -599,10 +599,14 @@ static int note_launch(gpk_ctx* c, int k, hipStream_t s) {
 // Diagnostic builds (GPK_DIAG_TIMES) write per-wave timestamps here.
 static std::atomic<uint64_t*> g_diag{nullptr};
 
+constexpr uint64_t kMaxBatchPackets = ((1ull << 31) - 1) * 256;  // include/gpk.h gpk_batch
+
 static int make_params(gpk_ctx* c, const gpk_parser* p, const gpk_batch* b, const gpk_results* o,
                        gpk::KParams& P, uint64_t packet_bytes = 0) {
   if (!c || !p || !b) return GPK_EINVAL;
   if (b->n && (!b->data || !b->offsets || !b->caplens)) return GPK_EINVAL;
+  // one 256-packet tile per workgroup: the grid's x dimension bounds a batch
+  if (b->n > kMaxBatchPackets) return GPK_EINVAL;
   // 16-byte chunk reads never leave the 16-byte granule of a valid byte only
   // if the packet buffer itself is 16-byte aligned.
   if (((uintptr_t)b->data & 15) != 0) return GPK_EINVAL;

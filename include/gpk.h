@@ -343,7 +343,8 @@ int gpk_ctx_set_table_mode(gpk_ctx* ctx, int mode);
  * packet whose header window would reach past it, and every packet when
  * data_bytes is 0, uses 16-byte-aligned loads). Pass the packed buffer size
  * (or at least the summed capture lengths) for best results; never more than
- * the readable bytes of data. */
+ * the readable bytes of data. n: at most (2^31 - 1) * 256 packets per call
+ * (one workgroup per 256 packets), else GPK_EINVAL. */
 typedef struct gpk_batch {
   const uint8_t* data;
   const uint64_t* offsets;
