@@ -222,6 +222,7 @@ extern "C" int gpk_bpf_run(gpk_bpf* f, const gpk_batch* b, const uint32_t* wirel
   if (!f || !b || !ret || (b->n && (!b->data || !b->offsets || !b->caplens))) return GPK_EINVAL;
   if (!b->n) return GPK_OK;
   const uint64_t blocks = (b->n + kBlock - 1) / kBlock;
+  if (blocks > 0x7fffffffull) return GPK_EINVAL;  // the grid's x dimension
   hipLaunchKernelGGL(bpf_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, (hipStream_t)stream, f->prog, f->len,
                      b->data, b->offsets, b->caplens, wirelens, b->n, ret, (uint8_t*)nullptr);
   return hipGetLastError() == hipSuccess ? GPK_OK : GPK_EHIP;

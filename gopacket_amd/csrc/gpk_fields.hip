@@ -136,7 +136,7 @@ extern "C" int gpk_extract_fields(const gpk_batch* b, const gpk_layout* layouts,
   if (!b || (b->n && (!b->data || !b->offsets || !b->caplens || !layouts || !fields))) return GPK_EINVAL;
   if (!b->n) return GPK_OK;
   const uint64_t blocks = (b->n + kBlock - 1) / kBlock;
-  if (blocks > 0xffffffffull) return GPK_EINVAL;
+  if (blocks > 0x7fffffffull) return GPK_EINVAL;  // the grid's x dimension
   hipLaunchKernelGGL(fields_kernel, dim3((unsigned)blocks), dim3(kBlock), (kBlock / 64) * kWaveDw * 4, (hipStream_t)stream,
                      b->data, b->offsets, b->caplens, layouts, b->n, fields);
   return hipGetLastError() == hipSuccess ? GPK_OK : GPK_EHIP;
