@@ -235,10 +235,20 @@ class TPacket:
         got_fields = []
 
         def fcb(user, first, n, f):
-            got_fields[:] = [np.ctypeslib.as_array(ctypes.cast(f, ctypes.POINTER(ctypes.c_uint8)), (n * 128,)).view(
-                _lib.FIELDS_DTYPE) if n else np.zeros(0, _lib.FIELDS_DTYPE)]
+            got_fields[:] = [(first, n, np.ctypeslib.as_array(ctypes.cast(f, ctypes.POINTER(ctypes.c_uint8)),
+                                                               (n * 128,)).view(_lib.FIELDS_DTYPE)
+                              if n else np.zeros(0, _lib.FIELDS_DTYPE))]
 
-        def cb(user, first, n, rec, err, fl, ci, cap):
+        raised = []  # an exception inside a ctypes callback would be printed and dropped: kept for after the call
+
+        def cb(*args):
+            if not raised:
+                try:
+                    _cb(*args)
+                except BaseException as e:  # noqa: B902 (re-raised below, after the C call returns)
+                    raised.append(e)
+
+        def _cb(user, first, n, rec, err, fl, ci, cap):
             if not n:
                 return
             views = (np.ctypeslib.as_array(ctypes.cast(rec, ctypes.POINTER(ctypes.c_uint8)), (n * 16,)).view(
@@ -248,8 +258,10 @@ class TPacket:
                      np.ctypeslib.as_array(ctypes.cast(ci, ctypes.POINTER(ctypes.c_uint8)), (n * 24,)).view(
                          _lib.TPINFO_DTYPE),
                      np.ctypeslib.as_array(ctypes.cast(cap, ctypes.POINTER(ctypes.c_uint32)), (n,)))
-            if fields:
-                views = views + (got_fields[0],)
+            if fields:  # the library calls fields_cb for the same packets right before this
+                if not got_fields or got_fields[0][:2] != (first, n):
+                    raise RuntimeError("no layer fields delivered for packets %d..%d" % (first, first + n))
+                views = views + (got_fields.pop()[2],)
             if on_batch is not None:
                 on_batch(first, n, *views)
             if collect:
@@ -260,6 +272,8 @@ class TPacket:
         o = _lib.PumpOpts(batch_pkts, max_packets, 1 if wait else 0, inflight, c_fcb)
         st = _lib.PumpStats()
         rc = _lib.lib().gpk_tpacket_pump(ctx.h, parser.h, self.h, ctypes.byref(o), c_cb, None, ctypes.byref(st))
+        if raised:
+            raise raised[0]
         if rc != _lib.GPK_OK:
             raise _lib.GpkError("gpk_tpacket_pump: %d %s %s" % (rc, st.error.decode(errors="replace"),
                                                                 _lib.lib().gpk_last_hip_error().decode()))

@@ -153,3 +153,20 @@ def test_pump_fields(gpu_ctx, vlan, batch):
     ref = oracle_parser(CONFIGS["statsassembly"]).decode(data, off, cap, nthreads=8, layouts=True)
     assert_same(got, ref, "pump+fields")
     assert np.array_equal(got["fields"].view(np.uint8).reshape(-1, 128), O.extract_fields(data, off, ref["layouts"]))
+
+
+def test_pump_callback_exception_reaches_the_caller(gpu_ctx):
+    """An exception raised in on_batch is raised by Pump once the call returns."""
+    S = _lib.synth_lib()
+    bs, nb = 65536, 4
+    ring = np.zeros(bs * nb, np.uint8)
+    S.gpk_synth_tpacket_v3(ring.ctypes.data, bs, nb, synth.C4_IMIX, 3, 7, 0, None)
+    tp = afpacket.AttachRing(ring, afpacket.TPacketVersion3, afpacket.OptFrameSize(4096), afpacket.OptBlockSize(bs),
+                             afpacket.OptNumBlocks(nb))
+
+    def boom(first, n, *views):
+        raise KeyError("consumer")
+
+    with pytest.raises(KeyError):
+        tp.Pump(gpu_ctx, device_parser(CONFIGS["statsassembly"]), batch_pkts=100, collect=False, on_batch=boom)
+    tp.Close()

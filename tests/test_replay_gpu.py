@@ -235,3 +235,17 @@ def test_replay_fields(gpu_ctx, capture, cfg_name, slot_bytes, slots, batch):
     assert_same(got, ref, "replay+fields")
     want = O.extract_fields(data, off, ref["layouts"])
     assert np.array_equal(got["fields"].view(np.uint8).reshape(-1, 128), want)
+
+
+def test_replay_callback_exception_reaches_the_caller(gpu_ctx, capture):
+    """An exception raised in on_batch (inside the ctypes callback) is raised
+    by replay_file once the call returns, and the context stays usable."""
+    path, raw = capture
+
+    def boom(first, n, *views):
+        raise ValueError("consumer failed at packet %d" % first)
+
+    with pytest.raises(ValueError, match="consumer failed at packet 0"):
+        gpu_ctx.replay_file(device_parser(CONFIGS["statsassembly"]), path, collect=False, on_batch=boom,
+                            slot_bytes=1 << 20, slots=2, batch_pkts=5000)
+    check(gpu_ctx, path, raw, slot_bytes=1 << 20, slots=2, batch_pkts=5000)
