@@ -71,7 +71,7 @@ EXPORTS = (
     "gpk_parser_set_outputs", "gpk_parser_decoder_for", "gpk_parser_set_ethertype",
     "gpk_parser_set_ipprotocol", "gpk_parser_set_tcp_port", "gpk_parser_set_udp_port", "gpk_ctx_create",
     "gpk_ctx_destroy", "gpk_ctx_set_table_mode", "gpk_decode_batch", "gpk_decode_batch_fields", "gpk_extract_fields",
-    "gpk_decode_kernel_name", "gpk_decode_occupancy", "gpk_diag_set_buffer", "gpk_decode_batch_host",
+    "gpk_decode_kernel_name", "gpk_decode_occupancy", "gpk_diag_set_buffer", "gpk_decode_batch_host", "gpk_decode_batch_host_fields",
     "gpk_decoded_list",
     "gpk_decoded_list_host", "gpk_host_alloc", "gpk_host_free", "gpk_format_error", "gpk_layer_type_name", "gpk_code_layer_type", "gpk_strerror",
     "gpk_last_hip_error", "gpk_abi_version",
@@ -239,6 +239,7 @@ def lib():
         "gpk_ctx_set_table_mode": ([vp, c_int], c_int),
         "gpk_decode_batch": ([vp, vp, P(Batch), P(Results), vp], c_int),
         "gpk_decode_batch_host": ([vp, vp, P(Batch), P(Results)], c_int),
+        "gpk_decode_batch_host_fields": ([vp, vp, P(Batch), P(Results), vp], c_int),
         "gpk_extract_fields": ([P(Batch), vp, vp, vp], c_int),
         "gpk_decode_batch_fields": ([vp, vp, P(Batch), P(Results), vp, vp], c_int),
         "gpk_decode_kernel_name": ([vp, vp, P(Batch), c_int, ctypes.c_char_p, ctypes.c_size_t], c_int),

@@ -790,7 +790,10 @@ static int ensure_dbuf(gpk_ctx* c, size_t bytes) {
 
 static size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
 
-int gpk_decode_batch_host(gpk_ctx* c, const gpk_parser* p, const gpk_batch* hb, const gpk_results* ho) {
+// The host-buffer decode, with the layer fields when hf is non-null (fused
+// launch, or with layouts the decode then gpk_extract_fields, as
+// gpk_decode_batch_fields does on the device).
+static int decode_host(gpk_ctx* c, const gpk_parser* p, const gpk_batch* hb, const gpk_results* ho, gpk_fields* hf) {
   if (!c || !p || !hb || !ho) return GPK_EINVAL;
   if (hb->n && (!hb->data || !hb->offsets || !hb->caplens || !ho->records)) return GPK_EINVAL;
   const uint64_t n = hb->n;
@@ -799,7 +802,8 @@ int gpk_decode_batch_host(gpk_ctx* c, const gpk_parser* p, const gpk_batch* hb, 
   size_t o_data = 0, o_off = align_up(o_data + hb->data_bytes + 16), o_cap = align_up(o_off + n * 8),
          o_rec = align_up(o_cap + n * 4), o_err = align_up(o_rec + n * sizeof(gpk_record)),
          o_fl = align_up(o_err + (ho->err_args ? n * 8 : 0)), o_lay = align_up(o_fl + (flows ? n * 24 : 0)),
-         total = align_up(o_lay + (ho->layouts ? n * sizeof(gpk_layout) : 0));
+         o_fld = align_up(o_lay + (ho->layouts ? n * sizeof(gpk_layout) : 0)),
+         total = align_up(o_fld + (hf ? n * sizeof(gpk_fields) : 0));
   std::lock_guard<std::mutex> g(c->mu);
   HIPCHK(hipSetDevice(c->device));
   int rc = ensure_dbuf(c, total);
@@ -820,15 +824,36 @@ int gpk_decode_batch_host(gpk_ctx* c, const gpk_parser* p, const gpk_batch* hb, 
   int slot = 0;
   rc = upload(c, p, P, &slot, s);
   if (rc) return rc;
-  HIPCHK(gpk_launch_decode(&P, (p->outputs & GPK_OUT_L4_CSUM) != 0, dr.layouts != nullptr, s));
+  gpk_fields* df = hf ? (gpk_fields*)(d + o_fld) : nullptr;
+  if (df && !dr.layouts) {
+    P.fields = df;
+    HIPCHK(gpk_launch_decode_fields(&P, s, nullptr));
+  } else {
+    HIPCHK(gpk_launch_decode(&P, (p->outputs & GPK_OUT_L4_CSUM) != 0, dr.layouts != nullptr, s));
+  }
   rc = note_launch(c, slot, s);
   if (rc) return rc;
+  if (df && dr.layouts && n) {
+    rc = gpk_extract_fields(&db, dr.layouts, df, s);
+    if (rc) return rc;
+  }
   HIPCHK(hipMemcpyAsync(ho->records, dr.records, n * sizeof(gpk_record), hipMemcpyDeviceToHost, s));
   if (ho->err_args) HIPCHK(hipMemcpyAsync(ho->err_args, dr.err_args, n * 8, hipMemcpyDeviceToHost, s));
   if (flows) HIPCHK(hipMemcpyAsync(ho->flows, dr.flows, n * 24, hipMemcpyDeviceToHost, s));
   if (ho->layouts) HIPCHK(hipMemcpyAsync(ho->layouts, dr.layouts, n * sizeof(gpk_layout), hipMemcpyDeviceToHost, s));
+  if (df) HIPCHK(hipMemcpyAsync(hf, df, n * sizeof(gpk_fields), hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
   return GPK_OK;
+}
+
+int gpk_decode_batch_host(gpk_ctx* c, const gpk_parser* p, const gpk_batch* hb, const gpk_results* ho) {
+  return decode_host(c, p, hb, ho, nullptr);
+}
+
+int gpk_decode_batch_host_fields(gpk_ctx* c, const gpk_parser* p, const gpk_batch* hb, const gpk_results* ho,
+                                 gpk_fields* host_fields) {
+  if (hb && hb->n && !host_fields) return GPK_EINVAL;
+  return decode_host(c, p, hb, ho, host_fields);
 }
 
 int gpk_decoded_list(gpk_ctx* c, const gpk_parser* p, const gpk_batch* b, uint64_t index, int64_t* out_types,

@@ -84,8 +84,11 @@ class Context:
         """_lib.TABLES_AUTO (compact LDS tables when they fit) or TABLES_GLOBAL."""
         check(lib().gpk_ctx_set_table_mode(self.h, int(mode)))
 
-    def decode_host(self, parser, data, offsets, caplens, layouts=False):
-        """Host batch in, host results out (copies HtoD, decodes, copies DtoH)."""
+    def decode_host(self, parser, data, offsets, caplens, layouts=False, fields=False):
+        """Host batch in, host results out (copies HtoD, decodes, copies DtoH).
+        fields=True: gpk_decode_batch_host_fields, the results gain "fields"
+        (FIELDS_DTYPE per packet; the fused launch, or with layouts the decode
+        then the extraction)."""
         data = np.ascontiguousarray(data, dtype=np.uint8)
         offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
         caplens = np.ascontiguousarray(caplens, dtype=np.uint32)
@@ -99,6 +102,11 @@ class Context:
         b = _lib.Batch(data.ctypes.data, offsets.ctypes.data, caplens.ctypes.data, n, len(data))
         r = _lib.Results(rec.ctypes.data, err.ctypes.data, flows.ctypes.data,
                          lay.ctypes.data if layouts else None)
+        if fields:
+            fld = np.zeros(n, _lib.FIELDS_DTYPE)
+            check(lib().gpk_decode_batch_host_fields(self.h, parser.h, ctypes.byref(b), ctypes.byref(r),
+                                                     fld.ctypes.data if n else None))
+            return dict(records=rec, err_args=err, flows=flows, layouts=lay, fields=fld)
         check(lib().gpk_decode_batch_host(self.h, parser.h, ctypes.byref(b), ctypes.byref(r)))
         return dict(records=rec, err_args=err, flows=flows, layouts=lay)
 
@@ -140,40 +148,12 @@ class Context:
 
     def decode_host_fields(self, parser, data, offsets, caplens, layouts=True):
         """decode_host plus the layer fields of every packet, both computed on
-        the device (host arrays in and out; torch for the buffers). layouts=True:
-        the decode with layouts, then extract_fields from them (two launches);
-        False: the fused decode + fields launch (gpk_decode_batch_fields), no
-        layouts returned."""
-        import torch
-        data = np.ascontiguousarray(data, dtype=np.uint8)
-        if not data.flags.writeable:  # torch.from_numpy wants a writable array (read-only views of bytes)
-            data = data.copy()
-        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
-        caplens = np.ascontiguousarray(caplens, dtype=np.uint32)
-        n = len(offsets)
-        if n and np.any(offsets + caplens.astype(np.uint64) > len(data)):
-            raise ValueError("packet range outside the data buffer")
-        dev = torch.device("cuda", self.device)
-        d_data = torch.zeros(len(data) + 32, dtype=torch.uint8, device=dev)  # 16-byte slack after the packets
-        d_data[:len(data)] = torch.from_numpy(data).to(dev)
-        d_off = torch.from_numpy(offsets.view(np.int64)).to(dev)
-        d_cap = torch.from_numpy(caplens.view(np.int32)).to(dev)
-        rec = torch.empty(n * 16, dtype=torch.uint8, device=dev)
-        err = torch.zeros(2 * n, dtype=torch.int32, device=dev)
-        fl = torch.zeros(3 * n, dtype=torch.int64, device=dev)
-        lay = torch.empty(n * 64, dtype=torch.uint8, device=dev) if layouts else None
-        fields = torch.empty(n * 128, dtype=torch.uint8, device=dev)
-        stream = torch.cuda.current_stream(dev)
-        if layouts:
-            self.decode_device(parser, d_data, d_off, d_cap, rec, err, fl, lay, stream=stream)
-            self.extract_fields(d_data, d_off, d_cap, lay, fields, stream=stream)
-        else:
-            self.decode_device_fields(parser, d_data, d_off, d_cap, rec, err, fl, fields, stream=stream)
-        torch.cuda.synchronize(dev)
-        return (dict(records=rec.cpu().numpy().view(_lib.RECORD_DTYPE), err_args=err.cpu().numpy().view(np.uint32),
-                     flows=fl.cpu().numpy().view(np.uint64),
-                     layouts=lay.cpu().numpy().view(_lib.LAYOUT_DTYPE) if layouts else None),
-                fields.cpu().numpy().view(_lib.FIELDS_DTYPE))
+        the device (gpk_decode_batch_host_fields; host arrays in and out).
+        layouts=True: the decode with layouts, then extract_fields from them
+        (two launches); False: the fused decode + fields launch, no layouts
+        returned. Returns (results, fields)."""
+        r = self.decode_host(parser, data, offsets, caplens, layouts=layouts, fields=True)
+        return r, r.pop("fields")
 
     def kernel_name(self, parser, data, offsets, caplens, layouts=False):
         """The decode kernel specialisation decode_device (torch tensors) or

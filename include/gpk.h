@@ -405,6 +405,13 @@ int gpk_diag_set_buffer(void* buf);
  * via gpk_host_alloc). Copies HtoD, decodes, copies DtoH; synchronous. */
 int gpk_decode_batch_host(gpk_ctx* ctx, const gpk_parser* p, const gpk_batch* host_batch,
                           const gpk_results* host_out);
+/* The same with the layer fields of every packet (gpk_fields, as
+ * gpk_decode_batch_fields writes them) into host memory host_fields[n]: the
+ * fused decode + fields launch, or with host_out->layouts the decode and then
+ * gpk_extract_fields. For callers whose packets are in host memory (a cgo
+ * caller without device buffers of its own). Synchronous. */
+int gpk_decode_batch_host_fields(gpk_ctx* ctx, const gpk_parser* p, const gpk_batch* host_batch,
+                                 const gpk_results* host_out, gpk_fields* host_fields);
 
 /* Full decoded list of a packet whose list is longer than 16 entries
  * (gpk_record_nlayers > 16). Device batch, device result not needed; writes

@@ -50,6 +50,8 @@ static int failures = 0;
     }                                            \
   } while (0)
 
+static int code_slot(unsigned code);
+
 static void* slurp(const char* dir, const char* name, size_t* len) {
   char path[4096];
   snprintf(path, sizeof(path), "%s/%s", dir, name);
@@ -210,7 +212,33 @@ static int decode_checks(const char* dir) {
       if (nl) *nl = '\n';
       line = nl ? nl + 1 : NULL;
     }
-    printf("%s: %u packets, %d error texts checked\n", names[cfg], n, texts);
+    /* the same batch with the layer fields (host buffers): the same records, and
+       for every packet without error the decoders the fields mark present are
+       the ones its decoded list names */
+    gpk_fields* hf = (gpk_fields*)malloc(sizeof(gpk_fields) * (size_t)n);
+    gpk_record* rec2 = (gpk_record*)malloc(16 * (size_t)n);
+    uint64_t* fl2 = (uint64_t*)malloc(24 * (size_t)n);
+    gpk_results r2 = {rec2, NULL, fl2, NULL};
+    rc = gpk_decode_batch_host_fields(ctx, p, &b, &r2, hf);
+    CHECK(rc == GPK_OK, "decode with fields %s: %s", names[cfg], gpk_strerror(rc));
+    CHECK(memcmp(rec2, rec, 16 * (size_t)n) == 0, "%s: records differ with fields", names[cfg]);
+    int present_checked = 0;
+    for (uint32_t i = 0; i < n && rc == GPK_OK; i++) {
+      const unsigned nl = gpk_record_nlayers(&rec[i]);
+      if (gpk_record_err(&rec[i]) || nl > 16) continue;
+      unsigned want = 0;
+      for (unsigned k = 0; k < nl; k++) {
+        const int sl = code_slot((unsigned)(rec[i].layers >> (4 * k)) & 0xF);
+        if (sl >= 0) want |= 1u << sl;
+      }
+      CHECK(hf[i].present == want, "%s packet %u: present %#x, decoded %#x", names[cfg], i, hf[i].present, want);
+      present_checked++;
+    }
+    free(hf);
+    free(rec2);
+    free(fl2);
+    printf("%s: %u packets, %d error texts checked, %d fields records checked\n", names[cfg], n, texts,
+           present_checked);
     gpk_parser_destroy(p);
   }
   gpk_ctx_destroy(ctx);

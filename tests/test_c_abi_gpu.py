@@ -21,6 +21,7 @@ def test_c_abi_decode_mode():
     assert out.returncode == 0, out.stdout + out.stderr
     assert "all checks passed (decode)" in out.stdout
     assert "statsassembly: 639 packets" in out.stdout
+    assert "fields records checked" in out.stdout
 
 
 def test_c_abi_replay_with_fields(tmp_path):
