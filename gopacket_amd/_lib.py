@@ -162,12 +162,15 @@ class NgInterface(ctypes.Structure):
 
 # gpk_replay_fields_cb(user, first_packet, n, const gpk_fields*)
 REPLAY_FIELDS_CB = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p)
+# gpk_replay_packets_cb(user, first_packet, n, base, offsets, caplens)
+REPLAY_PACKETS_CB = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p,
+                                     ctypes.c_void_p, ctypes.c_void_p)
 
 
 class ReplayOpts(ctypes.Structure):
     _fields_ = [("format", ctypes.c_int), ("ng_flags", ctypes.c_uint32), ("slot_bytes", ctypes.c_uint64),
                 ("slots", ctypes.c_int), ("batch_pkts", ctypes.c_uint64), ("read_threads", ctypes.c_int),
-                ("fields_cb", REPLAY_FIELDS_CB)]
+                ("fields_cb", REPLAY_FIELDS_CB), ("packets_cb", REPLAY_PACKETS_CB)]
 
 
 class ReplayStats(ctypes.Structure):

@@ -202,6 +202,8 @@ struct Bat {
   hipEvent_t e0 = nullptr, k0 = nullptr, k1 = nullptr, done = nullptr;
   uint64_t first = 0, n = 0, flows_n = 0;
   bool with_fields = false;  // this launch wrote fields
+  const uint8_t* base = nullptr;  // opts.packets_cb: the staging bytes h_off is relative to
+  int slot = -1;                  // ... and their slot, held until this batch is delivered
 };
 
 struct Pipeline {
@@ -211,6 +213,8 @@ struct Pipeline {
   uint64_t P = 0;
   gpk_replay_cb cb = nullptr;
   gpk_replay_fields_cb fields_cb = nullptr;
+  gpk_replay_packets_cb packets_cb = nullptr;
+  std::vector<int> slot_batches;  // undelivered batches per staging slot (packets_cb)
   void* user = nullptr;
   gpk_replay_stats* st = nullptr;
   std::string herr;
@@ -237,6 +241,10 @@ struct Pipeline {
     if (hipEventElapsedTime(&kms, B.k0, B.k1) == hipSuccess) st->kernel_s += kms * 1e-3;
     double t = now_s();
     for (uint64_t i = 0; i < B.n; i++) st->packet_bytes += B.h_cap[i];
+    if (packets_cb && B.base) packets_cb(user, B.first, B.n, B.base, B.h_off, B.h_cap);
+    if (B.slot >= 0 && (size_t)B.slot < slot_batches.size()) slot_batches[B.slot]--;
+    B.slot = -1;
+    B.base = nullptr;
     if (fields_cb && B.with_fields) fields_cb(user, B.first, B.n, B.h_fields);  // before the batch's results
     if (cb) cb(user, B.first, B.n, B.h_rec, B.h_err, B.h_flow, B.h_ci, B.h_cap);
     st->deliver_s += now_s() - t;
@@ -405,9 +413,10 @@ void free_cached(void* p) {
 static int replay_file(gpk_ctx* ctx, const gpk_parser* parser, const char* path, const gpk_replay_opts* o,
                        gpk_replay_cb cb, void* user, gpk_replay_stats* stats) {
   const double t_start = now_s();
-  gpk_replay_opts opt{0, 0, 256ull << 20, 4, 1ull << 20, 8, nullptr};
+  gpk_replay_opts opt{0, 0, 256ull << 20, 4, 1ull << 20, 8, nullptr, nullptr};
   if (o) {
     opt.fields_cb = o->fields_cb;
+    opt.packets_cb = o->packets_cb;
     opt.format = o->format;
     opt.ng_flags = o->ng_flags;
     if (o->slot_bytes) opt.slot_bytes = o->slot_bytes;
@@ -494,6 +503,7 @@ static int replay_file(gpk_ctx* ctx, const gpk_parser* parser, const char* path,
   Pipeline pl;
   pl.cb = cb;
   pl.fields_cb = opt.fields_cb;
+  pl.packets_cb = opt.packets_cb;
   pl.user = user;
   pl.st = stats;
   pl.P = opt.batch_pkts;
@@ -623,6 +633,9 @@ static int replay_file(gpk_ctx* ctx, const gpk_parser* parser, const char* path,
   auto fill_ahead = [&](uint64_t upto) {  // issue the fills of slots [next_fill, upto)
     while (good && next_fill < upto) {
       Slot& N = pl.slots[next_fill % pl.slots.size()];
+      // packets_cb: the slot's bytes are the packets its batches hand out
+      while (good && pl.packets_cb && pl.slot_batches[next_fill % pl.slots.size()] > 0 && !pl.inflight.empty())
+        good = pl.deliver_oldest();
       if (N.h2d_pending) {  // the slot's last HtoD read the host bytes about to be overwritten
         good = pl.ok(hipEventSynchronize(N.h2d), "hipEventSynchronize");
         N.h2d_pending = false;
@@ -639,6 +652,7 @@ static int replay_file(gpk_ctx* ctx, const gpk_parser* parser, const char* path,
   uint64_t carry_len = 0, packet_index = 0;
   bool finished = false;
   rc = GPK_OK;
+  pl.slot_batches.assign(pl.slots.size(), 0);
   fill_ahead(1);
   for (uint64_t si = 0; !finished && good; si++) {
     Slot& S = pl.slots[si % pl.slots.size()];
@@ -860,6 +874,11 @@ static int replay_file(gpk_ctx* ctx, const gpk_parser* parser, const char* path,
       }
       B.first = packet_index;
       B.n = n;
+      if (pl.packets_cb) {  // the packets stay in this slot's staging bytes until delivered
+        B.slot = (int)(si % pl.slots.size());
+        B.base = dwalk ? S.host + base_off : S.host + start;
+        pl.slot_batches[B.slot]++;
+      }
       good = good && pl.ok(hipEventRecord(B.e0, S.stream), "hipEventRecord");
       if (!dwalk)
         good = good &&
@@ -900,6 +919,9 @@ static int replay_file(gpk_ctx* ctx, const gpk_parser* parser, const char* path,
       if (B.with_fields)
         good = good && pl.ok(hipMemcpyAsync(B.h_fields, B.d_fields, n * sizeof(gpk_fields), hipMemcpyDeviceToHost,
                                             S.stream), "DtoH fields");
+      if (dwalk && pl.packets_cb)  // the device walk's offsets, for the packets' bytes on the host
+        good = good && pl.ok(hipMemcpyAsync(B.h_off, S.d_off + first, n * 8, hipMemcpyDeviceToHost, S.stream),
+                             "DtoH offsets");
       if (dwalk)
         good = good &&
                pl.ok(hipMemcpyAsync(B.h_cap, S.d_cap + first, n * 4, hipMemcpyDeviceToHost, S.stream), "DtoH caplens") &&

@@ -176,7 +176,7 @@ class Context:
         return out.value
 
     def replay_file(self, parser, path, fmt=0, ng_flags=0, slot_bytes=0, slots=0, batch_pkts=0, read_threads=0,
-                    collect=True, on_batch=None, fields=False):
+                    collect=True, on_batch=None, fields=False, packets=False):
         """gpk_replay_file: the whole capture through HBM (BASELINE config C5).
         collect=True gathers every result (records, err_args, flows SoA, ci,
         caplens) in packet order; on_batch(first, n, records, err_args, flows,
@@ -184,8 +184,24 @@ class Context:
         call). fields=True: every launch is the fused decode + layer fields
         (gpk_replay_opts.fields_cb): the results gain "fields" (FIELDS_DTYPE
         per packet), and on_batch a last argument, the launch's fields.
-        Returns (results-or-None, stats dict)."""
+        packets=True (collect=False only): on_batch also gets, last, the
+        launch's packets as (data, offsets, caplens): packet i is
+        data[offsets[i]:offsets[i] + caplens[i]], a view of the staging buffer
+        the file was read into (gpk_replay_opts.packets_cb; no copy, valid
+        during the call). Returns (results-or-None, stats dict)."""
+        if packets and collect:
+            raise ValueError("packets=True hands out views of the staging buffers: use collect=False and on_batch")
         parts = []
+        got_packets = []
+
+        def pcb(user, first, n, base, off, cap):
+            if not n:
+                return
+            o = np.ctypeslib.as_array(ctypes.cast(off, ctypes.POINTER(ctypes.c_uint64)), (n,))
+            c = np.ctypeslib.as_array(ctypes.cast(cap, ctypes.POINTER(ctypes.c_uint32)), (n,))
+            end = int((o + c.astype(np.uint64)).max())
+            data = np.ctypeslib.as_array(ctypes.cast(base, ctypes.POINTER(ctypes.c_uint8)), (max(end, 1),))
+            got_packets[:] = [(first, n, (data, o, c))]
         got_fields = []  # the current launch's fields (fields_cb runs right before cb)
 
         def fcb(user, first, n, f):
@@ -216,6 +232,10 @@ class Context:
                 if not got_fields or got_fields[0][:2] != (first, n):
                     raise RuntimeError("no layer fields delivered for packets %d..%d" % (first, first + n))
                 views = views + (got_fields.pop()[2],)
+            if packets:
+                if not got_packets or got_packets[0][:2] != (first, n):
+                    raise RuntimeError("no packets delivered for packets %d..%d" % (first, first + n))
+                views = views + (got_packets.pop()[2],)
             if on_batch is not None:
                 on_batch(first, n, *views)
             if collect:
@@ -223,7 +243,8 @@ class Context:
 
         c_cb = _lib.REPLAY_CB(cb)
         c_fcb = _lib.REPLAY_FIELDS_CB(fcb) if fields else _lib.REPLAY_FIELDS_CB()
-        o = _lib.ReplayOpts(fmt, ng_flags, slot_bytes, slots, batch_pkts, read_threads, c_fcb)
+        c_pcb = _lib.REPLAY_PACKETS_CB(pcb) if packets else _lib.REPLAY_PACKETS_CB()
+        o = _lib.ReplayOpts(fmt, ng_flags, slot_bytes, slots, batch_pkts, read_threads, c_fcb, c_pcb)
         st = _lib.ReplayStats()
         rc = lib().gpk_replay_file(self.h, parser.h, path.encode() if isinstance(path, str) else path,
                                    ctypes.byref(o), c_cb, None, ctypes.byref(st))

@@ -260,8 +260,10 @@ static int decode_checks(const char* dir) {
  * every packet decoded without error a record whose decoded list names exactly
  * the decoders the fields record marks present (gpk.h gpk_fields.present). */
 struct replay_state {
-  uint64_t next_first, fields_first, fields_n, packets, checked;
+  uint64_t next_first, fields_first, fields_n, packets, checked, bytes_checked;
   int have_fields;
+  const uint8_t* raw;      /* the capture file and the reader's index of it, to */
+  const gpk_capindex* x;   /* check the packets the replay hands out            */
   uint8_t* present; /* this batch's present bytes (fields valid during the callback only) */
   uint64_t cap;
 };
@@ -277,6 +279,23 @@ static void on_fields(void* user, uint64_t first, uint64_t n, const gpk_fields* 
   st->fields_first = first;
   st->fields_n = n;
   st->have_fields = 1;
+}
+
+static void on_packets(void* user, uint64_t first, uint64_t n, const uint8_t* base, const uint64_t* offsets,
+                       const uint32_t* caplens) {
+  struct replay_state* st = (struct replay_state*)user;
+  for (uint64_t i = 0; i < n; i++) {
+    const uint64_t k = first + i;
+    if (k >= st->x->n) {
+      CHECK(0, "packet %llu past the reader's %llu", (unsigned long long)k, (unsigned long long)st->x->n);
+      return;
+    }
+    if (caplens[i] != st->x->caplens[k] || memcmp(base + offsets[i], st->raw + st->x->offsets[k], caplens[i]) != 0) {
+      CHECK(0, "packet %llu: bytes differ from the reader's", (unsigned long long)k);
+      return;
+    }
+    st->bytes_checked++;
+  }
 }
 
 static int code_slot(unsigned code) { /* decoded-list code -> gpk_fields.present bit */
@@ -354,11 +373,16 @@ static int replay_checks(int nfiles, char** files) {
     o.slots = 3;
     o.batch_pkts = 777;
     o.fields_cb = on_fields;
+    o.packets_cb = on_packets;
+    st.raw = raw;
+    st.x = &x;
     gpk_replay_stats s;
     rc = gpk_replay_file(ctx, p, files[f], &o, on_results, &st, &s);
     CHECK(rc == GPK_OK, "replay %s: %s %s", files[f], gpk_strerror(rc), s.error);
     CHECK(st.packets == s.packets && s.packets == x.n, "%s: %llu delivered, stats %llu, reader %llu", files[f],
           (unsigned long long)st.packets, (unsigned long long)s.packets, (unsigned long long)x.n);
+    CHECK(st.bytes_checked == x.n, "%s: %llu packets' bytes checked of %llu", files[f],
+          (unsigned long long)st.bytes_checked, (unsigned long long)x.n);
     const char* base = strrchr(files[f], '/') ? strrchr(files[f], '/') + 1 : files[f];
     printf("replay %s: %llu packets, %llu checked against their fields\n", base,
            (unsigned long long)st.packets, (unsigned long long)st.checked);

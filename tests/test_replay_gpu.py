@@ -249,3 +249,38 @@ def test_replay_callback_exception_reaches_the_caller(gpu_ctx, capture):
         gpu_ctx.replay_file(device_parser(CONFIGS["statsassembly"]), path, collect=False, on_batch=boom,
                             slot_bytes=1 << 20, slots=2, batch_pkts=5000)
     check(gpu_ctx, path, raw, slot_bytes=1 << 20, slots=2, batch_pkts=5000)
+
+
+def test_replay_packets_and_hydrate(gpu_ctx, capture):
+    """packets=True: every launch's packet bytes as views of the staging
+    buffers (gpk_replay_opts.packets_cb), delivered with the fields and the
+    results; small slots force the slots to be refilled, which must wait for
+    their packets to be handed out. Every packet's bytes equal the reader
+    oracle's, and layer structs hydrated from the fields record over those
+    bytes equal a host-side decode's of the same packets."""
+    import hydrate_cases as H
+    from gopacket_amd import gopacket as G
+    path, raw = capture
+    res, pk = packets_and_expect(raw)
+    seen = []
+    pf, pr = H.parser(), H.parser()
+    pf._ctx = pr._ctx = gpu_ctx
+
+    def on_batch(first, n, rec, err, fl, ci, cap, fields, packets):
+        data, off, caps = packets
+        assert np.array_equal(caps, cap)
+        for i in range(n):
+            assert bytes(data[off[i]:off[i] + caps[i]]) == pk[first + i], first + i
+        k = min(n, 300)
+        rb = G.BatchResult(pf, G.PacketBatch(data, off, caps),
+                           dict(records=rec.copy(), err_args=err.copy(), flows=fl.copy(), layouts=None))
+        rb.fields = fields.copy()
+        ra = pr.DecodeBatch(G.PacketBatch.from_packets(pk[first:first + k]), layouts=True)
+        H.compare(ra, rb, pr, pf, range(k))
+        seen.append(n)
+
+    _, st = gpu_ctx.replay_file(device_parser(CONFIGS["statsassembly"]), path, slot_bytes=1 << 20, slots=2,
+                                batch_pkts=4000, collect=False, on_batch=on_batch, fields=True, packets=True)
+    assert st["packets"] == len(pk) == sum(seen)
+    with pytest.raises(ValueError):
+        gpu_ctx.replay_file(device_parser(CONFIGS["statsassembly"]), path, packets=True)
