@@ -123,9 +123,14 @@ class TpOpts(ctypes.Structure):
 PUMP_FIELDS_CB = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p)
 
 
+# gpk_tp_pump_packets_cb(user, first_packet, n, const uint8_t* const* data, const uint32_t* caplens)
+PUMP_PACKETS_CB = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p,
+                                   ctypes.c_void_p)
+
+
 class PumpOpts(ctypes.Structure):
     _fields_ = [("batch_pkts", ctypes.c_uint64), ("max_packets", ctypes.c_uint64), ("wait", ctypes.c_int),
-                ("inflight", ctypes.c_int), ("fields_cb", PUMP_FIELDS_CB)]
+                ("inflight", ctypes.c_int), ("fields_cb", PUMP_FIELDS_CB), ("packets_cb", PUMP_PACKETS_CB)]
 
 
 class PumpStats(ctypes.Structure):

@@ -225,14 +225,27 @@ class TPacket:
         _lib.check(_lib.lib().gpk_tpacket_set_fanout(self.h, int(t), int(id_)))
 
     def Pump(self, ctx, parser, batch_pkts=0, max_packets=0, wait=False, inflight=0, collect=True, on_batch=None,
-             fields=False):
+             fields=False, packets=False):
         """gpk_tpacket_pump: drain the ring through HBM and the decoder. Returns
         (results-or-None, stats dict); results as Context.replay_file's, with
         ci of TPINFO_DTYPE. fields=True: every launch is the fused decode +
         layer fields (gpk_tp_pump_opts.fields_cb); results gain "fields" and
-        on_batch a last argument, as in replay_file."""
+        on_batch a last argument, as in replay_file. packets=True (collect=False
+        only): on_batch also gets, last, (pointers, caplens): packet i's bytes
+        are ctypes.string_at(pointers[i], caplens[i]) (a ring frame or its VLAN
+        copy, valid during the call); ring headers go back to the kernel once
+        their batch was delivered."""
+        if packets and collect:
+            raise ValueError("packets=True hands out views of the ring: use collect=False and on_batch")
         parts = []
         got_fields = []
+        got_packets = []
+
+        def pcb(user, first, n, data, cap):
+            if n:
+                got_packets[:] = [(first, n, (
+                    np.ctypeslib.as_array(ctypes.cast(data, ctypes.POINTER(ctypes.c_uint64)), (n,)),
+                    np.ctypeslib.as_array(ctypes.cast(cap, ctypes.POINTER(ctypes.c_uint32)), (n,))))]
 
         def fcb(user, first, n, f):
             got_fields[:] = [(first, n, np.ctypeslib.as_array(ctypes.cast(f, ctypes.POINTER(ctypes.c_uint8)),
@@ -262,6 +275,10 @@ class TPacket:
                 if not got_fields or got_fields[0][:2] != (first, n):
                     raise RuntimeError("no layer fields delivered for packets %d..%d" % (first, first + n))
                 views = views + (got_fields.pop()[2],)
+            if packets:
+                if not got_packets or got_packets[0][:2] != (first, n):
+                    raise RuntimeError("no packets delivered for packets %d..%d" % (first, first + n))
+                views = views + (got_packets.pop()[2],)
             if on_batch is not None:
                 on_batch(first, n, *views)
             if collect:
@@ -269,7 +286,8 @@ class TPacket:
 
         c_cb = _lib.PUMP_CB(cb)
         c_fcb = _lib.PUMP_FIELDS_CB(fcb) if fields else _lib.PUMP_FIELDS_CB()
-        o = _lib.PumpOpts(batch_pkts, max_packets, 1 if wait else 0, inflight, c_fcb)
+        c_pcb = _lib.PUMP_PACKETS_CB(pcb) if packets else _lib.PUMP_PACKETS_CB()
+        o = _lib.PumpOpts(batch_pkts, max_packets, 1 if wait else 0, inflight, c_fcb, c_pcb)
         st = _lib.PumpStats()
         rc = _lib.lib().gpk_tpacket_pump(ctx.h, parser.h, self.h, ctypes.byref(o), c_cb, None, ctypes.byref(st))
         if raised:

@@ -1025,15 +1025,19 @@ struct PBat {
 
 static int tpacket_pump(gpk_ctx* ctx, const gpk_parser* parser, gpk_tpacket* t, const gpk_tp_pump_opts* o,
                         gpk_tp_pump_cb cb, void* user, gpk_tp_pump_stats* st) {
-  gpk_tp_pump_opts opt{1ull << 20, 0, 0, 4, nullptr};
+  gpk_tp_pump_opts opt{1ull << 20, 0, 0, 4, nullptr, nullptr};
   if (o) {
     if (o->batch_pkts) opt.batch_pkts = o->batch_pkts;
     opt.max_packets = o->max_packets;
     opt.wait = o->wait;
     if (o->inflight > 0) opt.inflight = o->inflight;
     opt.fields_cb = o->fields_cb;
+    opt.packets_cb = o->packets_cb;
   }
   const bool with_fields = opt.fields_cb != nullptr;
+  // packets_cb: ring headers stay the user's until their batch was delivered
+  const bool hold = opt.packets_cb != nullptr;
+  std::vector<const uint8_t*> ptrs(hold ? opt.batch_pkts : 0);
   const uint64_t P = opt.batch_pkts;
   const int NB = std::max(2, opt.inflight);
   const uint64_t side_cap = std::min<uint64_t>(64ull << 20, std::max<uint64_t>(1ull << 20, P * 256));
@@ -1085,6 +1089,7 @@ static int tpacket_pump(gpk_ctx* ctx, const gpk_parser* parser, gpk_tpacket* t, 
   int rc = GPK_OK;
 
   auto release_done = [&](bool block) {  // hand back headers whose HtoD has completed
+    if (hold) return true;  // ... only once delivered (deliver_oldest)
     for (int s : order) {
       PBat& b = B[s];
       if (!b.h2d_pending) continue;
@@ -1102,15 +1107,24 @@ static int tpacket_pump(gpk_ctx* ctx, const gpk_parser* parser, gpk_tpacket* t, 
     order.pop_front();
     PBat& b = B[s];
     if (!ok(hipEventSynchronize(b.done), "hipEventSynchronize")) return false;
-    if (b.h2d_pending) {
+    if (b.h2d_pending && !hold) {
       b.h2d_pending = false;
       gpk_tpacket_release(t, b.rel_seq);
     }
     float ms = 0, kms = 0;
     if (hipEventElapsedTime(&ms, b.e0, b.done) == hipSuccess) st->gpu_s += ms * 1e-3;
     if (hipEventElapsedTime(&kms, b.k0, b.k1) == hipSuccess) st->kernel_s += kms * 1e-3;
+    if (hold) {  // the packets: ring frames, or this slot's VLAN copies (h_off moved for the device mirror)
+      for (uint64_t i = 0; i < b.n; i++)
+        ptrs[i] = b.h_off[i] < ring_bytes ? t->ring + b.h_off[i] : b.h_side + (b.h_off[i] - ring_bytes - s * side_cap);
+      opt.packets_cb(user, b.first, b.n, ptrs.data(), b.h_cap);
+    }
     if (with_fields) opt.fields_cb(user, b.first, b.n, b.h_fields);
     if (cb) cb(user, b.first, b.n, b.h_rec, b.h_err, b.h_flow, b.h_ci, b.h_cap);
+    if (hold && b.h2d_pending) {  // delivered: the headers go back to the kernel
+      b.h2d_pending = false;
+      gpk_tpacket_release(t, b.rel_seq);
+    }
     b.inflight = false;
     return true;
   };
@@ -1144,12 +1158,13 @@ static int tpacket_pump(gpk_ctx* ctx, const gpk_parser* parser, gpk_tpacket* t, 
     gpk_tpacket_take_new_headers(t, &nf, &nc);
     if (n == 0 && nc == 0) {
       if (r == GPK_TP_ERROR) break;
-      // dry: release what has reached the device, then wait or stop
+      // dry: release what has reached the device (with packets_cb: what was
+      // delivered), then wait or stop
       if (!order.empty()) {
         bool any = false;
         for (int s : order) any = any || B[s].h2d_pending;
         if (any) {
-          if (!release_done(true)) good = false;
+          if (!(hold ? deliver_oldest() : release_done(true))) good = false;
           continue;
         }
       }

@@ -55,8 +55,8 @@ extern "C" {
 #endif
 
 /* 2: gpk_fields bytes 1-3 carry the HopByHop option map (present is a u8);
- *    gpk_replay_stats gained alloc_wait_s; gpk_replay_opts gained trailing fields
- *    and packets callbacks, gpk_tp_pump_opts a fields callback. A caller compiled against another
+ *    gpk_replay_stats gained alloc_wait_s; gpk_replay_opts and gpk_tp_pump_opts
+ *    gained trailing fields and packets callbacks. A caller compiled against another
  *    version must not call in: check gpk_abi_version() == GPK_ABI_VERSION. */
 #define GPK_ABI_VERSION 2
 

@@ -140,6 +140,14 @@ int gpk_tpacket_set_fanout(gpk_tpacket* t, int type, uint16_t id);
 /* Per batch, before its gpk_tp_pump_cb: the layer fields of its n packets
  * (gpk_fields, include/gpk.h), valid during the call. */
 typedef void (*gpk_tp_pump_fields_cb)(void* user, uint64_t first_packet, uint64_t n, const gpk_fields* fields);
+/* Per batch, first of its callbacks: the batch's packets as
+ * ZeroCopyReadPacketData returns their data, packet i = data[i][0, caplens[i])
+ * (a frame in the ring, or the copy with the inserted VLAN header), valid
+ * during the call. With it set, ring headers are handed back to the kernel
+ * after their batch was delivered, not as soon as their bytes reached the
+ * device. */
+typedef void (*gpk_tp_pump_packets_cb)(void* user, uint64_t first_packet, uint64_t n, const uint8_t* const* data,
+                                       const uint32_t* caplens);
 
 typedef struct gpk_tp_pump_opts {
   uint64_t batch_pkts;  /* packets per device launch (default 1 Mi)              */
@@ -148,6 +156,7 @@ typedef struct gpk_tp_pump_opts {
   int inflight;         /* batches in flight (default 4)                          */
   gpk_tp_pump_fields_cb fields_cb; /* non-null: every launch is the fused decode +
                                       layer fields, delivered through it     */
+  gpk_tp_pump_packets_cb packets_cb; /* non-null: the packets' bytes too        */
 } gpk_tp_pump_opts;
 
 typedef struct gpk_tp_pump_stats {

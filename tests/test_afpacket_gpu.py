@@ -170,3 +170,39 @@ def test_pump_callback_exception_reaches_the_caller(gpu_ctx):
     with pytest.raises(KeyError):
         tp.Pump(gpu_ctx, device_parser(CONFIGS["statsassembly"]), batch_pkts=100, collect=False, on_batch=boom)
     tp.Close()
+
+
+@pytest.mark.parametrize("vlan", [False, True])
+def test_pump_packets(gpu_ctx, vlan):
+    """packets=True: each batch's packets as ZeroCopyReadPacketData returns
+    them (ring frames, or the copies with the inserted VLAN header), equal to
+    the ring oracle's; the ring laps with an emulated kernel re-arming blocks
+    only after their batch was delivered."""
+    import ctypes
+    S = _lib.synth_lib()
+    bs, nb = 65536, 8
+    ring = np.zeros(bs * nb, np.uint8)
+    n = int(S.gpk_synth_tpacket_v3(ring.ctypes.data, bs, nb, synth.C4_IMIX, 17, 7, 3, None))
+    opts = dict(frame_size=4096, block_size=bs, num_blocks=nb, add_vlan_header=vlan)
+    pk, exp = expect(ring.tobytes(), AO.V3, opts)
+    args = [afpacket.OptFrameSize(4096), afpacket.OptBlockSize(bs), afpacket.OptNumBlocks(nb),
+            afpacket.OptPollTimeout(5_000_000_000)]
+    if vlan:
+        args.append(afpacket.OptAddVLANHeader(True))
+    tp = afpacket.AttachRing(ring, afpacket.TPacketVersion3, *args)
+    prod = S.gpk_synth_tp_producer_start(ring.ctypes.data, bs, nb)
+    got = []
+    try:
+        laps = 3
+
+        def on_batch(first, k, rec, err, fl, ci, cap, packets):
+            ptrs, caps = packets
+            assert np.array_equal(caps, cap)
+            got.extend(ctypes.string_at(int(p), int(c)) for p, c in zip(ptrs, caps))
+
+        _, st = tp.Pump(gpu_ctx, device_parser(CONFIGS["statsassembly"]), batch_pkts=97, inflight=3,
+                        max_packets=n * laps, wait=True, collect=False, on_batch=on_batch, packets=True)
+    finally:
+        S.gpk_synth_tp_producer_stop(prod)
+    tp.Close()
+    assert st["packets"] == n * laps and got == pk * laps
