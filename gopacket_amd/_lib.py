@@ -380,6 +380,9 @@ def synth_lib():
         S.gpk_probe_d2d.restype = ctypes.c_int
         S.gpk_probe_hostwrite.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_void_p]
         S.gpk_probe_hostwrite.restype = ctypes.c_int
+        S.gpk_probe_h2d_rate.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int, ctypes.c_int,
+                                         ctypes.c_int]
+        S.gpk_probe_h2d_rate.restype = ctypes.c_double
         S.gpk_synth_tpacket_v3.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int,
                                            ctypes.c_uint64, ctypes.c_int32, ctypes.c_uint32, ctypes.c_void_p]
         S.gpk_synth_tpacket_v3.restype = ctypes.c_uint64

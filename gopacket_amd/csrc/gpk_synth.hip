@@ -3,6 +3,7 @@
 // never linked into libgpk.so. Packets are generated in HBM directly (C3 is
 // ~100 GB at 64 M packets, far more than is worth copying over PCIe).
 #include <hip/hip_runtime.h>
+#include <chrono>
 #include <fcntl.h>
 #include <unistd.h>
 
@@ -852,6 +853,45 @@ int gpk_probe_mixed(const uint8_t* data, uint64_t nbytes, uint8_t* wbuf, uint64_
 int gpk_probe_hostwrite(uint8_t* dst, uint64_t nbytes, int blocks, void* stream) {
   hipLaunchKernelGGL(probe_hostwrite_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, dst, nbytes / 16);
   return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+// Host-to-device copy rate of `bytes` from host memory `src` (registered here
+// with hipHostRegister unless it is already pinned: register = 0) in copies of
+// `chunk` bytes over `streams` streams, `reps` rounds; returns GB/s or < 0
+// (tools/duplex_probe.py: ring memory as the AF_PACKET pump copies it).
+double gpk_probe_h2d_rate(const void* src, uint64_t bytes, uint64_t chunk, int streams, int reps, int register_) {
+  if (!src || !bytes || !chunk || streams < 1 || streams > 16 || reps < 1) return -1;
+  if (register_ && hipHostRegister(const_cast<void*>(src), bytes, hipHostRegisterDefault) != hipSuccess) return -2;
+  void* dst = nullptr;
+  double gbs = -3;
+  hipStream_t st[16] = {};
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  bool ok = hipMalloc(&dst, bytes) == hipSuccess && hipEventCreate(&e0) == hipSuccess &&
+            hipEventCreate(&e1) == hipSuccess;
+  for (int k = 0; ok && k < streams; k++) ok = hipStreamCreateWithFlags(&st[k], hipStreamNonBlocking) == hipSuccess;
+  if (ok) {
+    auto round = [&]() {
+      uint64_t i = 0;
+      for (uint64_t o = 0; o < bytes; o += chunk, i++)
+        (void)hipMemcpyAsync((char*)dst + o, (const char*)src + o, o + chunk <= bytes ? chunk : bytes - o,
+                             hipMemcpyHostToDevice, st[i % streams]);
+      for (int k = 0; k < streams; k++) (void)hipStreamSynchronize(st[k]);
+    };
+    round();
+    (void)hipDeviceSynchronize();
+    (void)hipEventRecord(e0, nullptr);
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int r = 0; r < reps; r++) round();
+    const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    gbs = (double)bytes * reps / s / 1e9;
+  }
+  for (int k = 0; k < streams; k++)
+    if (st[k]) (void)hipStreamDestroy(st[k]);
+  if (e0) (void)hipEventDestroy(e0);
+  if (e1) (void)hipEventDestroy(e1);
+  if (dst) (void)hipFree(dst);
+  if (register_) (void)hipHostUnregister(const_cast<void*>(src));
+  return gbs;
 }
 
 // Device memory of a given kind for placement experiments (tools/alloc_probe.py):

@@ -58,5 +58,31 @@ def main(mib=256, reps=8):
               % (blocks, run_w(False, blocks), run_w(True, blocks)), flush=True)
 
 
+def ring_memory(mib=256):
+    """HtoD rate from host memory of the kinds the pump copies from: a pinned
+    allocation, and ordinary (numpy) memory registered with hipHostRegister as
+    the pump registers a ring, in 4 MiB (a V3 block) and 64 MiB copies."""
+    import ctypes
+    import os
+    import sys
+    import numpy as np
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from gopacket_amd import _lib
+    S = _lib.synth_lib()
+    n = mib << 20
+    pinned = torch.empty(n, dtype=torch.uint8, pin_memory=True)
+    plain = np.ones(n, np.uint8)
+    for chunk in (4 << 20, 64 << 20):
+        for streams in (1, 4):
+            a = S.gpk_probe_h2d_rate(ctypes.c_void_p(pinned.data_ptr()), n, chunk, streams, 4, 0)
+            b = S.gpk_probe_h2d_rate(ctypes.c_void_p(plain.ctypes.data), n, chunk, streams, 4, 1)
+            print("HtoD %3d MiB copies on %d stream(s): pinned %5.1f GB/s, registered numpy memory %5.1f GB/s"
+                  % (chunk >> 20, streams, a, b), flush=True)
+
+
 if __name__ == "__main__":
+    import sys as _sys
+    if len(_sys.argv) > 1 and _sys.argv[1] == "ring":
+        ring_memory()
+        raise SystemExit(0)
     main()
