@@ -167,9 +167,9 @@ class NgInterface(ctypes.Structure):
 
 # gpk_replay_fields_cb(user, first_packet, n, const gpk_fields*)
 REPLAY_FIELDS_CB = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p)
-# gpk_replay_packets_cb(user, first_packet, n, base, offsets, caplens)
+# gpk_replay_packets_cb(user, first_packet, n, base, bytes, offsets, caplens)
 REPLAY_PACKETS_CB = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p,
-                                     ctypes.c_void_p, ctypes.c_void_p)
+                                     ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p)
 
 
 class ReplayOpts(ctypes.Structure):

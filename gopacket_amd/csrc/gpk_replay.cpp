@@ -203,6 +203,7 @@ struct Bat {
   uint64_t first = 0, n = 0, flows_n = 0;
   bool with_fields = false;  // this launch wrote fields
   const uint8_t* base = nullptr;  // opts.packets_cb: the staging bytes h_off is relative to
+  uint64_t base_bytes = 0;        // ... how many of them hold the slot's records
   int slot = -1;                  // ... and their slot, held until this batch is delivered
 };
 
@@ -241,7 +242,7 @@ struct Pipeline {
     if (hipEventElapsedTime(&kms, B.k0, B.k1) == hipSuccess) st->kernel_s += kms * 1e-3;
     double t = now_s();
     for (uint64_t i = 0; i < B.n; i++) st->packet_bytes += B.h_cap[i];
-    if (packets_cb && B.base) packets_cb(user, B.first, B.n, B.base, B.h_off, B.h_cap);
+    if (packets_cb && B.base) packets_cb(user, B.first, B.n, B.base, B.base_bytes, B.h_off, B.h_cap);
     if (B.slot >= 0 && (size_t)B.slot < slot_batches.size()) slot_batches[B.slot]--;
     B.slot = -1;
     B.base = nullptr;
@@ -877,6 +878,7 @@ static int replay_file(gpk_ctx* ctx, const gpk_parser* parser, const char* path,
       if (pl.packets_cb) {  // the packets stay in this slot's staging bytes until delivered
         B.slot = (int)(si % pl.slots.size());
         B.base = dwalk ? S.host + base_off : S.host + start;
+        B.base_bytes = dwalk ? start + len - base_off : len;  // the slot's bytes from base on
         pl.slot_batches[B.slot]++;
       }
       good = good && pl.ok(hipEventRecord(B.e0, S.stream), "hipEventRecord");

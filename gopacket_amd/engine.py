@@ -194,13 +194,12 @@ class Context:
         parts = []
         got_packets = []
 
-        def pcb(user, first, n, base, off, cap):
+        def pcb(user, first, n, base, nbytes, off, cap):
             if not n:
                 return
             o = np.ctypeslib.as_array(ctypes.cast(off, ctypes.POINTER(ctypes.c_uint64)), (n,))
             c = np.ctypeslib.as_array(ctypes.cast(cap, ctypes.POINTER(ctypes.c_uint32)), (n,))
-            end = int((o + c.astype(np.uint64)).max())
-            data = np.ctypeslib.as_array(ctypes.cast(base, ctypes.POINTER(ctypes.c_uint8)), (max(end, 1),))
+            data = np.ctypeslib.as_array(ctypes.cast(base, ctypes.POINTER(ctypes.c_uint8)), (max(nbytes, 1),))
             got_packets[:] = [(first, n, (data, o, c))]
         got_fields = []  # the current launch's fields (fields_cb runs right before cb)
 

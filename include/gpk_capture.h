@@ -149,12 +149,12 @@ int gpk_capreader_interface_str(const gpk_capreader* r, int section, int index, 
  * before gpk_replay_cb for the same packets. */
 typedef void (*gpk_replay_fields_cb)(void* user, uint64_t first_packet, uint64_t n, const gpk_fields* fields);
 /* The packets of one device launch, as ReadPacketData returned their data:
- * packet i is base[offsets[i], offsets[i] + caplens[i]), in the pinned staging
- * buffer the file was read into (no copy), valid during the call only; called
- * on the calling thread before the fields and results callbacks for the same
- * packets. */
+ * packet i is base[offsets[i], offsets[i] + caplens[i]), inside base[0, bytes),
+ * in the pinned staging buffer the file was read into (no copy), valid during
+ * the call only; called on the calling thread before the fields and results
+ * callbacks for the same packets. */
 typedef void (*gpk_replay_packets_cb)(void* user, uint64_t first_packet, uint64_t n, const uint8_t* base,
-                                      const uint64_t* offsets, const uint32_t* caplens);
+                                      uint64_t bytes, const uint64_t* offsets, const uint32_t* caplens);
 
 typedef struct gpk_replay_opts {
   int format;            /* GPK_CAP_PCAP / GPK_CAP_PCAPNG, 0 = from the magic */

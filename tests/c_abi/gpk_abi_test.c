@@ -281,11 +281,12 @@ static void on_fields(void* user, uint64_t first, uint64_t n, const gpk_fields* 
   st->have_fields = 1;
 }
 
-static void on_packets(void* user, uint64_t first, uint64_t n, const uint8_t* base, const uint64_t* offsets,
-                       const uint32_t* caplens) {
+static void on_packets(void* user, uint64_t first, uint64_t n, const uint8_t* base, uint64_t bytes,
+                       const uint64_t* offsets, const uint32_t* caplens) {
   struct replay_state* st = (struct replay_state*)user;
   for (uint64_t i = 0; i < n; i++) {
     const uint64_t k = first + i;
+    CHECK(offsets[i] + caplens[i] <= bytes, "packet %llu outside the batch's bytes", (unsigned long long)k);
     if (k >= st->x->n) {
       CHECK(0, "packet %llu past the reader's %llu", (unsigned long long)k, (unsigned long long)st->x->n);
       return;

@@ -1,0 +1,102 @@
+#!/usr/bin/env python3
+"""Soak: the library's long-lived paths run many times in one process, with
+host RSS and free device memory checked for growth. 30 replays of a ~2 GiB
+C4 pcapng (cycling plain / fields / packets / fields+packets, contexts kept
+and re-created), 2000 decode launches over 8 caller streams, 20 contexts
+created and destroyed, 30 AF_PACKET pumps over a lapping ring."""
+import gc
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def rss_mib():
+    for line in open("/proc/self/status"):
+        if line.startswith("VmRSS:"):
+            return int(line.split()[1]) / 1024
+    return -1
+
+
+def main():
+    import torch
+    import bench
+    from gopacket_amd import _lib, afpacket, engine, synth
+    S = _lib.synth_lib()
+    cfg = bench.CONFIGS["c4"]
+    kinds = [engine.DECODER_KINDS[d] for d in cfg["decoders"]]
+    path = os.path.join(os.environ.get("TMPDIR", "/tmp"), "gpk_soak_%d.pcapng" % os.getpid())
+    n = 5_000_000
+    assert S.gpk_synth_write_pcapng(path.encode(), 4, 0, n, 16) > 0
+    t0 = time.time()
+    marks = []
+
+    def mark(what):
+        gc.collect()
+        torch.cuda.synchronize()
+        free, total = torch.cuda.mem_get_info()
+        marks.append((what, rss_mib(), free / 2**20))
+        print("%-34s rss %8.1f MiB  device free %10.1f MiB  %5.1f s" % (what, marks[-1][1], marks[-1][2],
+                                                                          time.time() - t0), flush=True)
+
+    try:
+        ctx = engine.Context(0)
+        parser = engine.ParserConfig(17, kinds, outputs=cfg["outputs"])
+        mark("start")
+        reps = int(os.environ.get("SOAK_REPLAYS", "30"))
+        for k in range(reps):
+            if k % 10 == 9 and os.environ.get("SOAK_RECREATE", "1") == "1":  # a fresh context now and then
+                del ctx
+                gc.collect()
+                ctx = engine.Context(0)
+            fields, packets = bool(k & 1), bool(k & 2)
+            cnt = [0]
+
+            def on_batch(first, m, *v):
+                cnt[0] += m
+
+            _, st = ctx.replay_file(parser, path, collect=False, on_batch=on_batch, fields=fields, packets=packets)
+            assert st["packets"] == n == cnt[0] and st["error"] == "EOF", st
+            if k == 0 or k % 10 == 9:
+                mark("replay %d" % k)
+        d, o, c = synth.device_batch(4, 0, 1 << 16)
+        streams = [torch.cuda.Stream() for _ in range(8)]
+        outs = [(torch.empty(16 << 16, dtype=torch.uint8, device="cuda"), torch.zeros(2 << 16, dtype=torch.int32,
+                 device="cuda"), torch.empty(3 << 16, dtype=torch.int64, device="cuda")) for _ in streams]
+        for k in range(2000):
+            s = streams[k % 8]
+            rec, err, fl = outs[k % 8]
+            ctx.decode_device(parser, d, o, c, rec, err, fl, stream=s)
+        mark("2000 launches on 8 streams")
+        for k in range(20):
+            x = engine.Context(0)
+            p = engine.ParserConfig(17, kinds, outputs=cfg["outputs"])
+            x.decode_device(p, d, o, c, *outs[0])
+            torch.cuda.synchronize()
+            del x, p
+        mark("20 contexts")
+        bs, nb = 1 << 20, 16
+        ring = np.zeros(bs * nb, np.uint8)
+        S.gpk_synth_tpacket_v3(ring.ctypes.data, bs, nb, 4, 0, 2, 0, None)
+        for k in range(30):
+            ring[8::bs] = 1
+            tp = afpacket.AttachRing(ring, afpacket.TPacketVersion3, afpacket.OptFrameSize(4096),
+                                     afpacket.OptBlockSize(bs), afpacket.OptNumBlocks(nb))
+            _, st = tp.Pump(ctx, parser, batch_pkts=1 << 14, collect=False, on_batch=lambda *a: None,
+                            fields=bool(k & 1), packets=bool(k & 2))
+            tp.Close()
+            assert st["packets"] > 0
+        mark("30 pumps")
+        rss0, free0 = marks[1][1], marks[1][2]
+        print("soak done: rss %+.1f MiB, device free %+.1f MiB since the first replay" % (
+            marks[-1][1] - rss0, marks[-1][2] - free0), flush=True)
+    finally:
+        os.unlink(path)
+
+
+if __name__ == "__main__":
+    main()
