@@ -130,6 +130,9 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 #ifndef GPK_DIAG_FIELDS
 #define GPK_DIAG_FIELDS 0  // timing only: 1 = fused fields computed, not stored; 2 = stored, not read
 #endif
+#ifndef GPK_DIAG_NULLWIN
+#define GPK_DIAG_NULLWIN 0  // timing only: the stream-before-parse windows read the L2-resident table copy
+#endif
 #ifndef GPK_PB_NULL
 #define GPK_PB_NULL 0  // timing only: phase-B stream loads read nothing (zero-record descriptors)
 #endif
@@ -1397,7 +1400,11 @@ __device__ __forceinline__ void dma16(uint64_t src, uint32_t lds) {
 // packet with none reads the parser's table copy (as load_window).
 template <int W>
 __device__ __forceinline__ void window_dma(const KParams& P, const WinGeo& g, uint32_t region, uint32_t lane) {
+#if GPK_DIAG_NULLWIN  // timing only: every window from the L2-resident table copy
+  const uint64_t src = (uint64_t)(uintptr_t)P.tab;
+#else
   const uint64_t src = g.nch ? (uint64_t)(uintptr_t)(P.data + g.wb) : (uint64_t)(uintptr_t)P.tab;
+#endif
   const uint32_t last = g.nch ? g.nch - 1 : 0u;
 #pragma unroll
   for (int k = 0; k < W; k++) {
