@@ -169,8 +169,10 @@ def typed_names(code, elem_types):
     return names
 
 
-@pytest.mark.parametrize("name,pre,flags,code", files(), ids=lambda v: v if isinstance(v, str) and
-                         v.startswith("go block") else "")
+FILES = files()
+
+
+@pytest.mark.parametrize("name,pre,flags,code", FILES, ids=[f[0].replace(" ", "_") for f in FILES])
 def test_cgo_block_matches_headers(name, pre, flags, code):
     ok, err = compiles(pre, flags, "")
     assert ok, "%s: its cgo preamble does not compile:\n%s" % (name, err)
