@@ -136,6 +136,51 @@ def test_replay_device_walk(gpu_ctx, tmp_path, bo):
         del os.environ["GPK_REPLAY_HOST_WALK"]
 
 
+def block_starts(raw, bo="<"):
+    """Offsets of the pcapng blocks of an intact file (type, total length)."""
+    import struct
+    out, p = [], 0
+    while p + 8 <= len(raw):
+        L = struct.unpack_from(bo + "I", raw, p + 4)[0]
+        out.append((p, L))
+        p += L
+    return out
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_replay_device_walk_corrupt(gpu_ctx, tmp_path, seed):
+    """Byte flips in the blocks of a file the device walks: block type, the low
+    byte of a block length, interface id, capture length, original length,
+    trailer, packet bytes. The device walk must stop at every block that is not
+    a plain EPB and leave it to the host reader, which desynchronises or fails
+    exactly as Go's reader does (ngread.go:494-585); packets, capture info and
+    the reader's error then match the reader oracle. One record longer than
+    the staging carry region ends the call with GPK_EUNSUPP by design: the
+    flips keep block lengths small, but Go reads options past a short block
+    (ngread.go:199-236), so a shrunk capture length can make the following
+    megabytes one record's options. Small slots may refuse such a file; the
+    default slots must match the oracle."""
+    from gopacket_amd import _lib
+    raw = bytearray(walk_capture())
+    blocks = block_starts(bytes(raw))[4:]  # after the section header and the three interfaces
+    rng = np.random.default_rng(1000 + seed)
+    for _ in range(int(rng.integers(1, 5))):
+        p, L = blocks[int(rng.integers(0, len(blocks)))]
+        field = int(rng.integers(0, 7))
+        pos = [p, p + 4, p + 8, p + 20, p + 24, p + L - 4, p + 28 + int(rng.integers(0, max(1, L - 32)))][field]
+        raw[pos] ^= int(rng.integers(1, 256)) if field != 1 else int(rng.integers(1, 256)) & 0xFC | 4
+    path = tmp_path / "corrupt.pcapng"
+    path.write_bytes(bytes(raw))
+    for slot in (1 << 16, 1 << 20, 0):
+        try:
+            st = check(gpu_ctx, str(path), bytes(raw), slot_bytes=slot, slots=3 if slot else 0,
+                       batch_pkts=5000 if slot else 0)
+        except _lib.GpkError as e:
+            assert slot and "carry region" in str(e), (slot, str(e))
+            continue
+        assert st["packets"] > 0
+
+
 def test_replay_small_records_grow_device_index(gpu_ctx, tmp_path):
     """Simple Packet Blocks of 16 bytes (zero-length packets, ngread.go:515-530)
     are walked by the host reader and appended to the slot's device index,
