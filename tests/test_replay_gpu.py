@@ -147,7 +147,7 @@ def block_starts(raw, bo="<"):
     return out
 
 
-@pytest.mark.parametrize("seed", range(8))
+@pytest.mark.parametrize("seed", range(12))
 def test_replay_device_walk_corrupt(gpu_ctx, tmp_path, seed):
     """Byte flips in the blocks of a file the device walks: block type, the low
     byte of a block length, interface id, capture length, original length,
@@ -161,13 +161,16 @@ def test_replay_device_walk_corrupt(gpu_ctx, tmp_path, seed):
     megabytes one record's options. Small slots may refuse such a file; the
     default slots must match the oracle."""
     from gopacket_amd import _lib
-    raw = bytearray(walk_capture())
-    blocks = block_starts(bytes(raw))[4:]  # after the section header and the three interfaces
+    bo = ">" if seed >= 8 else "<"  # seeds 8-11: a big-endian section
+    raw = bytearray(walk_capture(bo))
+    blocks = block_starts(bytes(raw), bo)[4:]  # after the section header and the three interfaces
     rng = np.random.default_rng(1000 + seed)
     for _ in range(int(rng.integers(1, 5))):
         p, L = blocks[int(rng.integers(0, len(blocks)))]
         field = int(rng.integers(0, 7))
-        pos = [p, p + 4, p + 8, p + 20, p + 24, p + L - 4, p + 28 + int(rng.integers(0, max(1, L - 32)))][field]
+        lo = 0 if bo == "<" else 3  # the low byte of a 32-bit field
+        pos = [p + lo, p + 4 + lo, p + 8 + lo, p + 20 + lo, p + 24 + lo, p + L - 4 + lo,
+               p + 28 + int(rng.integers(0, max(1, L - 32)))][field]
         raw[pos] ^= int(rng.integers(1, 256)) if field != 1 else int(rng.integers(1, 256)) & 0xFC | 4
     path = tmp_path / "corrupt.pcapng"
     path.write_bytes(bytes(raw))
