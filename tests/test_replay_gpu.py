@@ -184,6 +184,32 @@ def test_replay_device_walk_corrupt(gpu_ctx, tmp_path, seed):
         assert st["packets"] > 0
 
 
+@pytest.mark.parametrize("seed", range(8))
+def test_replay_pcap_corrupt(gpu_ctx, tmp_path, seed):
+    """Classic pcap with byte flips in record headers (timestamps, capture
+    length, original length), both byte orders, micro- and nanosecond files:
+    Reader.ReadPacketData's checks (read.go:124-178: capture length over the
+    snap length or over the original length) end the stream where Go's do,
+    and every packet before matches the reader and decode oracles."""
+    import struct
+    from gopacket_amd import synth
+    pk = [synth.packet(4, i) for i in range(6000)]
+    bo = ">" if seed % 2 else "<"
+    raw = bytearray(pcapgen.pcap_file(pk, bo=bo, nano=seed % 4 >= 2, snaplen=2000))
+    starts, p = [], 24
+    while p + 16 <= len(raw):
+        starts.append(p)
+        p += 16 + struct.unpack_from(bo + "I", raw, p + 8)[0]
+    rng = np.random.default_rng(2000 + seed)
+    for _ in range(int(rng.integers(1, 4))):
+        p = starts[int(rng.integers(0, len(starts)))]
+        raw[p + 4 * int(rng.integers(0, 4)) + (0 if bo == "<" else 3)] ^= int(rng.integers(1, 256))
+    path = tmp_path / "corrupt.pcap"
+    path.write_bytes(bytes(raw))
+    for slot, slots, batch in ((8192, 2, 300), (0, 0, 0)):
+        check(gpu_ctx, str(path), bytes(raw), fmt="pcap", slot_bytes=slot, slots=slots, batch_pkts=batch)
+
+
 def test_replay_small_records_grow_device_index(gpu_ctx, tmp_path):
     """Simple Packet Blocks of 16 bytes (zero-length packets, ngread.go:515-530)
     are walked by the host reader and appended to the slot's device index,
