@@ -79,6 +79,7 @@ EXPORTS = (
     "gpk_capreader_create", "gpk_capreader_destroy", "gpk_capreader_index", "gpk_capreader_error",
     "gpk_capreader_link_type", "gpk_capreader_pcap_header", "gpk_capreader_nsections", "gpk_capreader_section_info",
     "gpk_capreader_ninterfaces", "gpk_capreader_interface", "gpk_capreader_interface_str", "gpk_replay_file",
+    "gpk_replay_file_range",
     "gpk_capreader_index_all", "gpk_capindex_free",
     # include/gpk_afpacket.h
     "gpk_tp_default_opts", "gpk_tp_check_opts", "gpk_tpacket_new", "gpk_tpacket_attach", "gpk_tpacket_close",
@@ -187,6 +188,12 @@ class ReplayStats(ctypes.Structure):
                 ("device_walk_packets", ctypes.c_uint64), ("alloc_wait_s", ctypes.c_double)]
 
 
+class ReplayRange(ctypes.Structure):
+    _fields_ = [("begin", ctypes.c_uint64), ("end", ctypes.c_uint64), ("header_end", ctypes.c_uint64),
+                ("sync_begin", ctypes.c_uint64), ("sync_end", ctypes.c_uint64), ("clean", ctypes.c_int),
+                ("state_changed", ctypes.c_int)]
+
+
 REPLAY_CB = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p,
                              ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p)
 
@@ -275,6 +282,8 @@ def lib():
         "gpk_capreader_interface": ([vp, c_int, c_int, P(NgInterface)], c_int),
         "gpk_capreader_interface_str": ([vp, c_int, c_int, c_int, ctypes.c_char_p, ctypes.c_size_t], c_int),
         "gpk_replay_file": ([vp, vp, ctypes.c_char_p, P(ReplayOpts), REPLAY_CB, vp, P(ReplayStats)], c_int),
+        "gpk_replay_file_range": ([vp, vp, ctypes.c_char_p, P(ReplayRange), P(ReplayOpts), REPLAY_CB, vp,
+                                   P(ReplayStats)], c_int),
         "gpk_capreader_index_all": ([vp, vp, u64, c_int, c_int, P(CapIndex), P(u64)], c_int),
         "gpk_capindex_free": ([P(CapIndex)], c_int),
         "gpk_tp_default_opts": ([P(TpOpts)], None),

@@ -44,6 +44,7 @@
 #include <vector>
 
 #include "gpk_pinned.h"
+#include "gpk_devguard.h"
 #include "../../include/gpk_afpacket.h"
 
 extern "C" int gpk_decode_batch_ex(gpk_ctx* c, const gpk_parser* p, const gpk_batch* b, const gpk_results* o,
@@ -1305,6 +1306,13 @@ extern "C" int gpk_tpacket_pump(gpk_ctx* ctx, const gpk_parser* parser, gpk_tpac
   if (!ctx || !parser || !t || !st) return GPK_EINVAL;
   memset(st, 0, sizeof(*st));
   try {
+    // the context's device for the pipeline's buffers, streams and launches
+    // (callbacks included); the caller's device is back on return
+    gpk::DeviceScope dscope(gpk_ctx_device(ctx));
+    if (dscope.err != hipSuccess) {
+      snprintf(st->error, sizeof(st->error), "hipSetDevice: %s", hipGetErrorString(dscope.err));
+      return GPK_EHIP;
+    }
     return tpacket_pump(ctx, parser, t, o, cb, user, st);
   } catch (const std::bad_alloc&) {
     snprintf(st->error, sizeof(st->error), "out of host memory");

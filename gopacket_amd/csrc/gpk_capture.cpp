@@ -25,6 +25,7 @@
 // readNameResolutionBlock ngread_nrb.go:63-130, readDecryptionSecretsBlock
 // ngread_dsb.go:17-39; NewReader/readHeader read.go:64-122, ReadPacketData
 // :124-140, readPacketHeader :171-180.
+#include <algorithm>
 #include <condition_variable>
 #include <cstdarg>
 #include <cstdio>
@@ -1146,6 +1147,25 @@ bool gpk_capreader_walk_state(const gpk_capreader* r, gpk::WalkState* out) {
     w.plain = it.second_mask != 0 && (out->mixed || it.link_type == st.link_type);
   }
   return true;
+}
+
+// The byte-range replay (gpk_replay_file_range): where a range's first block
+// lies, by the same rule as the speculative walk (four chained plain EPBs
+// under the reader's current state), and the reader-state version that tells
+// whether a range changed what the next one assumed.
+uint64_t gpk_capreader_sync(const gpk_capreader* r, const uint8_t* b, uint64_t from, uint64_t to, uint64_t end,
+                            uint64_t span) {
+  if (!r || r->format != GPK_CAP_PCAPNG || !r->opened || r->open_failed) return ~0ull;
+  for (uint64_t p = (from + 3) & ~3ull; p < to; p += 4) {  // the chain inside [p, p + span): a property of p alone
+    const uint64_t e = std::min<uint64_t>(end, p + span);
+    if (find_sync(r->st, r->flags, b, p, p + 1, e, p) == p) return p;
+  }
+  return ~0ull;
+}
+
+uint64_t gpk_capreader_state_version(const gpk_capreader* r) {
+  if (!r || r->format != GPK_CAP_PCAPNG || !r->opened || r->open_failed) return 0;
+  return state_version(r) | 1ull << 63;  // nonzero once open
 }
 
 extern "C" int gpk_capreader_index_all(gpk_capreader* r, const uint8_t* buf, uint64_t len, int eof, int threads,

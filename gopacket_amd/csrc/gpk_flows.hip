@@ -26,6 +26,7 @@
 #include <new>
 
 #include "../../include/gpk_flows.h"
+#include "gpk_devguard.h"
 
 // gpk_host.cpp: gpk_decode_batch with the fused key derivation (library-internal)
 extern "C" int gpk_decode_batch_keys(gpk_ctx* c, const gpk_parser* p, const gpk_batch* b, const gpk_results* o, int key_kind,
@@ -358,7 +359,8 @@ extern "C" int gpk_grouper_create(gpk_grouper** out, int device, uint64_t max_pa
   if (!out || max_packets == 0 || max_packets >= (1ull << kIdxBits)) return GPK_EINVAL;
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return GPK_ENODEV;
-  if (hipSetDevice(device) != hipSuccess) return GPK_EHIP;
+  gpk::DeviceScope dscope(device);  // the caller's device is restored on return
+  if (dscope.err != hipSuccess) return GPK_EHIP;
   gpk_grouper* g = new (std::nothrow) gpk_grouper();
   if (!g) return GPK_ENOMEM;
   g->device = device;
@@ -392,6 +394,7 @@ extern "C" int gpk_grouper_create(gpk_grouper** out, int device, uint64_t max_pa
 
 extern "C" int gpk_grouper_destroy(gpk_grouper* g) {
   if (!g) return GPK_EINVAL;
+  gpk::DeviceScope dscope(g->device);
   (void)hipDeviceSynchronize();
   free_all(g);
   delete g;
@@ -409,7 +412,8 @@ extern "C" int gpk_group_batch(gpk_grouper* g, const gpk_batch* b, const gpk_res
   const uint64_t n = b->n;
   if (n > g->cap) return GPK_EINVAL;
   hipStream_t s = (hipStream_t)stream;
-  if (hipSetDevice(g->device) != hipSuccess) return GPK_EHIP;
+  gpk::DeviceScope dscope(g->device);
+  if (dscope.err != hipSuccess) return GPK_EHIP;
   if (hipMemsetAsync(o->counts, 0, 8, s) != hipSuccess || hipMemsetAsync(o->start, 0, 4, s) != hipSuccess)
     return GPK_EHIP;
   if (n == 0) return GPK_OK;
@@ -436,7 +440,8 @@ extern "C" int gpk_decode_group_batch(gpk_ctx* ctx, const gpk_parser* p, const g
   hipStream_t s = (hipStream_t)stream;
   int rc = gpk_decode_batch_keys(ctx, p, b, r, kind, g->keys, g->hash, g->code, stream);
   if (rc) return rc;
-  if (hipSetDevice(g->device) != hipSuccess) return GPK_EHIP;
+  gpk::DeviceScope dscope(g->device);
+  if (dscope.err != hipSuccess) return GPK_EHIP;
   if (hipMemsetAsync(o->counts, 0, 8, s) != hipSuccess || hipMemsetAsync(o->start, 0, 4, s) != hipSuccess)
     return GPK_EHIP;
   if (n == 0) return GPK_OK;

@@ -28,6 +28,7 @@
 #include "gpk_device.h"
 #include "gpk_registry_gen.h"
 #include "gpk_pinned.h"
+#include "gpk_devguard.h"
 
 extern "C" hipError_t gpk_launch_decode(const gpk::KParams* P, int with_l4, int with_layout, hipStream_t stream);
 extern "C" int gpk_launch_describe(const gpk::KParams* P, int with_l4, int with_layout, char* buf, size_t cap);
@@ -162,6 +163,8 @@ static void default_tables(gpk::DevTables& t) {
 extern "C" {
 
 int gpk_abi_version(void) { return GPK_ABI_VERSION; }
+
+int gpk_ctx_device(const gpk_ctx* c) { return c ? c->device : -1; }
 
 const char* gpk_strerror(int status) {
   switch (status) {
@@ -305,7 +308,8 @@ int gpk_ctx_create(gpk_ctx** out, int device) {
   if (!out) return GPK_EINVAL;
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return GPK_ENODEV;
-  HIPCHK(hipSetDevice(device));
+  gpk::DeviceScope dscope(device);  // the context's stream and buffers on its device; the caller's back after
+  HIPCHK(dscope.err);
   gpk_walk_preload();  // the replay's record-walk module (gpk_walk.hip), loaded with the context
   warm_unwinder();
   gpk_ctx* c = new (std::nothrow) gpk_ctx;
@@ -338,7 +342,7 @@ int gpk_ctx_create(gpk_ctx** out, int device) {
 
 int gpk_ctx_destroy(gpk_ctx* c) {
   if (!c) return GPK_OK;
-  (void)hipSetDevice(c->device);
+  gpk::DeviceScope dscope(c->device);
   (void)hipDeviceSynchronize();  // launches still reading the table copies
   if (c->stream) (void)hipStreamDestroy(c->stream);
   free_slots(c);
@@ -654,7 +658,8 @@ int gpk_decode_batch(gpk_ctx* c, const gpk_parser* p, const gpk_batch* b, const 
   if (rc) return rc;
   hipStream_t s = (hipStream_t)stream;
   std::lock_guard<std::mutex> g(c->mu);
-  HIPCHK(hipSetDevice(c->device));
+  gpk::DeviceScope dscope(c->device);
+  HIPCHK(dscope.err);
   int slot = 0;
   rc = upload(c, p, P, &slot, s);
   if (rc) return rc;
@@ -675,7 +680,8 @@ int gpk_decode_batch_fields(gpk_ctx* c, const gpk_parser* p, const gpk_batch* b,
   P.fields = fields;
   hipStream_t s = (hipStream_t)stream;
   std::lock_guard<std::mutex> g(c->mu);
-  HIPCHK(hipSetDevice(c->device));
+  gpk::DeviceScope dscope(c->device);
+  HIPCHK(dscope.err);
   int slot = 0;
   rc = upload(c, p, P, &slot, s);
   if (rc) return rc;
@@ -701,7 +707,8 @@ extern "C" __attribute__((visibility("hidden"))) int gpk_decode_batch_ex(gpk_ctx
   P.fields = fields;
   hipStream_t s = (hipStream_t)stream;
   std::lock_guard<std::mutex> g(c->mu);
-  HIPCHK(hipSetDevice(c->device));
+  gpk::DeviceScope dscope(c->device);
+  HIPCHK(dscope.err);
   int slot = 0;
   rc = upload(c, p, P, &slot, s);
   if (rc) return rc;
@@ -734,7 +741,8 @@ extern "C" __attribute__((visibility("hidden"))) int gpk_decode_batch_keys(gpk_c
   P.kcode = kcode;
   hipStream_t s = (hipStream_t)stream;
   std::lock_guard<std::mutex> g(c->mu);
-  HIPCHK(hipSetDevice(c->device));
+  gpk::DeviceScope dscope(c->device);
+  HIPCHK(dscope.err);
   int slot = 0;
   rc = upload(c, p, P, &slot, s);
   if (rc) return rc;
@@ -751,7 +759,8 @@ int gpk_decode_kernel_name(gpk_ctx* c, const gpk_parser* p, const gpk_batch* b, 
   if (rc) return rc;
   (void)o;
   std::lock_guard<std::mutex> g(c->mu);
-  HIPCHK(hipSetDevice(c->device));
+  gpk::DeviceScope dscope(c->device);
+  HIPCHK(dscope.err);
   int slot = 0;
   rc = upload(c, p, P, &slot, c->stream);
   if (rc) return rc;
@@ -765,7 +774,8 @@ int gpk_decode_occupancy(gpk_ctx* c, const gpk_parser* p, const gpk_batch* b, in
   int rc = make_params(c, p, b, nullptr, P);
   if (rc) return rc;
   std::lock_guard<std::mutex> g(c->mu);
-  HIPCHK(hipSetDevice(c->device));
+  gpk::DeviceScope dscope(c->device);
+  HIPCHK(dscope.err);
   int slot = 0;
   rc = upload(c, p, P, &slot, c->stream);
   if (rc) return rc;
@@ -805,7 +815,8 @@ static int decode_host(gpk_ctx* c, const gpk_parser* p, const gpk_batch* hb, con
          o_fld = align_up(o_lay + (ho->layouts ? n * sizeof(gpk_layout) : 0)),
          total = align_up(o_fld + (hf ? n * sizeof(gpk_fields) : 0));
   std::lock_guard<std::mutex> g(c->mu);
-  HIPCHK(hipSetDevice(c->device));
+  gpk::DeviceScope dscope(c->device);
+  HIPCHK(dscope.err);
   int rc = ensure_dbuf(c, total);
   if (rc) return rc;
   char* d = (char*)c->dbuf;
@@ -864,7 +875,8 @@ int gpk_decoded_list(gpk_ctx* c, const gpk_parser* p, const gpk_batch* b, uint64
   if (rc) return rc;
   if (index >= b->n) return GPK_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
-  HIPCHK(hipSetDevice(c->device));
+  gpk::DeviceScope dscope(c->device);
+  HIPCHK(dscope.err);
   rc = ensure_dbuf(c, align_up(8 * (size_t)cap) + 256);
   if (rc) return rc;
   int64_t* dl = (int64_t*)c->dbuf;
@@ -891,7 +903,8 @@ int gpk_decoded_list_host(gpk_ctx* c, const gpk_parser* p, const uint8_t* pkt, u
   size_t o_off = align_up((size_t)caplen + 16), o_cap = o_off + 256, o_list = o_cap + 256,
          o_n = align_up(o_list + 8 * (size_t)cap), total = o_n + 256;
   std::lock_guard<std::mutex> g(c->mu);
-  HIPCHK(hipSetDevice(c->device));
+  gpk::DeviceScope dscope(c->device);
+  HIPCHK(dscope.err);
   int rc = ensure_dbuf(c, total);
   if (rc) return rc;
   char* d = (char*)c->dbuf;

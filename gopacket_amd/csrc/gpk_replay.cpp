@@ -49,6 +49,7 @@
 
 #include "../../include/gpk_capture.h"
 #include "gpk_pinned.h"
+#include "gpk_devguard.h"
 #include "gpk_walk.h"
 
 extern "C" int gpk_decode_batch_ex(gpk_ctx* c, const gpk_parser* p, const gpk_batch* b, const gpk_results* o,
@@ -109,11 +110,39 @@ bool device_local_cpus(int dev, cpu_set_t& out) {
 struct Src {  // the capture byte stream: plain file (parallel pread) or gzip (zlib)
   int fd = -1;
   gzFile gz = nullptr;
-  uint64_t size = 0, pos = 0;
+  uint64_t size = 0, pos = 0;  // size: of the stream (the file, or the parts' sum)
   bool at_end = false;
   int threads = 8;
   bool pin = false;  // run the reader threads on `cpus` (the device's NUMA node)
   cpu_set_t cpus;
+  // A byte-range replay reads a stream made of file parts (the section header
+  // and interfaces, then the range's blocks): (file offset, length) in order.
+  // Empty: the whole file.
+  std::vector<std::pair<uint64_t, uint64_t>> parts;
+
+  // stream bytes [at, at + n) into dst (across parts); returns the count read
+  uint64_t pread_at(uint8_t* dst, uint64_t at, uint64_t n) const {
+    uint64_t done = 0, vbase = 0;
+    for (size_t k = 0; k < (parts.empty() ? 1 : parts.size()) && done < n; k++) {
+      const uint64_t foff = parts.empty() ? 0 : parts[k].first, plen = parts.empty() ? size : parts[k].second;
+      const uint64_t v = at + done;
+      if (v >= vbase + plen) {
+        vbase += plen;
+        continue;
+      }
+      uint64_t rel = v - vbase;
+      const uint64_t want = std::min<uint64_t>(n - done, plen - rel);
+      uint64_t got = 0;
+      while (got < want) {
+        const ssize_t r = pread(fd, dst + done + got, want - got, (off_t)(foff + rel + got));
+        if (r <= 0) return done + got;
+        got += (uint64_t)r;
+      }
+      done += got;
+      vbase += plen;
+    }
+    return done;
+  }
 
   // Fill dst with up to cap bytes of the stream; returns the count.
   uint64_t read(uint8_t* dst, uint64_t cap) {
@@ -141,12 +170,7 @@ struct Src {  // the capture byte stream: plain file (parallel pread) or gzip (z
       th.emplace_back([&, t] {
         if (pin) (void)pthread_setaffinity_np(pthread_self(), sizeof(cpus), &cpus);
         uint64_t a = (uint64_t)t * per, e = std::min<uint64_t>(want, a + per);
-        while (a < e) {
-          ssize_t k = pread(fd, dst + a, e - a, (off_t)(base + a));
-          if (k <= 0) break;
-          a += (uint64_t)k;
-          got[t] += (uint64_t)k;
-        }
+        if (a < e) got[t] = pread_at(dst + a, base + a, e - a);
       });
     }
     for (auto& x : th) x.join();
@@ -411,8 +435,103 @@ void free_cached(void* p) {
 
 }  // namespace
 
+// ---- byte-range replay (gpk_replay_file_range) --------------------------------
+// N callers (one per GPU) replay one pcapng file by byte ranges with no data
+// exchange. The range [begin, end) of a caller becomes the blocks that START
+// in [sync(begin), sync(end)), where sync(X) is the first offset >= X (a
+// multiple of 4) at which four plain EPBs chain inside the next 4 MiB under
+// the reader state after the file's leading non-packet blocks (the section
+// header and interfaces, read once by every caller): a property of the offset
+// alone, so a caller's end and the next caller's begin are the same offset.
+// The caller's reader sees the stream [0, H) ++ [sync(begin), sync(end)),
+// H = the first packet block, and does exactly what NgReader.ReadPacketData
+// does over it (ngread.go:494-718). The split is exact when, for every caller
+// but the last, its reader met a clean io.EOF at sync(end) (so sync(end) was a
+// real block boundary: a chain from a real boundary lands on real boundaries
+// only) and no block in its range changed the reader state (a new section or
+// interface): gpk_replay_range.clean / state_changed. Otherwise the caller
+// that first fails must replay from its sync_begin to the end of the file
+// (end = 0) and the later callers' results are dropped.
+namespace {
+
+uint32_t rd32(const uint8_t* p, bool be) {
+  return be ? (uint32_t)p[0] << 24 | (uint32_t)p[1] << 16 | (uint32_t)p[2] << 8 | p[3]
+            : (uint32_t)p[3] << 24 | (uint32_t)p[2] << 16 | (uint32_t)p[1] << 8 | p[0];
+}
+
+// The first packet block (EPB 6, SPB 3, obsolete PB 2) of the file, walking
+// block headers from the section header on; where the walk cannot go on (a
+// malformed length, or 64 MiB of leading blocks), the offset it stopped at.
+uint64_t ng_header_end(int fd, uint64_t size) {
+  uint64_t p = 0;
+  bool be = false;
+  uint8_t h[12];
+  while (p + 12 <= size && p < (64ull << 20)) {
+    if (pread(fd, h, 12, (off_t)p) != 12) break;
+    if (rd32(h, false) == 0x0A0D0D0Au) {  // section header (a palindrome): its byte-order magic
+      if (rd32(h + 8, false) == 0x1A2B3C4Du) be = false;
+      else if (rd32(h + 8, true) == 0x1A2B3C4Du) be = true;
+      else break;
+    }
+    const uint32_t typ = rd32(h, be), len = rd32(h + 4, be);
+    if (typ == 2 || typ == 3 || typ == 6) return p;
+    if (len < 12 || (len & 3) || len > size - p) break;
+    p += len;
+  }
+  return p;
+}
+
+}  // namespace
+
+static int plan_range(Src& src, uint32_t ng_flags, gpk_replay_range* rg, uint64_t* hdr_version) {
+  const uint64_t size = src.size;
+  const uint64_t H = ng_header_end(src.fd, size);
+  gpk_capreader* hr = nullptr;
+  if (gpk_capreader_create(&hr, GPK_CAP_PCAPNG, ng_flags)) return GPK_ENOMEM;
+  struct Free {
+    gpk_capreader* r;
+    ~Free() { gpk_capreader_destroy(r); }
+  } free_hr{hr};
+  std::vector<uint8_t> buf(H + 16, 0);
+  if (H && (uint64_t)pread(src.fd, buf.data(), H, 0) != H) return GPK_EINVAL;
+  gpk_capindex x{};
+  uint64_t used = 0;
+  const int st = gpk_capreader_index_all(hr, buf.data(), H, 0, 1, &x, &used);
+  const bool none = x.n == 0;
+  gpk_capindex_free(&x);
+  *hdr_version = st == GPK_CAP_MORE && none && used == H ? gpk_capreader_state_version(hr) : 0;
+  constexpr uint64_t kSpan = 4ull << 20, kWin = 4ull << 20;
+  auto sync_at = [&](uint64_t X) -> uint64_t {
+    if (X <= H) return H;
+    if (X >= size || !*hdr_version) return size;  // no header state to sync under: the first caller takes all
+    for (uint64_t a = X & ~3ull, from = X - a; a < size; a += kWin, from = 0) {
+      const uint64_t w = std::min<uint64_t>(kWin + kSpan, size - a), to = std::min<uint64_t>(kWin, w);
+      buf.assign(w, 0);
+      const uint64_t got = (uint64_t)std::max<ssize_t>(0, pread(src.fd, buf.data(), w, (off_t)a));
+      const uint64_t p = gpk_capreader_sync(hr, buf.data(), from, to, got, kSpan);
+      if (p != ~0ull) return a + p;
+    }
+    return size;
+  };
+  const uint64_t b = rg->begin == 0 ? 0 : sync_at(rg->begin);
+  const uint64_t e = rg->end == 0 || rg->end >= size ? size : std::max<uint64_t>(b, sync_at(rg->end));
+  rg->header_end = H;
+  rg->sync_begin = b;
+  rg->sync_end = e;
+  src.parts.clear();
+  if (b == 0) {
+    src.parts.push_back({0, e});
+  } else {
+    src.parts.push_back({0, H});
+    if (e > b) src.parts.push_back({b, e - b});
+  }
+  src.size = 0;
+  for (auto& p : src.parts) src.size += p.second;
+  return GPK_OK;
+}
+
 static int replay_file(gpk_ctx* ctx, const gpk_parser* parser, const char* path, const gpk_replay_opts* o,
-                       gpk_replay_cb cb, void* user, gpk_replay_stats* stats) {
+                       gpk_replay_cb cb, void* user, gpk_replay_stats* stats, gpk_replay_range* rg) {
   const double t_start = now_s();
   gpk_replay_opts opt{0, 0, 256ull << 20, 4, 1ull << 20, 8, nullptr, nullptr};
   if (o) {
@@ -486,6 +605,20 @@ static int replay_file(gpk_ctx* ctx, const gpk_parser* parser, const char* path,
   if (!format) {
     const uint32_t m = (uint32_t)magic[0] | (uint32_t)magic[1] << 8 | (uint32_t)magic[2] << 16 | (uint32_t)magic[3] << 24;
     format = m == 0x0A0D0D0Au ? GPK_CAP_PCAPNG : GPK_CAP_PCAP;
+  }
+  // ---- a byte range of the file (gpk_replay_file_range) ---------------------
+  uint64_t hdr_version = 0;
+  if (rg) {
+    if (src.gz || format != GPK_CAP_PCAPNG) {
+      snprintf(stats->error, sizeof(stats->error), "byte-range replay needs an uncompressed pcapng file");
+      return GPK_EUNSUPP;
+    }
+    const int rrc = plan_range(src, opt.ng_flags, rg, &hdr_version);
+    if (rrc) {
+      snprintf(stats->error, sizeof(stats->error), "byte-range replay: reading the file failed");
+      return rrc;
+    }
+    stats->file_bytes = src.size;
   }
   int rc = gpk_capreader_create(&rd, format, opt.ng_flags);
   if (rc) return rc;
@@ -651,7 +784,7 @@ static int replay_file(gpk_ctx* ctx, const gpk_parser* parser, const char* path,
   // ---- the loop --------------------------------------------------------------
   const uint8_t* carry = nullptr;
   uint64_t carry_len = 0, packet_index = 0;
-  bool finished = false;
+  bool finished = false, clean_eof = false;
   rc = GPK_OK;
   pl.slot_batches.assign(pl.slots.size(), 0);
   fill_ahead(1);
@@ -940,6 +1073,7 @@ static int replay_file(gpk_ctx* ctx, const gpk_parser* parser, const char* path,
       int is_eof = 0, is_panic = 0;
       gpk_capreader_error(rd, stats->error, sizeof(stats->error), &is_eof, &is_panic);
       stats->reader_status = is_eof ? 0 : (is_panic ? 2 : 1);
+      clean_eof = is_eof != 0;
       finished = true;
     }
     stats->slots++;
@@ -974,6 +1108,10 @@ static int replay_file(gpk_ctx* ctx, const gpk_parser* parser, const char* path,
             (t_delivered - t_tail) * 1e3, (t_fills - t_tail) * 1e3, (now_s() - t_tail) * 1e3);
   stats->alloc_wait_s = pl.alloc_wait_ns.load() * 1e-9;
   stats->wall_s = now_s() - t_start;
+  if (rg) {
+    rg->clean = good && rc == GPK_OK && clean_eof && stats->stream_bytes == src.size ? 1 : 0;
+    rg->state_changed = gpk_capreader_state_version(rd) != hdr_version ? 1 : 0;
+  }
   if (trace && trace[0] == '1')
     fprintf(stderr, "gpk_replay: setup %.4f s, loop %.4f s, %llu slots\n", t_loop - t_start, now_s() - t_loop,
             (unsigned long long)stats->slots);
@@ -988,15 +1126,22 @@ static int replay_file(gpk_ctx* ctx, const gpk_parser* parser, const char* path,
   return rc;
 }
 
-// The C entry point: no C++ exception crosses it (a thread or an allocation
+// The C entry points: no C++ exception crosses them (a thread or an allocation
 // the host cannot provide ends the call with an error; the pipeline's
 // destructors have waited for its streams and threads by then).
-extern "C" int gpk_replay_file(gpk_ctx* ctx, const gpk_parser* parser, const char* path, const gpk_replay_opts* o,
-                               gpk_replay_cb cb, void* user, gpk_replay_stats* stats) {
+static int replay_entry(gpk_ctx* ctx, const gpk_parser* parser, const char* path, const gpk_replay_opts* o,
+                        gpk_replay_cb cb, void* user, gpk_replay_stats* stats, gpk_replay_range* rg) {
   if (!ctx || !parser || !path || !stats) return GPK_EINVAL;
   memset(stats, 0, sizeof(*stats));
   try {
-    return replay_file(ctx, parser, path, o, cb, user, stats);
+    // the context's device for the pipeline's buffers, streams and launches
+    // (callbacks included); the caller's device is back on return
+    gpk::DeviceScope dscope(gpk_ctx_device(ctx));
+    if (dscope.err != hipSuccess) {
+      snprintf(stats->error, sizeof(stats->error), "hipSetDevice: %s", hipGetErrorString(dscope.err));
+      return GPK_EHIP;
+    }
+    return replay_file(ctx, parser, path, o, cb, user, stats, rg);
   } catch (const std::bad_alloc&) {
     snprintf(stats->error, sizeof(stats->error), "out of host memory");
     return GPK_ENOMEM;
@@ -1004,4 +1149,19 @@ extern "C" int gpk_replay_file(gpk_ctx* ctx, const gpk_parser* parser, const cha
     snprintf(stats->error, sizeof(stats->error), "%s", e.what());
     return GPK_EHIP;
   }
+}
+
+extern "C" int gpk_replay_file(gpk_ctx* ctx, const gpk_parser* parser, const char* path, const gpk_replay_opts* o,
+                               gpk_replay_cb cb, void* user, gpk_replay_stats* stats) {
+  return replay_entry(ctx, parser, path, o, cb, user, stats, nullptr);
+}
+
+extern "C" int gpk_replay_file_range(gpk_ctx* ctx, const gpk_parser* parser, const char* path,
+                                     gpk_replay_range* range, const gpk_replay_opts* o, gpk_replay_cb cb, void* user,
+                                     gpk_replay_stats* stats) {
+  if (!range) return GPK_EINVAL;
+  range->header_end = range->sync_begin = range->sync_end = 0;
+  range->clean = range->state_changed = 0;
+  if (range->end && range->end < range->begin) return GPK_EINVAL;
+  return replay_entry(ctx, parser, path, o, cb, user, stats, range);
 }

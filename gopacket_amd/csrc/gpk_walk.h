@@ -49,6 +49,14 @@ struct WalkSegs {
 // gpk_capture.cpp: the reader's state for the device walk; false when the
 // walk cannot run there (not pcapng, not opened yet, too many interfaces).
 bool gpk_capreader_walk_state(const gpk_capreader* r, gpk::WalkState* out);
+// gpk_capture.cpp: the first p in [from, to), p = 0 (mod 4), where four plain
+// EPBs chain under the reader's state inside b[p, min(end, p + span)) (~0:
+// none, or the reader is not an open pcapng reader); and the version of the
+// state that rule depends on (sections ended, interfaces; 0 when not open),
+// which changes when a block other than a packet changes it.
+uint64_t gpk_capreader_sync(const gpk_capreader* r, const uint8_t* b, uint64_t from, uint64_t to, uint64_t end,
+                            uint64_t span);
+uint64_t gpk_capreader_state_version(const gpk_capreader* r);
 
 // gpk_walk.hip: pass 1 over buf[p0, len) (buf 16-byte aligned, the reader at
 // p0, blocks at p0 + 4k) in segments of `seg` bytes from buf, pass 2 writing

@@ -176,7 +176,7 @@ class Context:
         return out.value
 
     def replay_file(self, parser, path, fmt=0, ng_flags=0, slot_bytes=0, slots=0, batch_pkts=0, read_threads=0,
-                    collect=True, on_batch=None, fields=False, packets=False):
+                    collect=True, on_batch=None, fields=False, packets=False, byte_range=None):
         """gpk_replay_file: the whole capture through HBM (BASELINE config C5).
         collect=True gathers every result (records, err_args, flows SoA, ci,
         caplens) in packet order; on_batch(first, n, records, err_args, flows,
@@ -188,7 +188,10 @@ class Context:
         launch's packets as (data, offsets, caplens): packet i is
         data[offsets[i]:offsets[i] + caplens[i]], a view of the staging buffer
         the file was read into (gpk_replay_opts.packets_cb; no copy, valid
-        during the call). Returns (results-or-None, stats dict)."""
+        during the call). byte_range=(begin, end): one caller's share of the
+        file (gpk_replay_file_range; end 0 = the file's end); the stats then
+        carry "range" (header_end, sync_begin, sync_end, clean, state_changed).
+        Returns (results-or-None, stats dict)."""
         if packets and collect:
             raise ValueError("packets=True hands out views of the staging buffers: use collect=False and on_batch")
         parts = []
@@ -245,16 +248,27 @@ class Context:
         c_pcb = _lib.REPLAY_PACKETS_CB(pcb) if packets else _lib.REPLAY_PACKETS_CB()
         o = _lib.ReplayOpts(fmt, ng_flags, slot_bytes, slots, batch_pkts, read_threads, c_fcb, c_pcb)
         st = _lib.ReplayStats()
-        rc = lib().gpk_replay_file(self.h, parser.h, path.encode() if isinstance(path, str) else path,
-                                   ctypes.byref(o), c_cb, None, ctypes.byref(st))
+        cpath = path.encode() if isinstance(path, str) else path
+        rg = None
+        if byte_range is None:
+            rc = lib().gpk_replay_file(self.h, parser.h, cpath, ctypes.byref(o), c_cb, None, ctypes.byref(st))
+        else:
+            rg = _lib.ReplayRange(int(byte_range[0]), int(byte_range[1]))
+            rc = lib().gpk_replay_file_range(self.h, parser.h, cpath, ctypes.byref(rg), ctypes.byref(o), c_cb, None,
+                                             ctypes.byref(st))
         if raised:
             raise raised[0]
         if rc != _lib.GPK_OK:
-            raise _lib.GpkError("gpk_replay_file: %d %s %s" % (rc, st.error.decode(errors="replace"),
-                                                               lib().gpk_last_hip_error().decode()))
+            err = _lib.GpkError("gpk_replay_file: %d %s %s" % (rc, st.error.decode(errors="replace"),
+                                                              lib().gpk_last_hip_error().decode()))
+            if rg is not None:  # where the range was cut, for the caller's redo (shard.replay_file_sharded)
+                err.range = {k: int(getattr(rg, k)) for k, _ in _lib.ReplayRange._fields_}
+            raise err
         stats = {k: getattr(st, k) for k, _ in _lib.ReplayStats._fields_}
         stats["error"] = st.error.decode(errors="replace")
         stats["kernel"] = st.kernel.decode(errors="replace")
+        if rg is not None:
+            stats["range"] = {k: int(getattr(rg, k)) for k, _ in _lib.ReplayRange._fields_}
         res = None
         if collect:
             if parts:

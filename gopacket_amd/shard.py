@@ -92,3 +92,79 @@ def exchange_packets(data, offsets, caplens, dest, world, group=None, pack=None)
                        torch.cumsum(r_cap.to(torch.int64), 0)[:-1]]) if len(r_cap) else r_cap.to(torch.int64)
     src = torch.repeat_interleave(torch.arange(world, device=dev), torch.tensor(rp, device=dev))
     return r_data, r_off, r_cap, src, r_idx
+
+
+# ---- one capture file replayed by N ranks (C5 at N GPUs) ---------------------
+def file_range(size, rank, world):
+    """Rank r's cut of a file of `size` bytes: [size*r/N, size*(r+1)/N), the
+    last one to the end (0). gpk_replay_file_range moves each cut to the next
+    block start (include/gpk_capture.h)."""
+    begin = size * rank // world
+    end = 0 if rank == world - 1 else size * (rank + 1) // world
+    return begin, end
+
+
+def first_inexact(ranges):
+    """The first rank whose share breaks the concatenation (None: exact).
+    ranges: every rank's gpk_replay_range outputs in rank order. Rank k < N-1
+    must have met io.EOF exactly at its sync_end (clean) with no section or
+    interface block inside its range (state_changed); the last rank's end is
+    the file's, whatever it holds (ngread.go:494-718)."""
+    for k, r in enumerate(ranges[:-1]):
+        if not r["clean"] or r["state_changed"]:
+            return k
+    return None
+
+
+def replay_file_sharded(ctx, parser, path, rank, world, gather=None, **kw):
+    """Rank `rank` of `world` replays its byte range of the pcapng file at
+    `path` (Context.replay_file(byte_range=...), no data exchange), then the
+    ranks compare their range outcomes (a few integers each: gather(obj) ->
+    list of every rank's obj, torch.distributed.all_gather_object by default).
+    When a rank's range was inexact (first_inexact), that rank replays again
+    from its sync_begin to the end of the file and every later rank drops its
+    results, so the ranks' results, concatenated in rank order, are always
+    gpk_replay_file's on the whole file. Returns (results, stats, info):
+    info["first_packet"] is the global index of this rank's first packet,
+    info["ranges"] every rank's range outputs, info["redo_rank"] the rank that
+    replayed again (None when the split was exact), info["dropped"] whether
+    this rank's results were dropped."""
+    import os
+    if gather is None:
+        import torch.distributed as dist
+
+        def gather(obj):
+            if world == 1 and not dist.is_initialized():
+                return [obj]
+            out = [None] * world
+            dist.all_gather_object(out, obj)
+            return out
+    from . import _lib
+    size = os.path.getsize(path)
+    try:
+        res, st = ctx.replay_file(parser, path, byte_range=file_range(size, rank, world), **kw)
+        mine = dict(st["range"], packets=int(st["packets"]))
+    except _lib.GpkError as e:
+        # a range whose reader failed outright (for instance on a record longer
+        # than the staging carry region) is inexact like one that did not end
+        # cleanly; the redo, or the rank before, decides what the file holds
+        if not hasattr(e, "range") or rank == world - 1:
+            raise
+        res, st = None, dict(packets=0, error=str(e))
+        mine = dict(e.range, clean=0, packets=0)
+    ranges = gather(mine)
+    f = first_inexact(ranges)
+    dropped = False
+    if f is not None and rank == f:
+        res, st = ctx.replay_file(parser, path, byte_range=(ranges[f]["sync_begin"], 0), **kw)
+        st["redo_first"] = dict(mine)
+        mine = dict(st["range"], packets=int(st["packets"]))
+    elif f is not None and rank > f:
+        dropped = True
+        res = None if res is None else {k: v[:0] for k, v in res.items()}
+        st["packets"] = 0
+        mine = dict(mine, packets=0)
+    counts = gather(mine["packets"]) if f is not None else [r["packets"] for r in ranges]
+    info = dict(first_packet=int(sum(counts[:rank])), ranges=ranges, redo_rank=f, dropped=dropped,
+                packets_per_rank=[int(c) for c in counts])
+    return res, st, info

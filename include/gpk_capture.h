@@ -208,6 +208,34 @@ typedef void (*gpk_replay_cb)(void* user, uint64_t first_packet, uint64_t n, con
 int gpk_replay_file(gpk_ctx* ctx, const gpk_parser* p, const char* path, const gpk_replay_opts* opts,
                     gpk_replay_cb cb, void* user, gpk_replay_stats* stats);
 
+/* One caller's share of a pcapng file replayed by N callers (one per GPU, no
+ * data exchange): the same loop as gpk_replay_file (pcapgo.NgReader +
+ * DecodeLayers, ngread.go:494-718, parser.go:303-317) over the blocks that
+ * START in [sync(begin), sync(end)). sync(X) is the first offset >= X, a
+ * multiple of 4, where four plain Enhanced Packet Blocks chain inside the next
+ * 4 MiB under the reader state after the file's leading non-packet blocks
+ * (section header, interfaces), which every caller reads first: it depends on
+ * X and the file only, so caller k's sync(end) is caller k+1's sync(begin).
+ * begin 0: from the file's start; end 0: to its end. Callers number their
+ * packets from 0. Cut the file at size*k/N.
+ * The N results, concatenated in range order, are exactly gpk_replay_file's
+ * when every caller but the last reports clean (its reader met io.EOF exactly
+ * at sync_end, so sync_end is a real block boundary) and !state_changed (no
+ * section header or interface block inside its range). Otherwise let f be the
+ * first caller that does not: its result and every later one's are replaced
+ * by a replay of [f's sync_begin, end of file) (begin = sync_begin, end = 0),
+ * which is exact. Uncompressed pcapng only (GPK_EUNSUPP otherwise). */
+typedef struct gpk_replay_range {
+  uint64_t begin, end;    /* in: this caller's cut of the file's bytes                       */
+  uint64_t header_end;    /* out: the file's first packet block (the header every caller reads) */
+  uint64_t sync_begin;    /* out: the first block this caller replayed (0: the file's start)  */
+  uint64_t sync_end;      /* out: where its blocks had to end                                 */
+  int clean;              /* out: the reader met io.EOF exactly at sync_end                   */
+  int state_changed;      /* out: a block in the range changed the reader state               */
+} gpk_replay_range;
+int gpk_replay_file_range(gpk_ctx* ctx, const gpk_parser* p, const char* path, gpk_replay_range* range,
+                          const gpk_replay_opts* opts, gpk_replay_cb cb, void* user, gpk_replay_stats* stats);
+
 #ifdef __cplusplus
 }
 #endif

@@ -45,3 +45,23 @@ def test_c_abi_replay_with_fields(tmp_path):
     import re
     m = re.search(r"replay c4\.pcapng: (\d+) packets, (\d+) checked", out.stdout)
     assert m and int(m.group(1)) == 20000 and int(m.group(2)) > 15000, out.stdout
+
+
+def test_c_abi_threads_contexts():
+    """The Go-shaped multi-GPU caller: one process, four
+    OS threads, a gpk_ctx + parser per thread on device t % ndev (four
+    contexts on the test box's one GPU), each decoding its byte-balanced slice
+    of one batch concurrently: host buffers, device buffers on a stream of its
+    own, and a context shared by all four. The slices put back together equal
+    one context's decode bit for bit, that decode equals the committed oracle
+    expectations for every packet, and after every gpk_* call the thread's
+    current HIP device is the one it set before the call."""
+    exe = os.path.join(ROOT, "tests", "c_abi", "gpk_threads_test")
+    if not os.path.exists(exe):
+        build_c_abi_test()
+    out = subprocess.run([exe, os.path.join(ROOT, "tests", "golden", "c_abi"), "4", "400", "3"],
+                         capture_output=True, text=True, timeout=180)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert "all checks passed (threads)" in out.stdout
+    assert ", 0 differ from the oracle" in out.stdout, out.stdout
+    assert "per-thread host bit-exact, device bit-exact, shared bit-exact" in out.stdout, out.stdout
