@@ -163,6 +163,24 @@ def gather_ranks(x, world):
     return out
 
 
+def gather_obj(x, world):
+    """Every rank's x (any picklable object), in rank order; [x] at world size
+    1 without a process group."""
+    import torch.distributed as dist
+    if world == 1 and not dist.is_initialized():
+        return [x]
+    out = [None] * world
+    dist.all_gather_object(out, x)
+    return out
+
+
+def rank_threads():
+    """Host threads one rank may use for its parity checks: the job's CPU
+    share divided among the ranks on this node (torchrun's LOCAL_WORLD_SIZE)."""
+    local = max(1, int(os.environ.get("LOCAL_WORLD_SIZE", "1")))
+    return max(2, host_cores()[0] // local)
+
+
 def barrier(world):
     import torch
     import torch.distributed as dist
@@ -264,10 +282,21 @@ def run_config(name, n, steps, warmup, rank, world, ctx, check_sample=2048, prob
     parity = None
     if check_sample:
         parity = sample_parity(name, cfg, rec, fl, err, first, n, check_sample)
+        if world > 1:
+            every = gather_obj(parity, world)
+            parity = ("bit-exact on every rank: " if all(p.startswith("bit-exact") for p in every)
+                      else "MISMATCH on a rank: ") + "; ".join("rank %d %s" % (k, p) for k, p in enumerate(every))
     full = None
     if full_check:
-        full, full_s = full_parity(name, cfg, data, off, cap, rec, fl, err, n, host_cores()[0])
-        full = dict(result=full, seconds=round(full_s, 2))
+        full, full_s = full_parity(name, cfg, data, off, cap, rec, fl, err, n, rank_threads())
+        full = dict(result=full, seconds=round(full_s, 2), threads=rank_threads())
+        if world > 1:  # every rank checks its own shard; the line carries each rank's result
+            full = dict(ranks=gather_obj(dict(full, rank=rank, first_packet=first, packets=n), world),
+                        result=None, seconds=None)
+            bad = [x for x in full["ranks"] if not x["result"].startswith("bit-exact")]
+            full["result"] = ("bit-exact on every rank (%d ranks, %d packets)" % (world, sum(
+                x["packets"] for x in full["ranks"]))) if not bad else "MISMATCH on rank(s) %s" % [x["rank"] for x in bad]
+            full["seconds"] = max(x["seconds"] for x in full["ranks"])
     res = dict(full_parity=full, n=n, payload_bytes=payload_bytes, wall_s=wall_max, kernel_ms=kernel_ms,
                kernel_ms_ranks=kernel_ms_ranks,
                algo_bytes=payload_bytes + INDEX_BYTES * n, parity=parity, probe_gbs=probe_gbs, skeleton_ms=skel_ms,
@@ -990,7 +1019,7 @@ def bpf_filter_bench(ctx, n=64 * 2**20, reps=10):
                          "packets in HBM", packets=n, programs=out)
 
 
-def fields_bench(ctx, name="c4", n=64 * 2**20, reps=5, check_packets=4 << 20):
+def fields_bench(ctx, name="c4", n=64 * 2**20, reps=5, check_packets=4 << 20, first=0, threads=None):
     """Layer fields with the decode (gpk_decode_batch_fields, no layouts: ONE
     launch that also writes each packet's 128-byte gpk_fields record) against
     the two-launch form (decode with layouts, then gpk_extract_fields), on the
@@ -1005,7 +1034,7 @@ def fields_bench(ctx, name="c4", n=64 * 2**20, reps=5, check_packets=4 << 20):
     cfg = CONFIGS[name]
     parser = engine.ParserConfig(17, [engine.DECODER_KINDS[d] for d in cfg["decoders"]], outputs=cfg["outputs"])
     stream = torch.cuda.current_stream()
-    data, off, cap = synth.device_batch(cfg["synth"], 0, n, stream=stream)
+    data, off, cap = synth.device_batch(cfg["synth"], first, n, stream=stream)
     rec = torch.empty(n * 16, dtype=torch.uint8, device="cuda")
     err = torch.zeros(2 * n, dtype=torch.int32, device="cuda")
     fl = torch.empty(3 * n, dtype=torch.int64, device="cuda")
@@ -1041,7 +1070,7 @@ def fields_bench(ctx, name="c4", n=64 * 2**20, reps=5, check_packets=4 << 20):
         lo, hi = int(o.min()), int((o + c).max())
         host = np.zeros(hi - lo + 16, np.uint8)
         host[:hi - lo] = data[lo:hi].cpu().numpy()
-        ref = p.decode(host, o - np.uint64(lo), c, nthreads=host_cores()[0], layouts=True)
+        ref = p.decode(host, o - np.uint64(lo), c, nthreads=threads or rank_threads(), layouts=True)
         ok = rec[a * 16:b * 16].cpu().numpy().view(_lib.RECORD_DTYPE) == ref["records"]
         ok &= (err[2 * a:2 * b].cpu().numpy().view(np.uint32).reshape(-1, 2) == ref["err_args"].reshape(-1, 2)).all(1)
         rf = ref["flows"].reshape(3, -1)
@@ -1083,6 +1112,105 @@ def load_traffic(name, n):
                 "profiles/%s_pmc.json (%s)" % (t["profile"], t.get("kernel", "decode_kernel")))
     except (OSError, KeyError, ValueError):
         return None, None
+
+
+def c5_sharded(ctx, rank, world, gib=10.0, reps=2, threads=8):
+    """C5 at N GPUs: rank 0 writes the same pcapng as c5_replay (the C4 IMIX
+    mix, ~gib GiB, page cached); every rank replays its byte range of it
+    (shard.replay_file_sharded -> gpk_replay_file_range: its own staging, HtoD
+    link, walk and decode, no data exchange; the ranks swap only their range
+    outcomes, and an inexact split is redone, so the ranks' results in rank
+    order are always the whole file's). The job's wall per repetition is the
+    slowest rank's, from a common barrier; value = the file's packets / the best
+    repetition's job wall. Each rank checks its sampled packets against the
+    oracle at their global index."""
+    import torch
+    import torch.distributed as dist
+    from gopacket_amd import _lib, engine, shard, synth
+    from oracle import oracle as O
+    S = _lib.synth_lib()
+    cfg = CONFIGS["c4"]
+    parser = engine.ParserConfig(17, [engine.DECODER_KINDS[d] for d in cfg["decoders"]], outputs=cfg["outputs"])
+    per = S.gpk_synth_bytes(4, 0, 1 << 20) / (1 << 20) + 32 + 1.5
+    n = int(gib * 2**30 / per)
+    tag = os.environ.get("MASTER_PORT", str(os.getpid()))
+    path = os.path.join(os.environ.get("TMPDIR", "/tmp"), "gpk_c5_shared_%s.pcapng" % tag)
+    gen_s = 0.0
+    if rank == 0:
+        t0 = time.perf_counter()
+        size = S.gpk_synth_write_pcapng(path.encode(), 4, 0, n, host_cores()[0])
+        if size:
+            fd = os.open(path, os.O_RDONLY)
+            os.fsync(fd)
+            os.close(fd)
+        gen_s = time.perf_counter() - t0
+    ok = gather_obj(bool(rank != 0 or size), world)
+    if not all(ok):
+        raise RuntimeError("could not write %s" % path)
+    rng = np.random.default_rng(5 + rank)
+    local_sample = np.unique(rng.integers(0, n // world + n // (4 * world) + 1, 2048 // world + 64))
+    picked = {}
+
+    def on_batch(first, k, rec, err, fl, ci, cap):
+        lo, hi = np.searchsorted(local_sample, first), np.searchsorted(local_sample, first + k)
+        for i in local_sample[lo:hi]:
+            j = int(i) - first
+            picked[int(i)] = (rec[j].copy(), fl[[j, k + j, 2 * k + j]].copy())
+
+    runs = []
+    try:
+        for _ in range(reps):
+            picked.clear()
+            barrier(world)
+            t0 = time.perf_counter()
+            _, st, info = shard.replay_file_sharded(ctx, parser, path, rank, world, collect=False,
+                                                     on_batch=on_batch, read_threads=threads)
+            wall = time.perf_counter() - t0
+            runs.append((wall, st, info, dict(picked)))
+    finally:
+        barrier(world)
+        if rank == 0:
+            os.unlink(path)
+    probe = htod_probe(n * per / world)  # every rank's link at once, its share of the file per round
+    walls = [gather_obj(r[0], world) for r in runs]
+    best = min(range(reps), key=lambda k: max(walls[k]))
+    wall, st, info, got = runs[best]
+    # this rank's sampled packets against the oracle, at their global index
+    idx = sorted(i for i in got if not info["dropped"])
+    parity = "no sampled packets"
+    if idx:
+        pk = [synth.packet(4, info["first_packet"] + i) for i in idx]
+        cap = np.array([len(x) for x in pk], np.uint32)
+        off = np.concatenate([[0], np.cumsum(cap[:-1], dtype=np.uint64)]).astype(np.uint64)
+        ref = O.OracleParser(17, [ORACLE_DEC[d] for d in cfg["decoders"]], outputs=cfg["outputs"]).decode(
+            np.frombuffer(b"".join(pk) + bytes(16), np.uint8), off, cap, layouts=False)
+        g = np.array([got[i][0] for i in idx], _lib.RECORD_DTYPE)
+        gfl = np.stack([got[i][1] for i in idx], axis=1).reshape(-1)
+        good = np.array_equal(g, ref["records"]) and np.array_equal(gfl, ref["flows"])
+        parity = "%s (%d sampled packets vs oracle)" % ("bit-exact" if good else "MISMATCH", len(idx))
+    mine = dict(rank=rank, wall_s=round(wall, 4), packets=int(st["packets"]), first_packet=info["first_packet"],
+                file_bytes=int(st.get("file_bytes", 0)), error=st.get("error"), redo=info["redo_rank"] == rank,
+                dropped=info["dropped"], range=st.get("range"), parity=parity,
+                breakdown_s=dict(read=round(st.get("read_s", 0), 4), index=round(st.get("index_s", 0), 4),
+                                 gpu_copy_decode=round(st.get("gpu_s", 0), 4), kernel=round(st.get("kernel_s", 0), 4),
+                                 deliver=round(st.get("deliver_s", 0), 4)),
+                htod_probe_GBps=probe["htod_probe_GBps"])
+    ranks = gather_obj(mine, world)
+    total = sum(r["packets"] for r in ranks)
+    jw = max(walls[best])
+    last = max(r["rank"] for r in ranks if not r["dropped"])
+    exact = total == n and ranks[last]["error"] == "EOF" and all(
+        r["parity"].startswith("bit-exact") for r in ranks if not r["dropped"])
+    return dict(workload="C5 at %d GPUs: one pcapng of the C4 IMIX mix, each rank replays its byte range end to "
+                         "end incl. HtoD/DtoH (gpk_replay_file_range)" % world,
+                packets=total, file_packets=n, value=round(total / jw / 1e6, 2), unit="Mpkts/s",
+                GBps=round(sum(r["file_bytes"] for r in ranks) / jw / 1e9, 2), wall_s=round(jw, 4),
+                runs_wall_s=[round(max(w), 4) for w in walls], scaling="strong",
+                redo_rank=info["redo_rank"], write_s=round(gen_s, 2),
+                htod_probe_GBps_sum=round(sum(r["htod_probe_GBps"] for r in ranks), 2),
+                parity=("bit-exact" if exact else "MISMATCH") + " (%d of %d packets delivered across ranks, the "
+                       "last rank's reader at EOF, every rank's sample vs oracle)" % (total, n),
+                ranks=ranks, source="page-cached file in %s" % os.path.dirname(path))
 
 
 def main():
@@ -1138,7 +1266,17 @@ def main():
         results[name] = run_config(name, args.packets, args.steps, args.warmup, rank, world, ctx,
                                    check_sample=0 if args.no_parity else 2048,
                                    probe=not args.no_probe,
-                                   full_check=world == 1 and not (args.no_parity or args.no_full_parity))
+                                   full_check=not (args.no_parity or args.no_full_parity))
+    threads = host_cores()[0]
+    # every rank runs the rows below its own shard at N > 1 (weak: its own 64M batch; C5: its byte range)
+    fields_ranks = None
+    if not args.no_fields:
+        fr = fields_bench(ctx, n=args.packets, first=rank * args.packets, threads=rank_threads())
+        fields_ranks = gather_obj(dict(fr, rank=rank), world)
+    c5 = None
+    if args.c5 > 0:
+        c5 = (c5_replay(ctx, gib=args.c5, cpu_threads=threads) if world == 1
+              else c5_sharded(ctx, rank, world, gib=args.c5))
     if rank == 0:
         head = names[0]
         r = results[head]
@@ -1190,11 +1328,14 @@ def main():
             out["configs"][name] = row
         if args.pcie and world == 1:
             out["pcie_inclusive"] = pcie_inclusive(head, ctx)
-        if world == 1 and not args.no_fields:
-            out["fields"] = fields_bench(ctx, n=args.packets)
-        threads = host_cores()[0]
-        if args.c5 > 0 and world == 1:
-            out["c5"] = c5_replay(ctx, gib=args.c5, cpu_threads=threads)
+        if fields_ranks:
+            out["fields"] = dict(fields_ranks[0])
+            if world > 1:
+                out["fields"]["ranks"] = [{k: f[k] for k in ("rank", "value", "kernel_ms", "frac", "parity")}
+                                          for f in fields_ranks]
+                out["fields"]["value_all_ranks"] = round(sum(f["value"] for f in fields_ranks), 2)
+        if c5 is not None:
+            out["c5"] = c5
         if args.bpf and world == 1:
             out["bpf"] = bpf_filter_bench(ctx)
         if args.flows and world == 1:
@@ -1206,6 +1347,9 @@ def main():
             out["cpu_baseline"] = cpu_baseline(head, names, seconds=args.cpu_seconds)
         else:
             out["cpu_baseline"] = None
+            if world > 1:
+                out["cpu_baseline_note"] = ("measured at N=1 only (BENCH line): at N>1 the ranks share the host "
+                                            "cores, which the per-rank parity checks use")
         print(json.dumps(out))
     if dist.is_initialized():
         dist.barrier()

@@ -141,20 +141,25 @@ def replay_file_sharded(ctx, parser, path, rank, world, gather=None, **kw):
             return out
     from . import _lib
     size = os.path.getsize(path)
+    failed = None
     try:
         res, st = ctx.replay_file(parser, path, byte_range=file_range(size, rank, world), **kw)
         mine = dict(st["range"], packets=int(st["packets"]))
     except _lib.GpkError as e:
-        # a range whose reader failed outright (for instance on a record longer
+        # a range whose replay failed outright (for instance on a record longer
         # than the staging carry region) is inexact like one that did not end
-        # cleanly; the redo, or the rank before, decides what the file holds
-        if not hasattr(e, "range") or rank == world - 1:
+        # cleanly: after a false start it is dropped, else (a redo, or a kept
+        # last range) the failure is the whole file's and is raised below
+        if not hasattr(e, "range"):
             raise
+        failed = e
         res, st = None, dict(packets=0, error=str(e))
         mine = dict(e.range, clean=0, packets=0)
     ranges = gather(mine)
     f = first_inexact(ranges)
     dropped = False
+    if failed is not None and (f is None or rank < f):  # kept as it is: the failure is the file's
+        raise failed
     if f is not None and rank == f:
         res, st = ctx.replay_file(parser, path, byte_range=(ranges[f]["sync_begin"], 0), **kw)
         st["redo_first"] = dict(mine)

@@ -109,8 +109,8 @@ def test_bench_two_ranks_strong_and_weak():
         env.pop(k, None)
     cmd = [sys.executable, "bench.py", "--gpus", "2", "--dist-backend", "gloo",
            "--same-device", "--configs", "c3,c4s", "--packets", str(1 << 20), "--steps", "2", "--warmup", "1",
-           "--no-cpu-baseline", "--c5", "0", "--no-probe"]
-    out = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=280)
+           "--no-cpu-baseline", "--c5", "0.03", "--no-probe"]
+    out = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=400)
     assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-3000:]
     lines = [x for x in out.stdout.splitlines() if x.startswith("{")]
     assert len(lines) == 1, out.stdout[-2000:]
@@ -125,6 +125,22 @@ def test_bench_two_ranks_strong_and_weak():
     assert c["parity"].startswith("bit-exact") and 1.0 <= c["byte_balance"] < 1.001
     assert len(c["kernel_ms_ranks"]) == 2 and abs(c["kernel_ms"] - max(c["kernel_ms_ranks"])) < 1e-3
     assert r["roofline"]["kernel"].startswith("gpk::decode_kernel<true,false,true,false,")
+    # the N>1 line is as strong as the N=1 line: every rank checks every packet of its
+    # own shard against the oracle, runs the layer-fields row and its share of C5
+    assert r["parity"].startswith("bit-exact on every rank")
+    for row in (r["full_parity"], c["full_parity"]):
+        assert row["result"].startswith("bit-exact on every rank (2 ranks"), row
+        assert [x["rank"] for x in row["ranks"]] == [0, 1]
+        assert all(x["result"].startswith("bit-exact (all %d packets" % x["packets"]) for x in row["ranks"]), row
+    assert sum(x["packets"] for x in c["full_parity"]["ranks"]) == 1 << 20
+    assert [x["first_packet"] for x in r["full_parity"]["ranks"]] == [0, 1 << 20]
+    f = r["fields"]
+    assert len(f["ranks"]) == 2 and all(x["parity"].startswith("bit-exact") for x in f["ranks"]), f
+    c5 = r["c5"]
+    assert c5["parity"].startswith("bit-exact") and c5["packets"] == c5["file_packets"] > 0, c5
+    assert [x["rank"] for x in c5["ranks"]] == [0, 1] and c5["ranks"][1]["first_packet"] == c5["ranks"][0]["packets"]
+    assert c5["redo_rank"] is None and all(x["range"]["clean"] for x in c5["ranks"]), c5["ranks"]
+    assert r["cpu_baseline"] is None and "N=1 only" in r["cpu_baseline_note"]
 
 def test_bench_rccl_world_one():
     """bench.py's RCCL branch on a one-GPU box: torchrun with one rank and
