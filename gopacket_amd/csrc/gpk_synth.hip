@@ -361,16 +361,21 @@ __global__ __launch_bounds__(256) void probe_skeleton_idx_kernel(const uint8_t* 
       const uint64_t q = (flags & 1024)  ? ((w0 + lane) & ((1u << 14) - 1))
                          : (flags & 128) ? ((w0 + lane) & ((1u << 20) - 1))
                                          : w0 + lane;
-      uint8_t* r = wbuf + q * 16;
-      uint64_t* f = reinterpret_cast<uint64_t*>(wbuf + 16 * n) + (q - (w0 + lane));
+      // wbytes 8 / 32: the 8-byte narrow record (gpk_record8), alone or with the flows
+      const bool narrow = wbytes == 8 || wbytes == 32, flows = wbytes == 32 || wbytes >= 40;
+      const uint32_t rb = narrow ? 8u : 16u;
+      uint8_t* r = wbuf + q * rb;
+      uint64_t* f = reinterpret_cast<uint64_t*>(wbuf + rb * n) + (q - (w0 + lane));
       if (flags & 8) {  // default (temporal) store policy
-        if (wbytes >= 16) *reinterpret_cast<u32x4*>(r) = u32x4{acc, lane, 0u, 1u};
-        if (wbytes >= 40)
+        if (narrow) *reinterpret_cast<uint64_t*>(r) = (uint64_t)lane << 32 | acc;
+        else if (wbytes >= 16) *reinterpret_cast<u32x4*>(r) = u32x4{acc, lane, 0u, 1u};
+        if (flows)
 #pragma unroll
           for (int j = 0; j < 3; j++) f[j * n + w0 + lane] = (uint64_t)acc * (j + 1);
       } else {
-        if (wbytes >= 16) __builtin_nontemporal_store(u32x4{acc, lane, 0u, 1u}, reinterpret_cast<u32x4*>(r));
-        if (wbytes >= 40)
+        if (narrow) __builtin_nontemporal_store((uint64_t)lane << 32 | acc, reinterpret_cast<uint64_t*>(r));
+        else if (wbytes >= 16) __builtin_nontemporal_store(u32x4{acc, lane, 0u, 1u}, reinterpret_cast<u32x4*>(r));
+        if (flows)
 #pragma unroll
           for (int j = 0; j < 3; j++) __builtin_nontemporal_store((uint64_t)acc * (j + 1), f + j * n + w0 + lane);
       }
@@ -392,12 +397,17 @@ __global__ __launch_bounds__(256) void probe_skeleton_idx_kernel(const uint8_t* 
 #pragma unroll
     for (int j = 0; j < 3; j++) *reinterpret_cast<uint64_t*>(l + 10 * lane + 4 + 2 * j) = a * (j + 1);
     asm volatile("" ::: "memory");
-    const uint64_t lim = (n - w0) * 40;  // bytes of this wave's run
+    const uint64_t lim = (n - w0 < 64 ? n - w0 : 64) * 40;  // bytes of this wave's run
     u32x4* r = reinterpret_cast<u32x4*>(wbuf + w0 * 40);
 #pragma unroll
     for (uint32_t k = 0; k < 3; k++) {
       const uint32_t c = 64 * k + lane;
-      if (c < 160 && 16ull * c < lim) __builtin_nontemporal_store(reinterpret_cast<const u32x4*>(l)[c], r + c);
+      // whole chunks inside the run; an odd packet count leaves an 8-byte tail
+      if (c < 160 && 16ull * c + 16 <= lim) {
+        __builtin_nontemporal_store(reinterpret_cast<const u32x4*>(l)[c], r + c);
+      } else if (c < 160 && 16ull * c + 8 == lim) {
+        __builtin_nontemporal_store(reinterpret_cast<const uint64_t*>(l)[2 * c], reinterpret_cast<uint64_t*>(r + c));
+      }
     }
   };
   if (flags & 32) store_out();  // the outputs before the stream (their values are whatever acc holds then)
@@ -546,7 +556,8 @@ extern "C" {
 // one of the forms (0, 16, 40, 168), is rejected before launch (-1). Round 4's
 // fault: the wave-0 form stored flows into a 16-byte-per-packet buffer.
 static bool skeleton_args_ok(uint64_t n, uint32_t wbytes, int flags, uint64_t wbuf_bytes, bool storer) {
-  if (wbytes != 0 && wbytes != 16 && wbytes != 40 && wbytes != 168) return false;
+  if (wbytes != 0 && wbytes != 8 && wbytes != 16 && wbytes != 32 && wbytes != 40 && wbytes != 168) return false;
+  if ((flags & 256) && wbytes != 16 && wbytes != 40) return false;  // the wave-0 form stores 16-byte records
   if (storer && wbytes != 16 && wbytes != 40) return false;
   if ((flags & 512) && wbytes != 40) return false;
   return wbuf_bytes >= (uint64_t)wbytes * n;

@@ -20,6 +20,9 @@ def S():
     (16, 2 | 512, 16 * N),    # interleaved form needs 40 B per packet
     (168, 2, 40 * N),         # fields past a 40 B/packet buffer
     (24, 2, 40 * N),          # not a form
+    (0, 2 | 256, 16 * N),     # the wave-0 form stores 16-byte records whatever wbytes says
+    (8, 2 | 512, 40 * N),     # the interleaved form is the 40-byte one
+    (32, 2, 16 * N),          # narrow records + flows past a 16 B/packet buffer
 ])
 def test_skeleton_rejects_overrun(S, wbytes, flags, size):
     assert S.gpk_probe_skeleton_idx(16, 16, 16, N, 16, size, wbytes, flags, 16, None) == -1
