@@ -43,6 +43,8 @@ LAYOUT_ABSENT = 0xFFFFFFFF
 MAX_INLINE_LAYERS = 16
 
 RECORD_DTYPE = np.dtype([("layers", "<u8"), ("status", "<u4"), ("ip4_csum", "<u2"), ("l4_csum", "<u2")])
+RECORD8_DTYPE = np.dtype([("layers", "<u4"), ("status", "<u4")])  # gpk_record8 (gpk_decode_batch_narrow)
+ST8_NLAYERS_MASK, ST8_WIDE = 0xF, 1 << 12
 LAYOUT_DTYPE = np.dtype([("start", "<u4", (8,)), ("end", "<u4", (8,))])
 # include/gpk.h gpk_fields (128 B): the scalar layer fields (gpk_extract_fields)
 FIELDS_DTYPE = np.dtype({
@@ -70,7 +72,8 @@ EXPORTS = (
     "gpk_parser_create", "gpk_parser_destroy", "gpk_parser_add_decoder", "gpk_parser_set_options",
     "gpk_parser_set_outputs", "gpk_parser_decoder_for", "gpk_parser_set_ethertype",
     "gpk_parser_set_ipprotocol", "gpk_parser_set_tcp_port", "gpk_parser_set_udp_port", "gpk_ctx_create",
-    "gpk_ctx_destroy", "gpk_ctx_set_table_mode", "gpk_decode_batch", "gpk_decode_batch_fields", "gpk_extract_fields",
+    "gpk_ctx_destroy", "gpk_ctx_set_table_mode", "gpk_decode_batch", "gpk_decode_batch_narrow", "gpk_decode_batch_fields",
+    "gpk_extract_fields",
     "gpk_decode_kernel_name", "gpk_decode_occupancy", "gpk_diag_set_buffer", "gpk_decode_batch_host", "gpk_decode_batch_host_fields",
     "gpk_decoded_list",
     "gpk_decoded_list_host", "gpk_host_alloc", "gpk_host_free", "gpk_format_error", "gpk_layer_type_name", "gpk_code_layer_type", "gpk_strerror",
@@ -212,6 +215,11 @@ class Results(ctypes.Structure):
                 ("layouts", ctypes.c_void_p)]
 
 
+class Results8(ctypes.Structure):
+    _fields_ = [("records", ctypes.c_void_p), ("wide", ctypes.c_void_p), ("err_args", ctypes.c_void_p),
+                ("flows", ctypes.c_void_p)]
+
+
 _lib = None
 
 
@@ -253,6 +261,7 @@ def lib():
         "gpk_ctx_destroy": ([vp], c_int),
         "gpk_ctx_set_table_mode": ([vp, c_int], c_int),
         "gpk_decode_batch": ([vp, vp, P(Batch), P(Results), vp], c_int),
+        "gpk_decode_batch_narrow": ([vp, vp, P(Batch), P(Results8), vp], c_int),
         "gpk_decode_batch_host": ([vp, vp, P(Batch), P(Results)], c_int),
         "gpk_decode_batch_host_fields": ([vp, vp, P(Batch), P(Results), vp], c_int),
         "gpk_extract_fields": ([P(Batch), vp, vp, vp], c_int),

@@ -75,6 +75,10 @@ struct KParams {
   int32_t* kcode;
   uint64_t* diag;           // GPK_DIAG_TIMES builds only: 8 u64 per wave (gpk_diag_set_buffer)
   gpk_fields* fields;       // fused layer fields (gpk_decode_batch_fields), the fields kernels only
+  // narrow records (gpk_decode_batch_narrow): records holds gpk_record8[n], and a
+  // packet whose record does not fit writes its full one to wide[i] (gpk.h)
+  uint32_t narrow;
+  gpk_record* wide;
 };
 
 // Straight-line common-case parse (fast_parser below). Each bit says the

@@ -52,8 +52,8 @@ __device__ __forceinline__ uint64_t option_map(const H& h, uint32_t s, uint32_t 
 // 2 + k, walked as IPv6HopByHop.DecodeFromBytes walks them (ip6.go:509-526,
 // TLVs :327-346: Pad1 is one byte, every other option its length byte + 2;
 // the loop runs while the offset is below ActualLength = HeaderLength * 8 +
-// 8). Only for HeaderLength <= 2 (ActualLength <= 26: every start fits the 24
-// bits), else 0. s: the IPv6 start. The IPv6 decode succeeded, so every
+// 8). Only for HeaderLength <= 2 (ActualLength <= 24: every start, at byte
+// 2 + k < 24, fits the 24 bits), else 0. s: the IPv6 start. The IPv6 decode succeeded, so every
 // option it walked was inside the slice.
 template <class H>
 __device__ __forceinline__ uint32_t hbh_map(const H& h, uint32_t s) {

@@ -643,6 +643,8 @@ static int make_params(gpk_ctx* c, const gpk_parser* p, const gpk_batch* b, cons
   P.kcode = nullptr;
   P.diag = g_diag.load();
   P.fields = nullptr;
+  P.narrow = 0;
+  P.wide = nullptr;
   return GPK_OK;
 }
 
@@ -664,6 +666,27 @@ int gpk_decode_batch(gpk_ctx* c, const gpk_parser* p, const gpk_batch* b, const 
   rc = upload(c, p, P, &slot, s);
   if (rc) return rc;
   HIPCHK(gpk_launch_decode(&P, (p->outputs & GPK_OUT_L4_CSUM) != 0, o->layouts != nullptr, s));
+  return note_launch(c, slot, s);
+}
+
+int gpk_decode_batch_narrow(gpk_ctx* c, const gpk_parser* p, const gpk_batch* b, const gpk_results8* o8,
+                            void* stream) {
+  if (!o8 || (b && b->n && (!o8->records || !o8->wide))) return GPK_EINVAL;
+  // the kernels take the narrow records through the record pointer
+  const gpk_results o{reinterpret_cast<gpk_record*>(o8->records), o8->err_args, o8->flows, nullptr};
+  gpk::KParams P;
+  int rc = make_params(c, p, b, &o, P);
+  if (rc) return rc;
+  P.narrow = 1;
+  P.wide = o8->wide;
+  hipStream_t s = (hipStream_t)stream;
+  std::lock_guard<std::mutex> g(c->mu);
+  gpk::DeviceScope dscope(c->device);
+  HIPCHK(dscope.err);
+  int slot = 0;
+  rc = upload(c, p, P, &slot, s);
+  if (rc) return rc;
+  HIPCHK(gpk_launch_decode(&P, (p->outputs & GPK_OUT_L4_CSUM) != 0, 0, s));
   return note_launch(c, slot, s);
 }
 

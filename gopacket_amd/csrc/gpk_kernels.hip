@@ -1294,8 +1294,21 @@ __device__ __forceinline__ void decode_packet(const KParams& P, const TT& T, uin
       if (l4c == jexist || (udp && jexist == 0)) st |= GPK_ST_L4_VALID;
     }
   }
-  if (active)  // written once, never read back here: non-temporal
+  if (active && P.narrow) {
+    // gpk_record8 (gpk.h): the full record only where Correct is not the
+    // header's Checksum field (checksum.go:9-21; a UDP 0 is Valid unchecked,
+    // udp.go:144-158) or the list has more than 8 entries
+    const bool widen = q.nlayers > 8 || ((st & GPK_ST_IP4_CSUM) && !(st & GPK_ST_IP4_VALID)) ||
+                       ((st & GPK_ST_L4_CSUM) && l4c != jexist);
+    const uint32_t st8 = (st & ~(GPK_ST_NLAYERS_MASK << GPK_ST_NLAYERS_SHIFT)) |
+                         ((q.nlayers > 8 ? GPK_ST8_NLAYERS_MASK : q.nlayers) << GPK_ST_NLAYERS_SHIFT) |
+                         (widen ? GPK_ST8_WIDE : 0u);
+    __builtin_nontemporal_store((uint64_t)st8 << 32 | lay_lo, reinterpret_cast<uint64_t*>(P.records) + i);
+    if (widen)
+      __builtin_nontemporal_store(u32x4{lay_lo, lay_hi, st, ip4c | (l4c << 16)}, reinterpret_cast<u32x4*>(P.wide) + i);
+  } else if (active) {  // written once, never read back here: non-temporal
     __builtin_nontemporal_store(u32x4{lay_lo, lay_hi, st, ip4c | (l4c << 16)}, reinterpret_cast<u32x4*>(P.records) + i);
+  }
 }
 
 // kCompact: the parser's lookup tables are copied into LDS once per block

@@ -121,6 +121,20 @@ class Context:
                          layouts.data_ptr() if layouts is not None else None)
         check(lib().gpk_decode_batch(self.h, parser.h, ctypes.byref(b), ctypes.byref(r), _stream_ptr(stream)))
 
+    def decode_device_narrow(self, parser, data, offsets, caplens, records8, wide, err_args=None, flows=None,
+                             stream=None):
+        """gpk_decode_batch_narrow: decode_device with the 8-byte record
+        (records8: 8 bytes per packet, RECORD8_DTYPE) and the side array of full
+        records (wide: 16 bytes per packet, written only where a record8 has
+        ST8_WIDE). Device tensors; enqueued on `stream`."""
+        n = offsets.numel()
+        if records8.numel() * records8.element_size() < 8 * n or wide.numel() * wide.element_size() < 16 * n:
+            raise ValueError("records8 needs 8 and wide 16 bytes per packet")
+        b = _lib.Batch(data.data_ptr(), offsets.data_ptr(), caplens.data_ptr(), n, data.numel())
+        r = _lib.Results8(records8.data_ptr(), wide.data_ptr(), err_args.data_ptr() if err_args is not None else None,
+                          flows.data_ptr() if flows is not None else None)
+        check(lib().gpk_decode_batch_narrow(self.h, parser.h, ctypes.byref(b), ctypes.byref(r), _stream_ptr(stream)))
+
     def extract_fields(self, data, offsets, caplens, layouts, fields, stream=None):
         """gpk_extract_fields: the layer fields (include/gpk.h gpk_fields, 128
         bytes per packet; FIELDS_DTYPE) of a device batch from the layouts a

@@ -30,6 +30,8 @@
  *                                          layers/udp.go:132)
  *   gpk_decode_batch_host                  the same, starting and ending in host memory
  *                                          (pcap/afpacket sources hand over host buffers)
+ *   gpk_decode_batch_narrow                gpk_decode_batch with an 8-byte record per packet (the
+ *                                          full one only where it does not fit, gpk_record8)
  *   gpk_decode_batch_fields                gpk_decode_batch plus gpk_extract_fields in one launch
  *   gpk_extract_fields                     the scalar fields the six decoders' DecodeFromBytes set
  *                                          on their structs (layers/ethernet.go:42-55,
@@ -191,6 +193,39 @@ static inline unsigned gpk_record_nlayers(const gpk_record* r) {
   return (r->status >> GPK_ST_NLAYERS_SHIFT) & GPK_ST_NLAYERS_MASK;
 }
 
+/* ---- narrow per-packet result record (8 B, gpk_decode_batch_narrow) --------
+ * The same result in half the bytes, for the batches whose cost is the bytes a
+ * decode writes (small packets: the 16-byte record is a fifth of C2's memory
+ * traffic). ChecksumVerificationResult.Correct equals Actual whenever it is
+ * Valid (checksum.go:9-21), except for a UDP checksum of 0, which is Valid
+ * unchecked (udp.go:144-158); so the narrow record keeps the status bits and
+ * the first 8 codes of the decoded list, and a packet whose record does not
+ * fit (more than 8 layers, or an IPv4 / TCP / UDP Correct that differs from the
+ * header's Checksum field) has GPK_ST8_WIDE set and its full gpk_record in
+ * the side array wide[i], which is written for those packets only (as
+ * err_args is written only on error). For a packet without GPK_ST8_WIDE the
+ * gpk_record is {layers, status with nlayers, ip4_csum = the IPv4 Checksum
+ * field when GPK_ST_IP4_CSUM (else 0), l4_csum = the TCP / UDP Checksum field
+ * when GPK_ST_L4_CSUM (else 0)}: the fields of the layer structs DecodeLayers
+ * filled (the last IPv4, the transport layer). */
+typedef struct gpk_record8 {
+  uint32_t layers;   /* decoded list, 4-bit GPK_CODE_* per entry (first 8)                    */
+  uint32_t status;   /* the GPK_ST_* bits, with len(decoded) in 4 bits and GPK_ST8_WIDE below */
+} gpk_record8;
+#define GPK_ST8_NLAYERS_MASK 0xFu /* at GPK_ST_NLAYERS_SHIFT: len(decoded), 15 when more than 8 */
+#define GPK_ST8_WIDE (1u << 12)   /* the packet's full gpk_record is in wide[i]                 */
+
+typedef struct gpk_results8 {
+  gpk_record8* records; /* [n]   required                                                 */
+  gpk_record* wide;     /* [n]   required; written only where GPK_ST8_WIDE is set           */
+  uint32_t* err_args;   /* [2n]  optional; written only for packets with err                */
+  uint64_t* flows;      /* [3n]  as gpk_results.flows; required if GPK_OUT_FLOWS            */
+} gpk_results8;
+
+static inline unsigned gpk_record8_nlayers(const gpk_record8* r) {
+  return (r->status >> GPK_ST_NLAYERS_SHIFT) & GPK_ST8_NLAYERS_MASK;
+}
+
 /* ---- optional per-packet layout (64 B): where each layer struct points ----
  * For every DecodingLayer implementation (slot = kind-1, Payload and Fragment
  * share slot 7) the byte range [start, end) — relative to the packet start —
@@ -224,7 +259,7 @@ typedef struct gpk_fields {
   uint8_t hbh_opt_map[3];    /*   1 IPv6.HopByHop.Options (the last IPv6's inline HopByHop,
                                     ip6.go:244-256, 509-526): bit k (byte k/8, bit k%8) set =
                                     an option starts at HopByHop byte 2 + k; covers headers of
-                                    up to 26 bytes (HeaderLength <= 2), 0 for longer ones     */
+                                    up to 24 bytes (HeaderLength <= 2), 0 for longer ones     */
   uint16_t eth_type;         /*   4 Ethernet.EthernetType (EthernetTypeLLC = 0 below 0x0600) */
   uint16_t eth_length;       /*   6 Ethernet.Length (802.3 frames, else 0)               */
   uint8_t eth_dst[6];        /*   8 Ethernet.DstMAC                                       */
@@ -366,6 +401,12 @@ typedef struct gpk_results {
  * launch. The parser configuration is uploaded once per (ctx, parser change). */
 int gpk_decode_batch(gpk_ctx* ctx, const gpk_parser* p, const gpk_batch* batch,
                      const gpk_results* out, void* stream);
+
+/* gpk_decode_batch with the narrow 8-byte record (gpk_record8 above) and its
+ * side array of full records; device memory, same stream semantics. No
+ * layouts. The results are exactly gpk_decode_batch's, in the narrow form. */
+int gpk_decode_batch_narrow(gpk_ctx* ctx, const gpk_parser* p, const gpk_batch* batch,
+                            const gpk_results8* out, void* stream);
 
 /* Layer fields of every packet of a device batch from the layouts a
  * gpk_decode_batch with layouts wrote for it (device memory; fields[n] device

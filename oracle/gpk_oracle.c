@@ -687,7 +687,7 @@ static uint32_t pseudo_sum(const pkt_state* s) {
 
 static void decode_packet(const oracle_config* c, const uint8_t* pkt, uint32_t caplen, gpk_record* rec,
                           uint32_t* err_args, uint64_t* fl_link, uint64_t* fl_net, uint64_t* fl_tr,
-                          gpk_layout* lay) {
+                          gpk_layout* lay, uint16_t* actual) {
   pkt_state s;
   memset(&s, 0, sizeof(s));
   s.b = pkt;
@@ -710,6 +710,7 @@ static void decode_packet(const oracle_config* c, const uint8_t* pkt, uint32_t c
     uint16_t existing = be16(d + 10);
     uint32_t v = oracle_compute_checksum(d, ihl * 4, 0);
     ip4c = oracle_fold_checksum(v - (uint32_t)existing);
+    if (actual) actual[0] = existing; /* IPv4.Checksum, ChecksumVerificationResult.Actual */
     st |= GPK_ST_IP4_CSUM;
     if (ip4c == existing) st |= GPK_ST_IP4_VALID;
   }
@@ -727,6 +728,7 @@ static void decode_packet(const oracle_config* c, const uint8_t* pkt, uint32_t c
     csum += blen >> 16;
     csum = oracle_compute_checksum(d, blen, csum);
     l4c = oracle_fold_checksum(csum - (uint32_t)existing);
+    if (actual) actual[1] = existing; /* TCP/UDP.Checksum */
     st |= GPK_ST_L4_CSUM;
     if (s.transport == GPK_DEC_UDP) {
       st |= GPK_ST_L4_UDP;
@@ -914,15 +916,33 @@ typedef struct {
   uint32_t* err_args;
   uint64_t* flows;
   gpk_layout* layouts;
+  gpk_record8* narrow; /* non-NULL: the narrow form (records then holds the side array) */
 } work_t;
+
+/* gpk_record8 of a decoded packet (include/gpk.h): the full record goes to the
+ * side array only where Correct differs from the header's Checksum field
+ * (Actual; checksum.go:9-21, udp.go:144-158) or the list has more than 8
+ * entries. */
+static void narrow_record(const gpk_record* r, const uint16_t actual[2], gpk_record8* r8, gpk_record* wide) {
+  const uint32_t st = r->status, nl = (st >> GPK_ST_NLAYERS_SHIFT) & GPK_ST_NLAYERS_MASK;
+  const int widen = nl > 8 || ((st & GPK_ST_IP4_CSUM) && r->ip4_csum != actual[0]) ||
+                    ((st & GPK_ST_L4_CSUM) && r->l4_csum != actual[1]);
+  r8->layers = (uint32_t)r->layers;
+  r8->status = (st & ~(GPK_ST_NLAYERS_MASK << GPK_ST_NLAYERS_SHIFT)) |
+               ((nl > 8 ? GPK_ST8_NLAYERS_MASK : nl) << GPK_ST_NLAYERS_SHIFT) | (widen ? GPK_ST8_WIDE : 0u);
+  if (widen) *wide = *r;
+}
 
 static void* worker(void* arg) {
   work_t* w = (work_t*)arg;
   for (uint64_t i = w->lo; i < w->hi; i++) {
     uint64_t* fl = w->flows;
-    decode_packet(w->c, w->data + w->offsets[i], w->caplens[i], &w->records[i],
+    gpk_record rec;
+    uint16_t actual[2] = {0, 0};
+    decode_packet(w->c, w->data + w->offsets[i], w->caplens[i], w->narrow ? &rec : &w->records[i],
                   w->err_args ? w->err_args + 2 * i : NULL, fl ? fl + i : NULL, fl ? fl + w->n + i : NULL,
-                  fl ? fl + 2 * w->n + i : NULL, w->layouts ? w->layouts + i : NULL);
+                  fl ? fl + 2 * w->n + i : NULL, w->layouts ? w->layouts + i : NULL, actual);
+    if (w->narrow) narrow_record(&rec, actual, &w->narrow[i], &w->records[i]);
   }
   return NULL;
 }
@@ -936,7 +956,28 @@ void oracle_decode_batch(const oracle_config* c, const uint8_t* data, const uint
   pthread_t th[256];
   for (int t = 0; t < nthreads; t++) {
     w[t] = (work_t){c, data, offsets, caplens, n, n * t / nthreads, n * (t + 1) / nthreads,
-                    records, err_args, flows, layouts};
+                    records, err_args, flows, layouts, NULL};
+  }
+  if (nthreads == 1) {
+    worker(&w[0]);
+    return;
+  }
+  for (int t = 0; t < nthreads; t++) pthread_create(&th[t], NULL, worker, &w[t]);
+  for (int t = 0; t < nthreads; t++) pthread_join(th[t], NULL);
+}
+
+/* The same decode in the narrow form of gpk_decode_batch_narrow: records8[n],
+ * and wide[i] written only for the packets whose record8 has GPK_ST8_WIDE. */
+void oracle_decode_batch_narrow(const oracle_config* c, const uint8_t* data, const uint64_t* offsets,
+                                const uint32_t* caplens, uint64_t n, gpk_record8* records8, gpk_record* wide,
+                                uint32_t* err_args, uint64_t* flows, int nthreads) {
+  if (nthreads < 1) nthreads = 1;
+  if (nthreads > 256) nthreads = 256;
+  work_t w[256];
+  pthread_t th[256];
+  for (int t = 0; t < nthreads; t++) {
+    w[t] = (work_t){c, data, offsets, caplens, n, n * t / nthreads, n * (t + 1) / nthreads,
+                    wide, err_args, flows, NULL, records8};
   }
   if (nthreads == 1) {
     worker(&w[0]);

@@ -14,6 +14,7 @@ _LIB = None
 
 RECORD_DTYPE = np.dtype([("layers", "<u8"), ("status", "<u4"), ("ip4_csum", "<u2"), ("l4_csum", "<u2")])
 LAYOUT_DTYPE = np.dtype([("start", "<u4", (8,)), ("end", "<u4", (8,))])
+RECORD8_DTYPE = np.dtype([("layers", "<u4"), ("status", "<u4")])  # include/gpk.h gpk_record8
 
 FIELDS_ITEMSIZE = 128  # include/gpk.h gpk_fields
 
@@ -38,6 +39,9 @@ def lib():
         L.oracle_decode_batch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                           ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
                                           ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+        L.oracle_decode_batch_narrow.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                                 ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                                 ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
         L.oracle_decoded_list.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
                                           ctypes.c_void_p, ctypes.c_uint32]
         L.oracle_decoded_list.restype = ctypes.c_uint32
@@ -92,6 +96,24 @@ class OracleParser:
                               rec.ctypes.data, err.ctypes.data, flows.ctypes.data,
                               lay.ctypes.data if layouts else None, int(nthreads))
         return dict(records=rec, err_args=err, flows=flows, layouts=lay)
+
+    def decode_narrow(self, data, offsets, caplens, nthreads=1):
+        """The narrow form (gpk_decode_batch_narrow): records8 (RECORD8_DTYPE)
+        and the side array wide (RECORD_DTYPE, zero except where a record8 has
+        GPK_ST8_WIDE), err_args, flows."""
+        L = lib()
+        data = np.ascontiguousarray(data, dtype=np.uint8)
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        caplens = np.ascontiguousarray(caplens, dtype=np.uint32)
+        n = len(offsets)
+        rec8 = np.zeros(n, RECORD8_DTYPE)
+        wide = np.zeros(n, RECORD_DTYPE)
+        err = np.zeros(2 * n, np.uint32)
+        flows = np.zeros(3 * n, np.uint64)
+        L.oracle_decode_batch_narrow(self.ptr, data.ctypes.data, offsets.ctypes.data, caplens.ctypes.data, n,
+                                     rec8.ctypes.data, wide.ctypes.data, err.ctypes.data, flows.ctypes.data,
+                                     int(nthreads))
+        return dict(records8=rec8, wide=wide, err_args=err, flows=flows)
 
     def decoded_list(self, pkt):
         L = lib()

@@ -19,6 +19,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 STRUCTS = {  # C type -> Python mirror
     "gpk_batch": _lib.Batch,
     "gpk_results": _lib.Results,
+    "gpk_results8": _lib.Results8,
+    "gpk_replay_range": _lib.ReplayRange,
     "gpk_groups": _lib.Groups,
     "gpk_tp_opts": _lib.TpOpts,
     "gpk_tp_pump_opts": _lib.PumpOpts,
@@ -28,6 +30,7 @@ STRUCTS = {  # C type -> Python mirror
     "gpk_replay_opts": _lib.ReplayOpts,
     "gpk_replay_stats": _lib.ReplayStats,
     "gpk_record": _lib.RECORD_DTYPE,
+    "gpk_record8": _lib.RECORD8_DTYPE,
     "gpk_layout": _lib.LAYOUT_DTYPE,
     "gpk_fields": _lib.FIELDS_DTYPE,
     "gpk_bpf_insn": _lib.BPF_INSN_DTYPE,

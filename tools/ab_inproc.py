@@ -7,7 +7,10 @@ in interleaved rounds so clocks and thermals affect them alike.
     python tools/ab_inproc.py --configs c3,c2,c4 --rounds 5 --steps 5 base w6 w7 ...
 
 "base" = gopacket_amd/libgpk.so, NAME = gopacket_amd/build/libgpk_NAME.so;
-NAME@global runs that library with gpk_ctx_set_table_mode(GPK_TABLES_GLOBAL).
+NAME@global runs that library with gpk_ctx_set_table_mode(GPK_TABLES_GLOBAL);
+NAME@narrow runs gpk_decode_batch_narrow (the 8-byte record and its side array)
+instead of gpk_decode_batch, and --check compares it with a 16-byte variant by
+the gpk_record8 rules (include/gpk.h).
 --fields times gpk_decode_batch_fields (the fused decode + layer fields launch)
 instead of gpk_decode_batch. --check compares every variant's records, error
 arguments and flows (and fields) with the first variant's, bit for bit.
@@ -34,7 +37,25 @@ def load(name):
     L.gpk_decode_batch.argtypes = [vp, vp, vp, vp, vp]
     if hasattr(L, "gpk_decode_batch_fields"):
         L.gpk_decode_batch_fields.argtypes = [vp, vp, vp, vp, vp, vp]
+    if hasattr(L, "gpk_decode_batch_narrow"):
+        L.gpk_decode_batch_narrow.argtypes = [vp, vp, vp, vp, vp]
     return L
+
+
+def narrow_matches(rec16, rec8, wide, n):
+    """gpk_record8 rules: a widened packet's side record is the 16-byte record;
+    every other packet's layers and status bits (nlayers in 4 bits) are."""
+    import numpy as np
+    from gopacket_amd import _lib
+    r = rec16.cpu().numpy().view(_lib.RECORD_DTYPE)
+    r8 = rec8.cpu().numpy().view(_lib.RECORD8_DTYPE)
+    w8 = wide.cpu().numpy().view(_lib.RECORD_DTYPE)
+    w = (r8["status"] & _lib.ST8_WIDE) != 0
+    nl = (r["status"] >> 8) & 0xFFF
+    keep = ~np.uint32(0xFFF << 8)
+    return bool(np.array_equal(w8[w], r[w]) and np.array_equal(r8["layers"][~w].astype(np.uint64), r["layers"][~w])
+                and np.array_equal(r8["status"][~w] & keep, r["status"][~w] & keep)
+                and np.array_equal((r8["status"] >> 8) & 0xF, np.where(nl > 8, 15, nl).astype(np.uint32)))
 
 
 def main():
@@ -52,6 +73,7 @@ def main():
     import bench
     from gopacket_amd import _lib, engine, synth
     libs = {v: load(v.split("@")[0]) for v in a.variants}
+    narrow = {v: v.endswith("@narrow") for v in a.variants}
     stream = torch.cuda.current_stream()
     for name in a.configs.split(","):
         cfg = bench.CONFIGS[name]
@@ -67,6 +89,18 @@ def main():
         fields = torch.empty(n * 128 if a.fields else 16, dtype=torch.uint8, device="cuda")
         b = _lib.Batch(data.data_ptr(), off.data_ptr(), cap.data_ptr(), n, data.numel())
         r = _lib.Results(rec.data_ptr(), err.data_ptr(), fl.data_ptr(), None)
+        rec8 = torch.empty(n * 8 if any(narrow.values()) else 8, dtype=torch.uint8, device="cuda")
+        wide = torch.zeros(n * 16 if any(narrow.values()) else 16, dtype=torch.uint8, device="cuda")
+        r8 = _lib.Results8(rec8.data_ptr(), wide.data_ptr(), err.data_ptr(), fl.data_ptr())
+
+        def run(v, L, ctx, p):
+            if narrow[v]:
+                return L.gpk_decode_batch_narrow(ctx, p, ctypes.byref(b), ctypes.byref(r8),
+                                                 ctypes.c_void_p(stream.cuda_stream))
+            if a.fields:
+                return L.gpk_decode_batch_fields(ctx, p, ctypes.byref(b), ctypes.byref(r),
+                                                 ctypes.c_void_p(fields.data_ptr()), ctypes.c_void_p(stream.cuda_stream))
+            return L.gpk_decode_batch(ctx, p, ctypes.byref(b), ctypes.byref(r), ctypes.c_void_p(stream.cuda_stream))
         handles = {}
         for v, L in libs.items():
             ctx, p = ctypes.c_void_p(), ctypes.c_void_p()
@@ -96,14 +130,7 @@ def main():
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record(stream)
                 for _ in range(a.steps):
-                    if a.fields:
-                        rc = L.gpk_decode_batch_fields(ctx, p, ctypes.byref(b), ctypes.byref(r),
-                                                       ctypes.c_void_p(fields.data_ptr()),
-                                                       ctypes.c_void_p(stream.cuda_stream))
-                    else:
-                        rc = L.gpk_decode_batch(ctx, p, ctypes.byref(b), ctypes.byref(r),
-                                                ctypes.c_void_p(stream.cuda_stream))
-                    assert rc == 0
+                    assert run(v, L, ctx, p) == 0
                 e1.record(stream)
                 torch.cuda.synchronize()
                 if rnd:  # round 0 warms every variant up
@@ -121,21 +148,23 @@ def main():
                 err.fill_(-1)
                 fl.fill_(-1)
                 fields.fill_(0x5A)
-                if a.fields:
-                    rc = L.gpk_decode_batch_fields(ctx, p, ctypes.byref(b), ctypes.byref(r),
-                                                   ctypes.c_void_p(fields.data_ptr()), ctypes.c_void_p(stream.cuda_stream))
-                else:
-                    rc = L.gpk_decode_batch(ctx, p, ctypes.byref(b), ctypes.byref(r), ctypes.c_void_p(stream.cuda_stream))
-                assert rc == 0
+                wide.zero_()
+                assert run(v, L, ctx, p) == 0
                 torch.cuda.synchronize()
                 out = [x.clone() for x in (rec, err, fl, fields)]
+                if narrow[v]:  # the 16-byte records this narrow result stands for, where it can say them
+                    out[0] = (rec8.clone(), wide.clone())
                 if ref is None:
                     ref = out
                     continue
-                same = all(torch.equal(x, y) for x, y in zip(ref, out))
+                if narrow[v]:
+                    same = all(torch.equal(x, y) for x, y in zip(ref[1:3], out[1:3])) and \
+                        narrow_matches(ref[0], *out[0], n)
+                else:
+                    same = all(torch.equal(x, y) for x, y in zip(ref, out))
                 print("%-4s %-10s outputs %s the first variant's" % (name, v, "equal" if same else "DIFFER from"), flush=True)
             del ref, out
-        del data, off, cap, rec, err, fl, fields
+        del data, off, cap, rec, err, fl, fields, rec8, wide
         torch.cuda.empty_cache()
 
 
