@@ -59,8 +59,9 @@ class ParserConfig:
 
     def __del__(self):
         h = getattr(self, "h", None)
-        if h and _lib._lib is not None:
-            _lib._lib.gpk_parser_destroy(h)
+        L = getattr(_lib, "_lib", None) if _lib is not None else None  # module globals are None at exit
+        if h and L is not None:
+            L.gpk_parser_destroy(h)
             self.h = None
 
 
