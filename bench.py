@@ -212,7 +212,8 @@ def probe_read(data, nbytes, steps, stream):
     return (nbytes & ~15) / (e0.elapsed_time(e1) / steps * 1e-3) / 1e9
 
 
-def run_config(name, n, steps, warmup, rank, world, ctx, check_sample=2048, probe=False, full_check=False):
+def run_config(name, n, steps, warmup, rank, world, ctx, check_sample=2048, probe=False, full_check=False,
+               narrow=True):
     import torch
     from gopacket_amd import engine, shard, synth
     cfg = CONFIGS[name]
@@ -277,6 +278,30 @@ def run_config(name, n, steps, warmup, rank, world, ctx, check_sample=2048, prob
     kernel_ms = shard.max_over_ranks(kernel_ms_own, world, device="cuda")
     kernel_ms_ranks = gather_ranks(kernel_ms_own, world)
 
+    # the same decode with the 8-byte record (gpk_decode_batch_narrow, include/gpk.h gpk_record8), timed
+    # the same way on its own outputs; the every-packet check below covers both forms
+    nar = None
+    if narrow:
+        rec8 = torch.empty(n * 8, dtype=torch.uint8, device="cuda")
+        wide = torch.zeros(n * 16, dtype=torch.uint8, device="cuda")
+        err8 = torch.zeros(2 * n, dtype=torch.int32, device="cuda")
+        fl8 = torch.empty(3 * n, dtype=torch.int64, device="cuda") if fl is not None else None
+
+        def nstep():
+            ctx.decode_device_narrow(parser, data, off, cap, rec8, wide, err8, fl8, stream=stream)
+
+        for _ in range(max(warmup, 2)):
+            nstep()
+        barrier(world)
+        n0, n1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        n0.record(stream)
+        for _ in range(steps):
+            nstep()
+        n1.record(stream)
+        barrier(world)
+        nk = shard.max_over_ranks(n0.elapsed_time(n1) / steps, world, device="cuda")
+        nar = dict(kernel_ms=nk, buffers=(rec8, wide, err8, fl8))
+
     probe_gbs = probe_read(data, payload_bytes, steps, stream) if probe else None
     skel_ms = skeleton_ms(cfg, data, off, cap, n, steps, stream) if probe and not strong else None
     parity = None
@@ -288,7 +313,8 @@ def run_config(name, n, steps, warmup, rank, world, ctx, check_sample=2048, prob
                       else "MISMATCH on a rank: ") + "; ".join("rank %d %s" % (k, p) for k, p in enumerate(every))
     full = None
     if full_check:
-        full, full_s = full_parity(name, cfg, data, off, cap, rec, fl, err, n, rank_threads())
+        full, full_s = full_parity(name, cfg, data, off, cap, rec, fl, err, n, rank_threads(),
+                                   narrow=nar["buffers"] if nar else None)
         full = dict(result=full, seconds=round(full_s, 2), threads=rank_threads())
         if world > 1:  # every rank checks its own shard; the line carries each rank's result
             full = dict(ranks=gather_obj(dict(full, rank=rank, first_packet=first, packets=n), world),
@@ -297,12 +323,16 @@ def run_config(name, n, steps, warmup, rank, world, ctx, check_sample=2048, prob
             full["result"] = ("bit-exact on every rank (%d ranks, %d packets)" % (world, sum(
                 x["packets"] for x in full["ranks"]))) if not bad else "MISMATCH on rank(s) %s" % [x["rank"] for x in bad]
             full["seconds"] = max(x["seconds"] for x in full["ranks"])
-    res = dict(full_parity=full, n=n, payload_bytes=payload_bytes, wall_s=wall_max, kernel_ms=kernel_ms,
+    if nar:
+        nar.pop("buffers")
+    res = dict(full_parity=full, n=n, payload_bytes=payload_bytes, wall_s=wall_max, kernel_ms=kernel_ms, narrow=nar,
                kernel_ms_ranks=kernel_ms_ranks,
                algo_bytes=payload_bytes + INDEX_BYTES * n, parity=parity, probe_gbs=probe_gbs, skeleton_ms=skel_ms,
                strong=strong,
                kernel=kernel, blocks_per_cu=blocks_per_cu)
     del data, off, cap, rec, err, fl
+    if narrow:
+        del rec8, wide, err8, fl8
     torch.cuda.empty_cache()
     return res
 
@@ -400,11 +430,14 @@ def sample_parity(name, cfg, rec, fl, err, first, n, k):
     return "%s (%d sampled packets vs oracle)" % ("bit-exact" if ok else "MISMATCH", len(idx))
 
 
-def full_parity(name, cfg, data, off, cap, rec, fl, err, n, threads, chunk=1 << 20):
+def full_parity(name, cfg, data, off, cap, rec, fl, err, n, threads, chunk=1 << 20, narrow=None):
     """Every packet of the device batch against the CPU oracle (SURVEY.md §8c
     at full size): chunks of the batch's own bytes and index are copied back,
     decoded by oracle/gpk_oracle.c on `threads` host threads, and the records,
     error arguments and flows compared bit for bit with the device outputs.
+    narrow=(records8, wide, err_args, flows) of gpk_decode_batch_narrow on the
+    same batch: checked in the same pass against the oracle's narrow form
+    (every record8 and the whole side array, zero where no record widened).
     Returns (summary string, seconds)."""
     from gopacket_amd import _lib
     from oracle import oracle as O
@@ -431,6 +464,19 @@ def full_parity(name, cfg, data, off, cap, rec, fl, err, n, threads, chunk=1 << 
             rf = ref["flows"].reshape(3, -1)
             for k in range(3):
                 ok &= fl[k * n + a:k * n + b].cpu().numpy().view(np.uint64) == rf[k]
+        if narrow is not None:
+            r8, w8, e8, f8 = narrow
+            rn = p.decode_narrow(host, o - np.uint64(lo), c, nthreads=threads)
+            g8 = r8[a * 8:b * 8].cpu().numpy().view(np.uint64)
+            ok &= g8 == rn["records8"].view(np.uint64)
+            gw = w8[a * 16:b * 16].cpu().numpy().view(np.uint64).reshape(-1, 2)
+            ok &= (gw == rn["wide"].view(np.uint64).reshape(-1, 2)).all(axis=1)
+            ok &= (e8[2 * a:2 * b].cpu().numpy().view(np.uint32).reshape(-1, 2) ==
+                   rn["err_args"].reshape(-1, 2)).all(axis=1)
+            if f8 is not None:
+                rf = rn["flows"].reshape(3, -1)
+                for k in range(3):
+                    ok &= f8[k * n + a:k * n + b].cpu().numpy().view(np.uint64) == rf[k]
         nb = int((~ok).sum())
         if nb and first_bad is None:
             first_bad = a + int(np.argmin(ok))
@@ -438,8 +484,10 @@ def full_parity(name, cfg, data, off, cap, rec, fl, err, n, threads, chunk=1 << 
     secs = time.perf_counter() - t0
     if bad:
         return "MISMATCH (%d of %d packets differ from the oracle, first at %d)" % (bad, n, first_bad), secs
-    return "bit-exact (all %d packets vs oracle: records, error arguments%s)" % (
-        n, ", flows" if fl is not None else ""), secs
+    return "bit-exact (all %d packets vs oracle: records, error arguments%s%s)" % (
+        n, ", flows" if fl is not None else "",
+        "; and the narrow form: records8, side array, error arguments%s" % (", flows" if fl is not None else "")
+        if narrow is not None else ""), secs
 
 
 def host_cores():
@@ -1213,6 +1261,25 @@ def c5_sharded(ctx, rank, world, gib=10.0, reps=2, threads=8):
                 ranks=ranks, source="page-cached file in %s" % os.path.dirname(path))
 
 
+def narrow_row(r, world):
+    """The config's decode with the 8-byte record (gpk_decode_batch_narrow),
+    timed beside the 16-byte one on the same batch: kernel time (the slowest
+    rank's), rate by kernel time, HBM fraction of the same algorithmic bytes,
+    and the 16-byte kernel's time over it. Its every-packet parity is in the
+    config's full_parity."""
+    nr = r.get("narrow")
+    if not nr:
+        return None
+    k = nr["kernel_ms"]
+    pk = r["strong"]["total_packets"] if r.get("strong") else r["n"] * world
+    ach = r["algo_bytes"] / (k * 1e-3) / 1e9
+    return dict(kernel_ms=round(k, 4), value_by_kernel=round(pk / k / 1e3, 2), unit="Mpkts/s",
+                achieved_GBps=round(ach, 1), frac=round(ach / HBM_PEAK_GBS, 4),
+                speedup_vs_16B=round(r["kernel_ms"] / k, 4),
+                record="gpk_record8: 8 B per packet, the full 16 B record in a side array only where it does not "
+                       "fit (Correct != the header Checksum, or more than 8 layers)")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -1305,6 +1372,7 @@ def main():
                          "of_skeleton": r["skeleton_ms"] and round(r["skeleton_ms"] / r["kernel_ms"], 4)},
             "parity": r["parity"],
             "full_parity": r["full_parity"],
+            "narrow": narrow_row(r, world),
             "dist_backend": dist.get_backend() if dist.is_initialized() else None,
             "configs": {},
         }
@@ -1320,7 +1388,8 @@ def main():
                    "frac": round(ach / HBM_PEAK_GBS, 4), "parity": s["parity"], "full_parity": s["full_parity"],
                    "probe_read_GBps": s["probe_gbs"] and round(s["probe_gbs"], 1),
                    "skeleton_ms": s["skeleton_ms"] and round(s["skeleton_ms"], 4),
-                   "of_skeleton": s["skeleton_ms"] and round(s["skeleton_ms"] / s["kernel_ms"], 4)}
+                   "of_skeleton": s["skeleton_ms"] and round(s["skeleton_ms"] / s["kernel_ms"], 4),
+                   "narrow": narrow_row(s, world)}
             if st:
                 row.update(scaling="strong", total_packets=st["total_packets"], byte_balance=st["balance"],
                            note="one batch split at byte-balanced cuts; kernel_ms/achieved: the slowest rank's "

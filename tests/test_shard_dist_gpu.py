@@ -132,6 +132,8 @@ def test_bench_two_ranks_strong_and_weak():
         assert row["result"].startswith("bit-exact on every rank (2 ranks"), row
         assert [x["rank"] for x in row["ranks"]] == [0, 1]
         assert all(x["result"].startswith("bit-exact (all %d packets" % x["packets"]) for x in row["ranks"]), row
+        assert all("and the narrow form" in x["result"] for x in row["ranks"]), row
+    assert r["narrow"]["kernel_ms"] > 0 and c["narrow"]["kernel_ms"] > 0
     assert sum(x["packets"] for x in c["full_parity"]["ranks"]) == 1 << 20
     assert [x["first_packet"] for x in r["full_parity"]["ranks"]] == [0, 1 << 20]
     f = r["fields"]
