@@ -785,12 +785,27 @@ def c5_replay(ctx, gib=10.0, reps=2, threads=8, cpu_threads=16):
         ok = st["packets"] == n and len(idx) == len(sample) and np.array_equal(got, want)
         return "%s (%d sampled packets' fields vs oracle)" % ("bit-exact" if ok else "MISMATCH", len(idx))
 
+    seen_bytes = [0]
+
+    def on_batch_packets(first, k, rec, err, fl, ci, cap, pk):
+        seen_bytes[0] += int(pk[2].sum(dtype=np.uint64))  # the packets' bytes, handed out in place
+
+    def replay_packets(p):  # gpk_replay_opts.packets_cb: the packets' staging bytes with each launch's results
+        rs = []
+        for _ in range(reps):
+            seen_bytes[0] = 0
+            _, r = ctx.replay_file(p, path, collect=False, on_batch=on_batch_packets, read_threads=threads,
+                                   packets=True)
+            rs.append(r)
+        return rs
+
     cpu = None
     c1 = None
     try:
         runs, got4 = replay(parser)
         valid4 = valid[0]
         runsf, gotf = replay_fields(parser)
+        runsp = replay_packets(parser)
         # the same file through C1's parser (Ethernet/IPv4/TCP/Payload, IPv4+TCP checksums): the
         # small-packet dword-aligned kernel on replay batches
         c1cfg = CONFIGS["c1"]
@@ -816,6 +831,14 @@ def c5_replay(ctx, gib=10.0, reps=2, threads=8, cpu_threads=16):
                   GBps=round(stf["file_bytes"] / stf["wall_s"] / 1e9, 2), wall_s=round(stf["wall_s"], 4),
                   runs_wall_s=[round(r["wall_s"], 4) for r in runsf], kernel=stf["kernel"],
                   kernel_s=round(stf["kernel_s"], 4), parity=check_fields(stf, gotf))
+    stp = min(runsp, key=lambda x: x["wall_s"])
+    packets_row = dict(what="the same replay with gpk_replay_opts.packets_cb: each launch's packets handed out in "
+                            "their staging bytes with its results (a staging slot is refilled only after its "
+                            "packets were delivered)",
+                       value=round(stp["packets"] / stp["wall_s"] / 1e6, 2), unit="Mpkts/s",
+                       GBps=round(stp["file_bytes"] / stp["wall_s"] / 1e9, 2), wall_s=round(stp["wall_s"], 4),
+                       runs_wall_s=[round(r["wall_s"], 4) for r in runsp],
+                       packets_ok=stp["packets"] == n and seen_bytes[0] == stp["packet_bytes"])
     w = st["wall_s"]
     w0 = runs[0]["wall_s"]
     return dict(workload="C5: pcapng replay of the C4 IMIX mix, end to end incl. HtoD/DtoH",
@@ -832,7 +855,7 @@ def c5_replay(ctx, gib=10.0, reps=2, threads=8, cpu_threads=16):
                 batches=st["batches"], slots=st["slots"], l4_valid=valid4, write_s=round(gen_s, 2),
                 kernel=st["kernel"], **probe,
                 frac_of_htod_probe=round(st["file_bytes"] / w / 1e9 / probe["htod_probe_GBps"], 4),
-                parity=parity, c1_parser=c1, fields=fields,
+                parity=parity, c1_parser=c1, fields=fields, packets=packets_row,
                 source="page-cached file in %s" % os.path.dirname(path), cpu_baseline=cpu)
 
 

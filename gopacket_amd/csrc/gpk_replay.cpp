@@ -813,7 +813,10 @@ static int replay_file(gpk_ctx* ctx, const gpk_parser* parser, const char* path,
     stats->stream_bytes += fresh;
     // read ahead into every slot whose carry has moved on (the one just
     // taken from slot si - 1 included)
-    if (!eof) fill_ahead(si + pl.slots.size());
+    // (with packets_cb the slot refilled next is the previous one, whose packets
+    // are handed out with its batches' results: refilled after this slot's
+    // batches are launched, so waiting for that delivery overlaps them)
+    if (!eof && !pl.packets_cb) fill_ahead(si + pl.slots.size());
     // walk the records of [start, start+len): on the device once the reader
     // is open (gpk_walk.h), the rest (and everything before) on the host
     // (parallel, gpk_capreader_index_all)
@@ -1069,6 +1072,7 @@ static int replay_file(gpk_ctx* ctx, const gpk_parser* parser, const char* path,
       first += n;
     }
     gpk_capindex_free(&xi);
+    if (!eof && pl.packets_cb && good) fill_ahead(si + pl.slots.size());
     if (st == GPK_CAP_END) {
       int is_eof = 0, is_panic = 0;
       gpk_capreader_error(rd, stats->error, sizeof(stats->error), &is_eof, &is_panic);

@@ -212,6 +212,18 @@ class Context:
         parts = []
         got_packets = []
 
+        raised = []  # an exception inside a ctypes callback would be printed and dropped: kept for after the call
+
+        def guarded(f):  # every callback: the first exception is kept and re-raised after the C call
+            def g(*args):
+                if not raised:
+                    try:
+                        f(*args)
+                    except BaseException as e:  # noqa: B902 (re-raised below, after the C call returns)
+                        raised.append(e)
+            return g
+
+        @guarded
         def pcb(user, first, n, base, nbytes, off, cap):
             if not n:
                 return
@@ -221,19 +233,14 @@ class Context:
             got_packets[:] = [(first, n, (data, o, c))]
         got_fields = []  # the current launch's fields (fields_cb runs right before cb)
 
+        @guarded
         def fcb(user, first, n, f):
             got_fields[:] = [(first, n, np.ctypeslib.as_array(ctypes.cast(f, ctypes.POINTER(ctypes.c_uint8)),
                                                                (n * 128,)).view(_lib.FIELDS_DTYPE)
                               if n else np.zeros(0, _lib.FIELDS_DTYPE))]
 
-        raised = []  # an exception inside a ctypes callback would be printed and dropped: kept for after the call
-
         def cb(*args):
-            if not raised:
-                try:
-                    _cb(*args)
-                except BaseException as e:  # noqa: B902 (re-raised below, after the C call returns)
-                    raised.append(e)
+            guarded(_cb)(*args)
 
         def _cb(user, first, n, rec, err, fl, ci, cap):
             if not n:
