@@ -855,7 +855,7 @@ def c5_replay(ctx, gib=10.0, reps=2, threads=8, cpu_threads=16):
                 batches=st["batches"], slots=st["slots"], l4_valid=valid4, write_s=round(gen_s, 2),
                 kernel=st["kernel"], **probe,
                 frac_of_htod_probe=round(st["file_bytes"] / w / 1e9 / probe["htod_probe_GBps"], 4),
-                parity=parity, c1_parser=c1, fields=fields, packets=packets_row,
+                parity=parity, c1_parser=c1, fields=fields, packets_cb=packets_row,
                 source="page-cached file in %s" % os.path.dirname(path), cpu_baseline=cpu)
 
 
