@@ -26,6 +26,9 @@ def main():
     ap.add_argument("--hydrate", type=int, default=0, metavar="K",
                     help="every K-th seed also: Hydrate from the one-launch fields result against Hydrate from "
                          "layouts, struct by struct (tests/hydrate_cases.compare), over the seed's first 4000 packets")
+    ap.add_argument("--narrow", type=int, default=0, metavar="K",
+                    help="every K-th seed also: gpk_decode_batch_narrow against the oracle's narrow form and the "
+                         "16-byte decode, every parser (tests/test_narrow_gpu.check_narrow)")
     ap.add_argument("--layouts", default="", type=lambda x: [y for y in x.split(",") if y],
                     help="placements to cycle through: packed, shuffled, reversed, wave_shuffled, gapped, sparse_mix")
     a = ap.parse_args()
@@ -56,6 +59,10 @@ def main():
             if seed % 3 == 0 and layout == "packed":
                 fields_check(ctx, name, packets, align=align)
                 n_batches += 2
+            if a.narrow and seed % a.narrow == 0:
+                from test_narrow_gpu import check_narrow
+                check_narrow(ctx, cfg, data, off, cap, "seed %d align %d %s %s narrow" % (seed, align, layout, name))
+                n_batches += 1
         if a.hydrate and seed % a.hydrate == 0:
             import hydrate_cases as H
             from gopacket_amd import gopacket as G
