@@ -1284,7 +1284,7 @@ def c5_sharded(ctx, rank, world, gib=10.0, reps=2, threads=8):
                 ranks=ranks, source="page-cached file in %s" % os.path.dirname(path))
 
 
-def narrow_row(r, world):
+def narrow_row(r, world, name=None):
     """The config's decode with the 8-byte record (gpk_decode_batch_narrow),
     timed beside the 16-byte one on the same batch: kernel time (the slowest
     rank's), rate by kernel time, HBM fraction of the same algorithmic bytes,
@@ -1296,9 +1296,10 @@ def narrow_row(r, world):
     k = nr["kernel_ms"]
     pk = r["strong"]["total_packets"] if r.get("strong") else r["n"] * world
     ach = r["algo_bytes"] / (k * 1e-3) / 1e9
+    traffic, profile = load_traffic(name + "n", r["n"]) if name else (None, None)
     return dict(kernel_ms=round(k, 4), value_by_kernel=round(pk / k / 1e3, 2), unit="Mpkts/s",
                 achieved_GBps=round(ach, 1), frac=round(ach / HBM_PEAK_GBS, 4),
-                speedup_vs_16B=round(r["kernel_ms"] / k, 4),
+                speedup_vs_16B=round(r["kernel_ms"] / k, 4), traffic=traffic, traffic_profile=profile,
                 record="gpk_record8: 8 B per packet, the full 16 B record in a side array only where it does not "
                        "fit (Correct != the header Checksum, or more than 8 layers)")
 
@@ -1317,6 +1318,9 @@ def main():
     ap.add_argument("--no-full-parity", action="store_true",
                     help="skip the every-packet comparison against the oracle (sampled parity only)")
     ap.add_argument("--no-probe", action="store_true", help="skip the streaming-read reference kernel")
+    ap.add_argument("--no-narrow", action="store_true",
+                    help="skip the narrow-record timing beside each config (it launches the same kernel symbols: "
+                         "keep it out of kernel traces that average by name)")
     ap.add_argument("--pcie", action="store_true", help="also time the host-buffer path (PCIe-inclusive)")
     ap.add_argument("--c5", type=float, default=10.0, metavar="GIB",
                     help="config C5: replay a GIB-GiB pcapng end to end (gpk_replay_file); 0 = skip")
@@ -1356,7 +1360,8 @@ def main():
         results[name] = run_config(name, args.packets, args.steps, args.warmup, rank, world, ctx,
                                    check_sample=0 if args.no_parity else 2048,
                                    probe=not args.no_probe,
-                                   full_check=not (args.no_parity or args.no_full_parity))
+                                   full_check=not (args.no_parity or args.no_full_parity),
+                                   narrow=not args.no_narrow)
     threads = host_cores()[0]
     # every rank runs the rows below its own shard at N > 1 (weak: its own 64M batch; C5: its byte range)
     fields_ranks = None
@@ -1395,7 +1400,7 @@ def main():
                          "of_skeleton": r["skeleton_ms"] and round(r["skeleton_ms"] / r["kernel_ms"], 4)},
             "parity": r["parity"],
             "full_parity": r["full_parity"],
-            "narrow": narrow_row(r, world),
+            "narrow": narrow_row(r, world, head),
             "dist_backend": dist.get_backend() if dist.is_initialized() else None,
             "configs": {},
         }
@@ -1412,7 +1417,7 @@ def main():
                    "probe_read_GBps": s["probe_gbs"] and round(s["probe_gbs"], 1),
                    "skeleton_ms": s["skeleton_ms"] and round(s["skeleton_ms"], 4),
                    "of_skeleton": s["skeleton_ms"] and round(s["skeleton_ms"] / s["kernel_ms"], 4),
-                   "narrow": narrow_row(s, world)}
+                   "narrow": narrow_row(s, world, name)}
             if st:
                 row.update(scaling="strong", total_packets=st["total_packets"], byte_balance=st["balance"],
                            note="one batch split at byte-balanced cuts; kernel_ms/achieved: the slowest rank's "

@@ -31,7 +31,8 @@ import pmc_summary  # noqa: E402
 
 def packets_of(cfg):
     import bench
-    c = bench.CONFIGS[cfg[:-1] if cfg.endswith("f") else cfg]  # c4f: C4's batch with the fused fields
+    # c4f: C4's batch with the fused fields; c2n etc.: the config's batch through the narrow record
+    c = bench.CONFIGS[cfg[:-1] if cfg.endswith("f") or cfg.endswith("n") else cfg]
     return c.get("packets", 64 * 2**20)
 
 

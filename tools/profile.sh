@@ -15,14 +15,16 @@ CFGS=${2:-c3,c2,c4,c1}
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -f csv -d $OUT/kt_c3 -o kt -- python3 bench.py --configs c3 --no-cpu-baseline --c5 0 --no-fields --steps 10 --warmup 2 > $OUT/kt_c3_bench.json || exit 1
-BCFGS=$(echo $CFGS | tr , '\n' | grep -v '^c4f$' | paste -sd, -)
-B="bench.py --no-cpu-baseline --no-parity --c5 0 --configs $BCFGS"
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -f csv -d $OUT/kt_c3 -o kt -- python3 bench.py --configs c3 --no-cpu-baseline --c5 0 --no-fields --no-narrow --steps 10 --warmup 2 > $OUT/kt_c3_bench.json || exit 1
+BCFGS=$(echo $CFGS | tr , '\n' | grep -v '^c4f$' | grep -v 'n$' | paste -sd, -)
+B="bench.py --no-cpu-baseline --no-parity --no-narrow --c5 0 --configs $BCFGS"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -f csv -d $OUT/kt -o kt -- python3 $B --steps 5 --warmup 1 > $OUT/kt_bench.json || exit 1
 P="--kernel-include-regex decode_(sb_|)kernel -f csv"
 for c in $(echo $CFGS | tr , ' '); do
   # c4f: the fused decode + fields launch on C4's batch (gpk_decode_batch_fields)
+  # c2n / c3n / ...: that config's batch through the narrow record (gpk_decode_batch_narrow)
   if [ "$c" = "c4f" ]; then A="tools/ab_inproc.py --configs c4 --fields --rounds 1 --steps 2 base";
+  elif [ "${c: -1}" = "n" ]; then A="tools/ab_inproc.py --configs ${c%n} --rounds 1 --steps 2 base@narrow";
   else A="tools/ab_inproc.py --configs $c --rounds 1 --steps 2 base"; fi
   timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE $P -d $OUT/$c/fetch -o fetch -- python3 $A > /dev/null || exit 2
   timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE $P -d $OUT/$c/write -o write -- python3 $A > /dev/null || exit 3
