@@ -27,6 +27,7 @@
 #include "../../include/gpk_afpacket.h"
 #include "../../include/gpk_capture.h"
 #include "../../gopacket_amd/csrc/gpk_pinned.h"
+#include "../../gopacket_amd/csrc/gpk_walk.h"
 
 // The pump and the replay are not driven here (they need a device); the
 // symbols they reference from other translation units abort if reached.
@@ -212,6 +213,14 @@ void run_capture(const std::vector<uint8_t>& file, int fmt, Rng& r) {
     g_sink += touch(all.data() + x.offsets[i], x.caplens[i]) + (uint64_t)x.ci[i].ts_sec;
   }
   gpk_capindex_free(&x);
+  // the byte-range replay's block sync (gpk_replay_file_range) over random windows of the
+  // bytes: inside [from, to), 4-aligned, reading nothing past end
+  for (int k = 0; k < 8 && all.n; k++) {
+    const uint64_t from = r.below(all.n), to = from + r.below(all.n - from + 1), span = 32 + r.below(1u << 16);
+    const uint64_t p = gpk_capreader_sync(rd, all.data(), from, to, all.n, span);
+    CHECK(p == ~0ull || (p >= from && p < to && p % 4 == 0));
+  }
+  g_sink += gpk_capreader_state_version(rd);
   metadata(rd);
   gpk_capreader_destroy(rd);
 }
