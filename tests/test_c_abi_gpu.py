@@ -47,7 +47,8 @@ def test_c_abi_replay_with_fields(tmp_path):
     assert m and int(m.group(1)) == 20000 and int(m.group(2)) > 15000, out.stdout
 
 
-def test_c_abi_threads_contexts():
+@pytest.mark.parametrize("threads,copies,reps", [(4, 400, 3), (8, 150, 2)])
+def test_c_abi_threads_contexts(threads, copies, reps):
     """The Go-shaped multi-GPU caller: one process, four
     OS threads, a gpk_ctx + parser per thread on device t % ndev (four
     contexts on the test box's one GPU), each decoding its byte-balanced slice
@@ -55,11 +56,11 @@ def test_c_abi_threads_contexts():
     own, and a context shared by all four. The slices put back together equal
     one context's decode bit for bit, that decode equals the committed oracle
     expectations for every packet, and after every gpk_* call the thread's
-    current HIP device is the one it set before the call."""
+    current HIP device is the one it set before the call. Also 8 threads."""
     exe = os.path.join(ROOT, "tests", "c_abi", "gpk_threads_test")
     if not os.path.exists(exe):
         build_c_abi_test()
-    out = subprocess.run([exe, os.path.join(ROOT, "tests", "golden", "c_abi"), "4", "400", "3"],
+    out = subprocess.run([exe, os.path.join(ROOT, "tests", "golden", "c_abi"), str(threads), str(copies), str(reps)],
                          capture_output=True, text=True, timeout=180)
     assert out.returncode == 0, out.stdout + out.stderr
     assert "all checks passed (threads)" in out.stdout
