@@ -25,6 +25,10 @@ _Static_assert(offsetof(gpk_record, status) == 8, "status at 8");
 _Static_assert(offsetof(gpk_record, ip4_csum) == 12, "ip4_csum at 12");
 _Static_assert(offsetof(gpk_record, l4_csum) == 14, "l4_csum at 14");
 _Static_assert(sizeof(gpk_layout) == 64, "gpk_layout is 64 bytes");
+_Static_assert(sizeof(gpk_record8) == 8 && offsetof(gpk_record8, status) == 4, "gpk_record8 is 8 bytes");
+_Static_assert(sizeof(gpk_results8) == 32 && offsetof(gpk_results8, wide) == 8, "gpk_results8 is 4 pointers");
+_Static_assert(sizeof(gpk_replay_range) == 48 && offsetof(gpk_replay_range, clean) == 40,
+               "gpk_replay_range: 5 words, then clean and state_changed");
 _Static_assert(sizeof(gpk_batch) == 40, "gpk_batch is 5 words");
 _Static_assert(sizeof(gpk_results) == 32, "gpk_results is 4 pointers");
 _Static_assert(sizeof(gpk_fields) == 128, "gpk_fields is 128 bytes");
