@@ -1206,7 +1206,7 @@ def c5_sharded(ctx, rank, world, gib=10.0, reps=2, threads=8):
     n = int(gib * 2**30 / per)
     tag = os.environ.get("MASTER_PORT", str(os.getpid()))
     path = os.path.join(os.environ.get("TMPDIR", "/tmp"), "gpk_c5_shared_%s.pcapng" % tag)
-    gen_s = 0.0
+    gen_s, size = 0.0, 0
     if rank == 0:
         t0 = time.perf_counter()
         size = S.gpk_synth_write_pcapng(path.encode(), 4, 0, n, host_cores()[0])
@@ -1215,7 +1215,7 @@ def c5_sharded(ctx, rank, world, gib=10.0, reps=2, threads=8):
             os.fsync(fd)
             os.close(fd)
         gen_s = time.perf_counter() - t0
-    ok = gather_obj(bool(rank != 0 or size), world)
+    ok = gather_obj(rank != 0 or size > 0, world)
     if not all(ok):
         raise RuntimeError("could not write %s" % path)
     rng = np.random.default_rng(5 + rank)
