@@ -176,9 +176,12 @@ def gather_obj(x, world):
 
 def rank_threads():
     """Host threads one rank may use for its parity checks: the job's CPU
-    share divided among the ranks on this node (torchrun's LOCAL_WORLD_SIZE)."""
+    share divided among the ranks on this node (torchrun's LOCAL_WORLD_SIZE),
+    at most OMP_NUM_THREADS (a per-process setting)."""
     local = max(1, int(os.environ.get("LOCAL_WORLD_SIZE", "1")))
-    return max(2, host_cores()[0] // local)
+    per = max(2, host_cores()[2] // local)
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    return min(per, int(omp)) if omp.isdigit() and int(omp) > 0 else per
 
 
 def barrier(world):
