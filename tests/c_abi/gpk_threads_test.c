@@ -4,6 +4,7 @@
  * decoding its byte-balanced slice of one batch concurrently with the others.
  *
  *   gpk_threads_test <golden dir> <threads> <copies> <reps>
+ *   gpk_threads_test replay <pcapng> <threads>
  *
  * The batch is <copies> shuffled copies of the golden packets of
  * tests/golden/c_abi (reference vectors, the reference's capture files,
@@ -30,6 +31,7 @@
 #include <hip/hip_runtime_api.h>
 
 #include "gpk.h"
+#include "gpk_capture.h"
 
 static int failures = 0;
 static pthread_mutex_t fail_mu = PTHREAD_MUTEX_INITIALIZER;
@@ -214,7 +216,149 @@ static int same(const struct out* a, const struct out* b, uint64_t n, const char
   return good;
 }
 
+/* ---- replay: one pcapng file, a thread (and context) per byte range -------- *
+ * The Go shape of C5 on N GPUs in one process: goroutines each replaying their
+ * range of one file (gpk_replay_file_range) on their own context at the same
+ * time. The ranges' results, concatenated, must equal one context's
+ * gpk_replay_file of the whole file: records, error arguments, flow hashes,
+ * capture info, capture lengths; every range clean and unchanged (a synthetic
+ * capture has no interface blocks past its header); the threads' devices kept. */
+struct collected {
+  gpk_record* rec;
+  uint32_t* err;
+  uint64_t* fl; /* per packet: link, network, transport */
+  gpk_capture_info* ci;
+  uint32_t* cap;
+  uint64_t n, room;
+};
+
+static void grow(struct collected* c, uint64_t need) {
+  if (need <= c->room) return;
+  uint64_t r = c->room ? c->room : 4096;
+  while (r < need) r *= 2;
+  c->rec = (gpk_record*)realloc(c->rec, r * sizeof(gpk_record));
+  c->err = (uint32_t*)realloc(c->err, r * 8);
+  c->fl = (uint64_t*)realloc(c->fl, r * 24);
+  c->ci = (gpk_capture_info*)realloc(c->ci, r * sizeof(gpk_capture_info));
+  c->cap = (uint32_t*)realloc(c->cap, r * 4);
+  c->room = r;
+}
+
+static void on_results(void* user, uint64_t first, uint64_t n, const gpk_record* rec, const uint32_t* err,
+                       const uint64_t* flows, const gpk_capture_info* ci, const uint32_t* caplens) {
+  struct collected* c = (struct collected*)user;
+  CHECK(first == c->n, "results for packet %llu, expected %llu", (unsigned long long)first, (unsigned long long)c->n);
+  grow(c, c->n + n);
+  memcpy(c->rec + c->n, rec, n * sizeof(gpk_record));
+  memcpy(c->err + 2 * c->n, err, n * 8);
+  for (uint64_t i = 0; i < n; i++)
+    for (int j = 0; j < 3; j++) c->fl[3 * (c->n + i) + j] = flows[(uint64_t)j * n + i];
+  memcpy(c->ci + c->n, ci, n * sizeof(gpk_capture_info));
+  memcpy(c->cap + c->n, caplens, n * 4);
+  c->n += n;
+}
+
+static struct {
+  const char* path;
+  uint64_t size;
+  int threads, ndev;
+  struct collected* parts;
+  gpk_replay_range* ranges;
+  gpk_replay_stats* stats;
+} R;
+
+static void* replay_run(void* arg) {
+  const int t = ((struct worker*)arg)->t;
+  const int dev = t % R.ndev, own = (t + 1) % R.ndev;
+  CHECK(hipSetDevice(own) == hipSuccess, "thread %d: hipSetDevice(%d)", t, own);
+  gpk_ctx* ctx = NULL;
+  int rc = gpk_ctx_create(&ctx, dev);
+  CHECK(rc == GPK_OK, "thread %d: gpk_ctx_create: %s", t, gpk_strerror(rc));
+  DEVCHK(own, "gpk_ctx_create");
+  gpk_parser* p = make_parser();
+  if (!ctx || !p) return NULL;
+  gpk_replay_range* rg = &R.ranges[t];
+  rg->begin = R.size * (uint64_t)t / (uint64_t)R.threads;
+  rg->end = t == R.threads - 1 ? 0 : R.size * (uint64_t)(t + 1) / (uint64_t)R.threads;
+  gpk_replay_opts o;
+  memset(&o, 0, sizeof(o));
+  o.slot_bytes = 8u << 20; /* small slots: several per range */
+  o.slots = 3;
+  o.batch_pkts = 50000;
+  rc = gpk_replay_file_range(ctx, p, R.path, rg, &o, on_results, &R.parts[t], &R.stats[t]);
+  CHECK(rc == GPK_OK, "thread %d: gpk_replay_file_range: %s %s", t, gpk_strerror(rc), R.stats[t].error);
+  DEVCHK(own, "gpk_replay_file_range");
+  gpk_parser_destroy(p);
+  gpk_ctx_destroy(ctx);
+  DEVCHK(own, "gpk_ctx_destroy");
+  return NULL;
+}
+
+static int replay_main(const char* path, int T) {
+  if (hipGetDeviceCount(&R.ndev) != hipSuccess || R.ndev < 1) return 2;
+  FILE* f = fopen(path, "rb");
+  if (!f) return 2;
+  fseek(f, 0, SEEK_END);
+  R.size = (uint64_t)ftell(f);
+  fclose(f);
+  R.path = path;
+  R.threads = T;
+  R.parts = (struct collected*)calloc(T, sizeof(struct collected));
+  R.ranges = (gpk_replay_range*)calloc(T, sizeof(gpk_replay_range));
+  R.stats = (gpk_replay_stats*)calloc(T, sizeof(gpk_replay_stats));
+  /* one context, the whole file */
+  struct collected whole;
+  memset(&whole, 0, sizeof(whole));
+  gpk_ctx* ctx = NULL;
+  if (gpk_ctx_create(&ctx, 0) != GPK_OK) return 2;
+  gpk_parser* p = make_parser();
+  gpk_replay_opts o;
+  memset(&o, 0, sizeof(o));
+  gpk_replay_stats st;
+  int rc = gpk_replay_file(ctx, p, path, &o, on_results, &whole, &st);
+  CHECK(rc == GPK_OK && strcmp(st.error, "EOF") == 0, "whole replay: %s %s", gpk_strerror(rc), st.error);
+  /* the ranges, a thread and context each, at once */
+  struct worker* w = (struct worker*)calloc(T, sizeof(*w));
+  for (int t = 0; t < T; t++) {
+    w[t].t = t;
+    if (pthread_create(&w[t].th, NULL, replay_run, &w[t])) return 2;
+  }
+  for (int t = 0; t < T; t++) pthread_join(w[t].th, NULL);
+  uint64_t total = 0, bad = 0;
+  for (int t = 0; t < T; t++) {
+    const gpk_replay_range* g = &R.ranges[t];
+    CHECK(g->clean && !g->state_changed, "range %d not exact: clean %d state_changed %d", t, g->clean,
+          g->state_changed);
+    CHECK(t == 0 || g->sync_begin == R.ranges[t - 1].sync_end, "range %d does not start where %d ended", t, t - 1);
+    const struct collected* c = &R.parts[t];
+    for (uint64_t i = 0; i < c->n && total + i < whole.n; i++) {
+      const uint64_t k = total + i;
+      int good = memcmp(&c->rec[i], &whole.rec[k], sizeof(gpk_record)) == 0 &&
+                 memcmp(&c->fl[3 * i], &whole.fl[3 * k], 24) == 0 &&
+                 memcmp(&c->ci[i], &whole.ci[k], sizeof(gpk_capture_info)) == 0 && c->cap[i] == whole.cap[k];
+      if (good && gpk_record_err(&c->rec[i])) good = memcmp(&c->err[2 * i], &whole.err[2 * k], 8) == 0;
+      if (!good && bad++ < 5) CHECK(0, "range %d packet %llu differs from the whole replay", t, (unsigned long long)i);
+    }
+    total += c->n;
+  }
+  CHECK(total == whole.n, "%llu packets across ranges, %llu in the whole replay", (unsigned long long)total,
+        (unsigned long long)whole.n);
+  printf("replay: %d ranges on %d device(s) at once, packets", T, R.ndev);
+  for (int t = 0; t < T; t++) printf(" %llu", (unsigned long long)R.parts[t].n);
+  printf(" = %llu of %llu, %s\n", (unsigned long long)total, (unsigned long long)whole.n,
+         bad || total != whole.n ? "DIFFER" : "bit-exact");
+  gpk_parser_destroy(p);
+  gpk_ctx_destroy(ctx);
+  if (failures) {
+    fprintf(stderr, "%d check(s) failed\n", failures);
+    return 1;
+  }
+  printf("gpk C ABI: all checks passed (threads replay)\n");
+  return 0;
+}
+
 int main(int argc, char** argv) {
+  if (argc >= 4 && strcmp(argv[1], "replay") == 0) return replay_main(argv[2], atoi(argv[3]));
   if (argc < 5) {
     fprintf(stderr, "usage: %s <golden dir> <threads> <copies> <reps>\n", argv[0]);
     return 2;

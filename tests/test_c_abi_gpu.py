@@ -66,3 +66,24 @@ def test_c_abi_threads_contexts(threads, copies, reps):
     assert "all checks passed (threads)" in out.stdout
     assert ", 0 differ from the oracle" in out.stdout, out.stdout
     assert "per-thread host bit-exact, device bit-exact, shared bit-exact" in out.stdout, out.stdout
+
+
+@pytest.mark.parametrize("threads", [3, 8])
+def test_c_abi_threads_replay_ranges(tmp_path, threads):
+    """C5's Go shape on N GPUs in one process: a thread and a context per byte
+    range of one pcapng (gpk_replay_file_range), all replaying at once (the
+    replay pipeline's reader threads, staging, device walk and launches of
+    several contexts side by side); the ranges' results concatenated equal one
+    context's whole-file replay bit for bit (records, error arguments, flows,
+    capture info, capture lengths), every range clean, every thread's device
+    kept."""
+    from gopacket_amd import _lib
+    exe = os.path.join(ROOT, "tests", "c_abi", "gpk_threads_test")
+    if not os.path.exists(exe):
+        build_c_abi_test()
+    path = str(tmp_path / "c4.pcapng")
+    assert _lib.synth_lib().gpk_synth_write_pcapng(path.encode(), 4, 77, 200000, 4) > 0
+    out = subprocess.run([exe, "replay", path, str(threads)], capture_output=True, text=True, timeout=180)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert "all checks passed (threads replay)" in out.stdout
+    assert "= 200000 of 200000, bit-exact" in out.stdout, out.stdout
