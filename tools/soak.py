@@ -3,7 +3,9 @@
 host RSS and free device memory checked for growth. 30 replays of a ~2 GiB
 C4 pcapng (cycling plain / fields / packets / fields+packets, contexts kept
 and re-created), 2000 decode launches over 8 caller streams, 20 contexts
-created and destroyed, 30 AF_PACKET pumps over a lapping ring."""
+created and destroyed, 30 AF_PACKET pumps over a lapping ring; round 6: 10
+byte-range splits of the same file (2-4 ranges each, every range clean and the
+packets summing to the file's) and 2000 narrow-record launches."""
 import gc
 import os
 import sys
@@ -63,6 +65,22 @@ def main():
             assert st["packets"] == n == cnt[0] and st["error"] == "EOF", st
             if k == 0 or k % 10 == 9:
                 mark("replay %d" % k)
+        from gopacket_amd import shard
+        size = os.path.getsize(path)
+        for k in range(int(os.environ.get("SOAK_SPLITS", "10"))):  # byte-range replays (gpk_replay_file_range)
+            world, got = 2 + k % 3, 0
+            for r in range(world):
+                cnt = [0]
+
+                def on_batch(first, m, *v):
+                    cnt[0] += m
+
+                _, st = ctx.replay_file(parser, path, byte_range=shard.file_range(size, r, world), collect=False,
+                                        on_batch=on_batch)
+                assert st["range"]["clean"] and not st["range"]["state_changed"] and st["packets"] == cnt[0], st
+                got += cnt[0]
+            assert got == n, (k, got, n)
+        mark("10 byte-range splits")
         d, o, c = synth.device_batch(4, 0, 1 << 16)
         streams = [torch.cuda.Stream() for _ in range(8)]
         outs = [(torch.empty(16 << 16, dtype=torch.uint8, device="cuda"), torch.zeros(2 << 16, dtype=torch.int32,
@@ -72,6 +90,12 @@ def main():
             rec, err, fl = outs[k % 8]
             ctx.decode_device(parser, d, o, c, rec, err, fl, stream=s)
         mark("2000 launches on 8 streams")
+        r8 = [(torch.empty(8 << 16, dtype=torch.uint8, device="cuda"), torch.zeros(16 << 16, dtype=torch.uint8,
+               device="cuda")) for _ in streams]
+        for k in range(2000):
+            rec, err, fl = outs[k % 8]
+            ctx.decode_device_narrow(parser, d, o, c, r8[k % 8][0], r8[k % 8][1], err, fl, stream=streams[k % 8])
+        mark("2000 narrow launches on 8 streams")
         for k in range(20):
             x = engine.Context(0)
             p = engine.ParserConfig(17, kinds, outputs=cfg["outputs"])
