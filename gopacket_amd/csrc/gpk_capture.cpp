@@ -154,6 +154,11 @@ struct gpk_capreader {
   bool st_saved = false;
   OptBuf opt, opt_snap;
   bool opt_saved = false;
+  // every change of st or opt counts one (touch / touch_opt), undone with the
+  // change on a rollback: equal counts after the same bytes whatever the
+  // chunking, so a byte-range replay can tell whether its range changed any
+  // reader state (gpk_replay_file_range)
+  uint64_t mutations = 0;
   uint32_t typ = 0, blen = 0;  // currentBlock
   uint16_t opt_code = 0;
   // ci of the current call
@@ -197,12 +202,14 @@ struct gpk_capreader {
   }
   bool be() const { return st.be; }
   void touch() {
+    mutations++;
     if (!st_saved) {
       st_snap = st;
       st_saved = true;
     }
   }
   void touch_opt() {
+    mutations++;
     if (!opt_saved) {
       opt_snap = opt;
       opt_saved = true;
@@ -709,6 +716,7 @@ int gpk_capreader_index(gpk_capreader* r, const uint8_t* buf, uint64_t len, int 
       } catch (NeedMore&) {
         r->st = NgState();
         r->opt = OptBuf();
+        r->mutations = 0;
         r->pos = 0;
         throw;
       } catch (GoErr& e) {
@@ -726,7 +734,7 @@ int gpk_capreader_index(gpk_capreader* r, const uint8_t* buf, uint64_t len, int 
         status = GPK_CAP_FULL;
         break;
       }
-      const uint64_t start = r->pos;
+      const uint64_t start = r->pos, m0 = r->mutations;
       r->st_saved = r->opt_saved = false;
       try {
         const uint64_t off = ng ? r->ng_read_packet() : r->pcap_read_packet();
@@ -743,6 +751,7 @@ int gpk_capreader_index(gpk_capreader* r, const uint8_t* buf, uint64_t len, int 
       } catch (NeedMore&) {
         if (r->st_saved) r->st = std::move(r->st_snap);
         if (r->opt_saved) r->opt = std::move(r->opt_snap);
+        r->mutations = m0;
         r->pos = start;
         status = GPK_CAP_MORE;
         break;
@@ -1162,6 +1171,8 @@ uint64_t gpk_capreader_sync(const gpk_capreader* r, const uint8_t* b, uint64_t f
   }
   return ~0ull;
 }
+
+uint64_t gpk_capreader_mutations(const gpk_capreader* r) { return r ? r->mutations : 0; }
 
 uint64_t gpk_capreader_state_version(const gpk_capreader* r) {
   if (!r || r->format != GPK_CAP_PCAPNG || !r->opened || r->open_failed) return 0;

@@ -483,7 +483,8 @@ uint64_t ng_header_end(int fd, uint64_t size) {
 
 }  // namespace
 
-static int plan_range(Src& src, uint32_t ng_flags, gpk_replay_range* rg, uint64_t* hdr_version) {
+static int plan_range(Src& src, uint32_t ng_flags, gpk_replay_range* rg, uint64_t* hdr_version,
+                      uint64_t* hdr_mutations) {
   const uint64_t size = src.size;
   const uint64_t H = ng_header_end(src.fd, size);
   gpk_capreader* hr = nullptr;
@@ -494,12 +495,19 @@ static int plan_range(Src& src, uint32_t ng_flags, gpk_replay_range* rg, uint64_
   } free_hr{hr};
   std::vector<uint8_t> buf(H + 16, 0);
   if (H && (uint64_t)pread(src.fd, buf.data(), H, 0) != H) return GPK_EINVAL;
+  // the leading blocks as a stream that ends at H: the reader applies every one
+  // of them and meets io.EOF at H (with more bytes to come it would roll the
+  // blocks it read while looking for the first packet back)
   gpk_capindex x{};
   uint64_t used = 0;
-  const int st = gpk_capreader_index_all(hr, buf.data(), H, 0, 1, &x, &used);
+  const int st = gpk_capreader_index_all(hr, buf.data(), H, 1, 1, &x, &used);
   const bool none = x.n == 0;
   gpk_capindex_free(&x);
-  *hdr_version = st == GPK_CAP_MORE && none && used == H ? gpk_capreader_state_version(hr) : 0;
+  int at_eof = 0;
+  gpk_capreader_error(hr, nullptr, 0, &at_eof, nullptr);
+  const bool ok = st == GPK_CAP_END && at_eof && none && used == H;
+  *hdr_version = ok ? gpk_capreader_state_version(hr) : 0;
+  *hdr_mutations = gpk_capreader_mutations(hr);
   constexpr uint64_t kSpan = 4ull << 20, kWin = 4ull << 20;
   auto sync_at = [&](uint64_t X) -> uint64_t {
     if (X <= H) return H;
@@ -607,13 +615,13 @@ static int replay_file(gpk_ctx* ctx, const gpk_parser* parser, const char* path,
     format = m == 0x0A0D0D0Au ? GPK_CAP_PCAPNG : GPK_CAP_PCAP;
   }
   // ---- a byte range of the file (gpk_replay_file_range) ---------------------
-  uint64_t hdr_version = 0;
+  uint64_t hdr_version = 0, hdr_mutations = 0;
   if (rg) {
     if (src.gz || format != GPK_CAP_PCAPNG) {
       snprintf(stats->error, sizeof(stats->error), "byte-range replay needs an uncompressed pcapng file");
       return GPK_EUNSUPP;
     }
-    const int rrc = plan_range(src, opt.ng_flags, rg, &hdr_version);
+    const int rrc = plan_range(src, opt.ng_flags, rg, &hdr_version, &hdr_mutations);
     if (rrc) {
       snprintf(stats->error, sizeof(stats->error), "byte-range replay: reading the file failed");
       return rrc;
@@ -1114,7 +1122,9 @@ static int replay_file(gpk_ctx* ctx, const gpk_parser* parser, const char* path,
   stats->wall_s = now_s() - t_start;
   if (rg) {
     rg->clean = good && rc == GPK_OK && clean_eof && stats->stream_bytes == src.size ? 1 : 0;
-    rg->state_changed = gpk_capreader_state_version(rd) != hdr_version ? 1 : 0;
+    // any change of the reader's state past the leading blocks (a section, an
+    // interface, statistics, an option value the next block could reuse)
+    rg->state_changed = gpk_capreader_mutations(rd) != hdr_mutations ? 1 : 0;
   }
   if (trace && trace[0] == '1')
     fprintf(stderr, "gpk_replay: setup %.4f s, loop %.4f s, %llu slots\n", t_loop - t_start, now_s() - t_loop,

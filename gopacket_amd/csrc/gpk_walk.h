@@ -57,6 +57,10 @@ bool gpk_capreader_walk_state(const gpk_capreader* r, gpk::WalkState* out);
 uint64_t gpk_capreader_sync(const gpk_capreader* r, const uint8_t* b, uint64_t from, uint64_t to, uint64_t end,
                             uint64_t span);
 uint64_t gpk_capreader_state_version(const gpk_capreader* r);
+// gpk_capture.cpp: how many changes of the reader's state (section, interfaces,
+// the reused option buffer) the blocks read so far made; the same count after
+// the same bytes however they were chunked.
+uint64_t gpk_capreader_mutations(const gpk_capreader* r);
 
 // gpk_walk.hip: pass 1 over buf[p0, len) (buf 16-byte aligned, the reader at
 // p0, blocks at p0 + 4k) in segments of `seg` bytes from buf, pass 2 writing

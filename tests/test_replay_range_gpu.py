@@ -108,6 +108,36 @@ def test_range_default_opts_and_fields(gpu_ctx, imix):
     assert np.array_equal(np.concatenate([p["fields"] for p in parts]), whole["fields"])
 
 
+def test_range_option_blocks_are_state(gpu_ctx, tmp_path):
+    """An EPB with options and an interface statistics block change reader
+    state a later block can read (NgReader reuses one option buffer: a
+    zero-length option keeps the previous value, ngread.go:215-219), so the
+    range holding either is not exact for the ranges after it; a name record
+    changes nothing. Three files, one of each, split 2 ways with the block in
+    the first half."""
+    from gopacket_amd import synth
+    parser = device_parser(CONFIGS["statsassembly"])
+    for kind in ("options", "isb", "nrb"):
+        raw = pcapgen.shb() + pcapgen.idb(1, 0)
+        for i in range(4000):
+            p = synth.packet(4, i)
+            if i == 1000 and kind == "options":
+                raw += pcapgen.epb(p, ts=i, options=pcapgen.opt(1, b"note") + pcapgen.end_opt())
+            elif i == 1000 and kind == "isb":
+                raw += pcapgen.isb(0, 5, options=pcapgen.opt(4, bytes(8)) + pcapgen.end_opt())
+            elif i == 1000:
+                raw += pcapgen.nrb([(1, b"\x0a\x00\x00\x01x\x00")])
+            else:
+                raw += pcapgen.epb(p, ts=i)
+        path = tmp_path / ("%s.pcapng" % kind)
+        path.write_bytes(raw)
+        whole, _ = gpu_ctx.replay_file(parser, str(path))
+        got, _, ranges, f = split_replay(gpu_ctx, parser, str(path), 2)
+        assert same(got, whole), kind
+        assert ranges[0]["clean"], kind
+        assert ranges[0]["state_changed"] == (kind != "nrb") and f == (None if kind == "nrb" else 0), (kind, ranges)
+
+
 @pytest.mark.parametrize("bo", ["<", ">"])
 def test_range_fake_chains(gpu_ctx, tmp_path, bo):
     """Payloads with fake EPB chains, three interfaces, an EPB with options, a
@@ -116,8 +146,12 @@ def test_range_fake_chains(gpu_ctx, tmp_path, bo):
     raw = walk_capture(bo)
     path = tmp_path / "walk.pcapng"
     path.write_bytes(raw)
-    whole_and_split(gpu_ctx, str(path), (2, 3, 7, 16), expect_exact=False, slot_bytes=1 << 18, slots=3,
-                    batch_pkts=3000)
+    _, _, seen = whole_and_split(gpu_ctx, str(path), (2, 3, 7, 16), expect_exact=False, slot_bytes=1 << 18,
+                                 slots=3, batch_pkts=3000)
+    for world, (f, ranges) in seen.items():  # the file's three interfaces are its header: every cut finds a block
+        assert all(g["sync_end"] > g["sync_begin"] for g in ranges), (world, ranges)
+        # the EPB with options (packet 4000, ~1/3 in) and the statistics block (~3/4 in) are reader state
+        assert f is not None and f < world - 1, (world, f)
 
 
 def test_range_cut_inside_fake_chain(gpu_ctx, tmp_path):
@@ -158,8 +192,8 @@ def test_range_cut_inside_fake_chain(gpu_ctx, tmp_path):
 
 def test_range_new_interface_and_big_blocks(gpu_ctx, tmp_path):
     """A new interface block mid-file (the reader state changes: the rank that
-    holds it is inexact for the ranks after it), blocks of 16-64 KiB, an EPB
-    with options and a name record."""
+    holds it is inexact for the ranks after it), blocks of 16-64 KiB and a name
+    record (which changes no reader state)."""
     from gopacket_amd import synth
     rng = np.random.default_rng(11)
     raw = pcapgen.shb() + pcapgen.idb(1, 0)
@@ -167,9 +201,7 @@ def test_range_new_interface_and_big_blocks(gpu_ctx, tmp_path):
         p = synth.packet(4, i)
         if i % 2500 == 17:
             p = p + bytes(rng.integers(0, 256, int(rng.integers(16, 64)) << 10, dtype=np.uint8))
-        if i == 12345:
-            raw += pcapgen.epb(p, ts=i, options=pcapgen.opt(1, b"note") + pcapgen.end_opt())
-        elif i == 6000:
+        if i == 6000:
             raw += pcapgen.nrb([(1, b"\x0a\x00\x00\x01x\x00")])
         elif i == 15000:
             raw += pcapgen.idb(1, 0)
