@@ -221,7 +221,9 @@ int gpk_replay_file(gpk_ctx* ctx, const gpk_parser* p, const char* path, const g
  * The N results, concatenated in range order, are exactly gpk_replay_file's
  * when every caller but the last reports clean (its reader met io.EOF exactly
  * at sync_end, so sync_end is a real block boundary) and !state_changed (no
- * section header or interface block inside its range). Otherwise let f be the
+ * block inside its range changed reader state: a section header, an interface,
+ * interface statistics, or an option value NgReader keeps for the next option,
+ * as EPB options do). Otherwise let f be the
  * first caller that does not: its result and every later one's are replaced
  * by a replay of [f's sync_begin, end of file) (begin = sync_begin, end = 0),
  * which is exact. Uncompressed pcapng only (GPK_EUNSUPP otherwise). */
@@ -231,7 +233,7 @@ typedef struct gpk_replay_range {
   uint64_t sync_begin;    /* out: the first block this caller replayed (0: the file's start)  */
   uint64_t sync_end;      /* out: where its blocks had to end                                 */
   int clean;              /* out: the reader met io.EOF exactly at sync_end                   */
-  int state_changed;      /* out: a block in the range changed the reader state               */
+  int state_changed;      /* out: a block in the range changed reader state (see above)       */
 } gpk_replay_range;
 int gpk_replay_file_range(gpk_ctx* ctx, const gpk_parser* p, const char* path, gpk_replay_range* range,
                           const gpk_replay_opts* opts, gpk_replay_cb cb, void* user, gpk_replay_stats* stats);
