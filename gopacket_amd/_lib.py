@@ -22,6 +22,7 @@ SYNTH_PATH = os.path.join(_HERE, "libgpk_synth.so")
 # include/gpk.h constants
 GPK_OK = 0
 GPK_EINVAL, GPK_ENOMEM, GPK_EHIP, GPK_ENODEV, GPK_EUNSUPP = -1, -2, -3, -4, -5
+GPK_STOPPED = 1  # a replay or ring pump ended early at gpk_stop (not an error)
 OUT_IP4_CSUM, OUT_L4_CSUM, OUT_FLOWS, OUT_ALL = 1, 2, 4, 7
 TABLES_AUTO, TABLES_GLOBAL = 0, 1
 DEC_NONE, DEC_ETHERNET, DEC_DOT1Q, DEC_IPV4, DEC_IPV6, DEC_IPV6_EXT, DEC_TCP, DEC_UDP, DEC_PAYLOAD, \
@@ -72,7 +73,7 @@ EXPORTS = (
     "gpk_parser_create", "gpk_parser_destroy", "gpk_parser_add_decoder", "gpk_parser_set_options",
     "gpk_parser_set_outputs", "gpk_parser_decoder_for", "gpk_parser_set_ethertype",
     "gpk_parser_set_ipprotocol", "gpk_parser_set_tcp_port", "gpk_parser_set_udp_port", "gpk_ctx_create",
-    "gpk_ctx_destroy", "gpk_ctx_set_table_mode", "gpk_decode_batch", "gpk_decode_batch_narrow", "gpk_decode_batch_fields",
+    "gpk_ctx_destroy", "gpk_ctx_set_table_mode", "gpk_stop", "gpk_decode_batch", "gpk_decode_batch_narrow", "gpk_decode_batch_fields",
     "gpk_extract_fields",
     "gpk_decode_kernel_name", "gpk_decode_occupancy", "gpk_diag_set_buffer", "gpk_decode_batch_host", "gpk_decode_batch_host_fields",
     "gpk_decoded_list",
@@ -84,6 +85,9 @@ EXPORTS = (
     "gpk_capreader_ninterfaces", "gpk_capreader_interface", "gpk_capreader_interface_str", "gpk_replay_file",
     "gpk_replay_file_range",
     "gpk_capreader_index_all", "gpk_capindex_free",
+    "gpk_capreader_section_end_at", "gpk_capreader_nstat_events", "gpk_capreader_stat_event",
+    "gpk_capreader_nnames", "gpk_capreader_name", "gpk_capreader_skip_section", "gpk_capreader_set_snaplen",
+    "gpk_capreader_keep_options", "gpk_capreader_packet_options",
     # include/gpk_afpacket.h
     "gpk_tp_default_opts", "gpk_tp_check_opts", "gpk_tpacket_new", "gpk_tpacket_attach", "gpk_tpacket_close",
     "gpk_tpacket_ring", "gpk_tpacket_index", "gpk_tpacket_defer", "gpk_tpacket_set_threads", "gpk_tpacket_release_seq", "gpk_tpacket_release",
@@ -260,6 +264,7 @@ def lib():
         "gpk_ctx_create": ([P(vp), c_int], c_int),
         "gpk_ctx_destroy": ([vp], c_int),
         "gpk_ctx_set_table_mode": ([vp, c_int], c_int),
+        "gpk_stop": ([vp], c_int),
         "gpk_decode_batch": ([vp, vp, P(Batch), P(Results), vp], c_int),
         "gpk_decode_batch_narrow": ([vp, vp, P(Batch), P(Results8), vp], c_int),
         "gpk_decode_batch_host": ([vp, vp, P(Batch), P(Results)], c_int),
@@ -290,6 +295,17 @@ def lib():
         "gpk_capreader_ninterfaces": ([vp, c_int], c_int),
         "gpk_capreader_interface": ([vp, c_int, c_int, P(NgInterface)], c_int),
         "gpk_capreader_interface_str": ([vp, c_int, c_int, c_int, ctypes.c_char_p, ctypes.c_size_t], c_int),
+        "gpk_capreader_section_end_at": ([vp, c_int, P(ctypes.c_uint64), P(ctypes.c_uint64)], c_int),
+        "gpk_capreader_nstat_events": ([vp], c_int),
+        "gpk_capreader_stat_event": ([vp, c_int, P(ctypes.c_uint64), P(ctypes.c_uint64), P(c_int), P(NgInterface),
+                                      ctypes.c_char_p, ctypes.c_size_t], c_int),
+        "gpk_capreader_nnames": ([vp], c_int),
+        "gpk_capreader_name": ([vp, c_int, P(c_int), vp, P(c_int), P(c_int), ctypes.c_char_p, ctypes.c_size_t],
+                               c_int),
+        "gpk_capreader_skip_section": ([vp], c_int),
+        "gpk_capreader_set_snaplen": ([vp, ctypes.c_uint32], c_int),
+        "gpk_capreader_keep_options": ([vp, c_int], c_int),
+        "gpk_capreader_packet_options": ([vp, ctypes.c_uint64, P(vp), P(ctypes.c_uint64)], c_int),
         "gpk_replay_file": ([vp, vp, ctypes.c_char_p, P(ReplayOpts), REPLAY_CB, vp, P(ReplayStats)], c_int),
         "gpk_replay_file_range": ([vp, vp, ctypes.c_char_p, P(ReplayRange), P(ReplayOpts), REPLAY_CB, vp,
                                    P(ReplayStats)], c_int),

@@ -3,13 +3,13 @@
 Mirrors the reference's afpacket package for the ingest side of the path
 (SURVEY.md §8(f)2):
 
-  NewTPacket(*opts) -> TPacket                afpacket/afpacket.go:309-343
-  Opt* option types, Default* constants       afpacket/options.go:28-119
-  parseOptions(*opts)                         options.go:121-211 (error texts)
-  TPacket.ZeroCopyReadPacketData()            afpacket.go:367-399
-  TPacket.ReadPacketData() / ReadPacketDataTo afpacket.go:436-463
-  TPacket.Stats() / SocketStats()             afpacket.go:402-431
-  TPacket.SetBPF / SetFanout / Close          afpacket.go:336-349,545-553,291-306
+  NewTPacket(*opts) -> TPacket                afpacket/afpacket.go:261-294
+  Opt* option types, Default* constants       afpacket/options.go:22-132
+  parseOptions(*opts)                         options.go:160-211 (error texts)
+  TPacket.ZeroCopyReadPacketData()            afpacket.go:335-367
+  TPacket.ReadPacketData() / ReadPacketDataTo afpacket.go:438-460
+  TPacket.Stats() / SocketStats()             afpacket.go:370-431
+  TPacket.SetBPF / SetFanout / Close          afpacket.go:297-309,542-548,243-254
 
 plus what the reference has no counterpart for:
 
@@ -234,7 +234,9 @@ class TPacket:
         only): on_batch also gets, last, (pointers, caplens): packet i's bytes
         are ctypes.string_at(pointers[i], caplens[i]) (a ring frame or its VLAN
         copy, valid during the call); ring headers go back to the kernel once
-        their batch was delivered."""
+        their batch was delivered. A callback that raises ends the pump at
+        once (gpk_stop) and the exception is raised from here; ctx.stop() from
+        a callback or another thread ends it too (stats["stopped"])."""
         if packets and collect:
             raise ValueError("packets=True hands out views of the ring: use collect=False and on_batch")
         parts = []
@@ -243,13 +245,14 @@ class TPacket:
 
         raised = []  # an exception inside a ctypes callback would be printed and dropped: kept for after the call
 
-        def guarded(f):  # every callback: the first exception is kept and re-raised after the C call
+        def guarded(f):  # every callback: the first exception is kept, ends the pump, and is re-raised after it
             def g(*args):
                 if not raised:
                     try:
                         f(*args)
                     except BaseException as e:  # noqa: B902 (re-raised below, after the C call returns)
                         raised.append(e)
+                        _lib.lib().gpk_stop(ctx.h)  # no further callback: the pump drains and returns
             return g
 
         @guarded
@@ -299,12 +302,13 @@ class TPacket:
         rc = _lib.lib().gpk_tpacket_pump(ctx.h, parser.h, self.h, ctypes.byref(o), c_cb, None, ctypes.byref(st))
         if raised:
             raise raised[0]
-        if rc != _lib.GPK_OK:
+        if rc not in (_lib.GPK_OK, _lib.GPK_STOPPED):
             raise _lib.GpkError("gpk_tpacket_pump: %d %s %s" % (rc, st.error.decode(errors="replace"),
                                                                 _lib.lib().gpk_last_hip_error().decode()))
         stats = {k: getattr(st, k) for k, _ in _lib.PumpStats._fields_}
         stats["error"] = st.error.decode(errors="replace")
         stats["kernel"] = st.kernel.decode(errors="replace")
+        stats["stopped"] = rc == _lib.GPK_STOPPED
         res = None
         if collect:
             if parts:

@@ -2,11 +2,11 @@
 // (include/gpk_afpacket.h).
 //
 // The reader restates afpacket.TPacket.ZeroCopyReadPacketData
-// (afpacket/afpacket.go:367-399) over the three header layouts of
+// (afpacket/afpacket.go:335-367) over the three header layouts of
 // afpacket/header.go: the same ring position arithmetic (getTPacketHeader
 // :469-492), the same release-when-moving-on rule (releaseCurrentPacket
-// :353-358), the same "empty block" retry, the same v3 next-packet step
-// (header.go:249-263) and the same VLAN-header insertion (:150-158).
+// :316-321), the same "empty block" retry, the same v3 next-packet step
+// (header.go:254-268) and the same VLAN-header insertion (:147-155).
 // Differences are confined to what a batch interface must change:
 //   * where the reference blocks in poll(2), the walk stops (GPK_TP_WAIT) and
 //     resumes exactly there on the next call;
@@ -88,7 +88,7 @@ double now_s() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
-// Header sizes (header.go:125-127) and the sockaddr_ll that follows each.
+// Header sizes (header.go:135-137) and the sockaddr_ll that follows each.
 constexpr uint64_t kV1Hdr = 0x20, kV2Hdr = 0x20, kV3Hdr = 0x30;
 
 // A fixed set of worker threads that run one function per call: the
@@ -212,7 +212,7 @@ uint32_t header_status(const gpk_tpacket* t, uint64_t h) {
   return t->version == GPK_TPACKET_V3 ? ld_status_acquire(p + 8) : ld_status_acquire(p);
 }
 
-void clear_status(gpk_tpacket* t, uint64_t h) {  // clearStatus (header.go:152,185,237)
+void clear_status(gpk_tpacket* t, uint64_t h) {  // clearStatus (header.go:163-165,189-191,235-237)
   uint8_t* p = t->ring + header_pos(t, h);
   if (t->version == GPK_TPACKET_V3) {
     __atomic_store_n(reinterpret_cast<uint32_t*>(p + 8), 0u, __ATOMIC_RELEASE);
@@ -247,7 +247,7 @@ struct Call {
     return -1;
   }
 
-  // getTPacketHeader (afpacket.go:469-492)
+  // getTPacketHeader (afpacket.go:462-486)
   int get_header() {
     GoState& s = t->s;
     if (t->version == GPK_TPACKET_V3) {
@@ -268,7 +268,7 @@ struct Call {
     return 0;
   }
 
-  // the v3 next() step (header.go:249-263); v1/v2 next() is always false
+  // the v3 next() step (header.go:254-268); v1/v2 next() is always false
   bool next() {
     GoState& s = t->s;
     if (t->version != GPK_TPACKET_V3) return false;
@@ -287,13 +287,13 @@ struct Call {
     return true;
   }
 
-  void release_current() {  // releaseCurrentPacket (afpacket.go:353-358)
+  void release_current() {  // releaseCurrentPacket (afpacket.go:316-321)
     releases->push_back(t->s.cur_hdr);
     t->s.offset++;
     t->s.should_release = false;
   }
 
-  // pollForFirstPacket (afpacket.go:494-523): 1 = ready, 0 = wait, -1 = error
+  // pollForFirstPacket (afpacket.go:488-516): 1 = ready, 0 = wait, -1 = error
   int poll_first() {
     GoState& s = t->s;
     const uint64_t h = s.cur_hdr;
@@ -636,7 +636,7 @@ void set_err(char* err, size_t cap, const std::string& s) {
 
 extern "C" {
 
-void gpk_tp_default_opts(gpk_tp_opts* o) {  // defaultOpts (options.go:105-114)
+void gpk_tp_default_opts(gpk_tp_opts* o) {  // defaultOpts (options.go:149-158)
   memset(o, 0, sizeof(*o));
   o->frame_size = 4096;
   o->block_size = 4096 * 128;
@@ -735,7 +735,7 @@ int gpk_tpacket_new(gpk_tpacket** out, const gpk_tp_opts* o, char* err, size_t c
   sll.sll_protocol = htons(oc.protocol);
   sll.sll_ifindex = ifindex;
   if (bind(fd, (struct sockaddr*)&sll, sizeof(sll)) < 0) return fail(strerror(errno));
-  // setRequestedTPacketVersion (:183-196)
+  // setRequestedTPacketVersion (:182-194)
   int version = -1;
   for (int v = GPK_TPACKET_V3; v >= GPK_TPACKET_V1; v--) {
     if (oc.version != GPK_TPACKET_HIGHEST && oc.version != v) continue;
@@ -751,7 +751,7 @@ int gpk_tpacket_new(gpk_tpacket** out, const gpk_tp_opts* o, char* err, size_t c
     if (setsockopt(fd, SOL_PACKET, PACKET_VNET_HDR, &val, sizeof(val)) < 0)
       return fail(std::string("setsockopt packet_vnet_hdr_sz: ") + strerror(errno));
   }
-  // setUpRing (:207-244)
+  // setUpRing (:205-240)
   const uint64_t total = (uint64_t)oc.frames_per_block * oc.num_blocks * oc.frame_size;
   if (version == GPK_TPACKET_V3) {
     struct tpacket_req3 req;
@@ -968,7 +968,7 @@ int gpk_tpacket_stats(const gpk_tpacket* t, int64_t* packets, int64_t* polls) {
 
 int gpk_tpacket_socket_stats(gpk_tpacket* t, uint32_t* packets, uint32_t* drops, uint32_t* freeze_q) {
   if (!t) return GPK_EINVAL;
-  if (t->fd >= 0) {  // the kernel clears its counters on every read: accumulate (afpacket.go:395-431)
+  if (t->fd >= 0) {  // the kernel clears its counters on every read: accumulate (afpacket.go:378-431)
     struct tpacket_stats_v3 st{};
     socklen_t sl = t->version == GPK_TPACKET_V3 ? sizeof(struct tpacket_stats_v3) : sizeof(struct tpacket_stats);
     if (getsockopt(t->fd, SOL_PACKET, PACKET_STATISTICS, &st, &sl) < 0) return GPK_EINVAL;
@@ -1088,6 +1088,14 @@ static int tpacket_pump(gpk_ctx* ctx, const gpk_parser* parser, gpk_tpacket* t, 
   uint64_t packet_index = 0;
   const double t0 = now_s();
   int rc = GPK_OK;
+  // gpk_stop: from its first check after a stop no callback is made
+  const uint64_t stop0 = gpk_ctx_stop_seq(ctx);
+  bool stopped = false;
+  uint64_t delivered = 0;
+  auto stop_seen = [&]() {
+    if (!stopped && gpk_ctx_stop_seq(ctx) != stop0) stopped = true;
+    return stopped;
+  };
 
   auto release_done = [&](bool block) {  // hand back headers whose HtoD has completed
     if (hold) return true;  // ... only once delivered (deliver_oldest)
@@ -1115,13 +1123,15 @@ static int tpacket_pump(gpk_ctx* ctx, const gpk_parser* parser, gpk_tpacket* t, 
     float ms = 0, kms = 0;
     if (hipEventElapsedTime(&ms, b.e0, b.done) == hipSuccess) st->gpu_s += ms * 1e-3;
     if (hipEventElapsedTime(&kms, b.k0, b.k1) == hipSuccess) st->kernel_s += kms * 1e-3;
-    if (hold) {  // the packets: ring frames, or this slot's VLAN copies (h_off moved for the device mirror)
+    const bool deliver = !stop_seen();  // a batch is delivered whole or not at all
+    if (deliver) delivered += b.n;
+    if (deliver && hold) {  // the packets: ring frames, or this slot's VLAN copies (h_off moved for the device mirror)
       for (uint64_t i = 0; i < b.n; i++)
         ptrs[i] = b.h_off[i] < ring_bytes ? t->ring + b.h_off[i] : b.h_side + (b.h_off[i] - ring_bytes - s * side_cap);
       opt.packets_cb(user, b.first, b.n, ptrs.data(), b.h_cap);
     }
-    if (with_fields) opt.fields_cb(user, b.first, b.n, b.h_fields);
-    if (cb) cb(user, b.first, b.n, b.h_rec, b.h_err, b.h_flow, b.h_ci, b.h_cap);
+    if (deliver && with_fields) opt.fields_cb(user, b.first, b.n, b.h_fields);
+    if (deliver && cb) cb(user, b.first, b.n, b.h_rec, b.h_err, b.h_flow, b.h_ci, b.h_cap);
     if (hold && b.h2d_pending) {  // delivered: the headers go back to the kernel
       b.h2d_pending = false;
       gpk_tpacket_release(t, b.rel_seq);
@@ -1131,7 +1141,7 @@ static int tpacket_pump(gpk_ctx* ctx, const gpk_parser* parser, gpk_tpacket* t, 
   };
 
   int slot = 0;
-  while (good) {
+  while (good && !stop_seen()) {
     if (opt.max_packets && packet_index >= opt.max_packets) break;
     // a free slot
     while (B[slot].inflight && good) good = deliver_oldest();
@@ -1274,10 +1284,11 @@ static int tpacket_pump(gpk_ctx* ctx, const gpk_parser* parser, gpk_tpacket* t, 
     if (r == GPK_TP_ERROR) break;
   }
   while (good && !order.empty()) good = deliver_oldest();
-  (void)hipDeviceSynchronize();
+  for (auto& b : B)  // this pump's copies out of the ring have finished (other streams' work is not waited for)
+    if (b.stream) (void)hipStreamSynchronize(b.stream);
   gpk_tpacket_release(t, UINT64_MAX);
   t->defer = was_deferred;
-  st->packets = packet_index;
+  st->packets = stopped ? delivered : packet_index;
   st->wall_s = now_s() - t0;
   if (registered) (void)hipHostUnregister(t->ring);
   for (auto& b : B) {
@@ -1296,7 +1307,7 @@ static int tpacket_pump(gpk_ctx* ctx, const gpk_parser* parser, gpk_tpacket* t, 
     snprintf(st->error, sizeof(st->error), "%s", herr.c_str());
     return GPK_EHIP;
   }
-  return rc;
+  return stopped && rc == GPK_OK ? GPK_STOPPED : rc;
 }
 
 // The C entry point: no C++ exception crosses it (a thread or an allocation

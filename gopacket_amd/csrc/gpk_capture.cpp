@@ -16,15 +16,15 @@
 // from a snapshot taken lazily at the first mutation — and indexing stops
 // there: the caller re-presents the rest with more bytes appended.
 //
-// Reference functions (pcapgo/): NewNgReader ngread.go:64-106, readBytes
-// :112-126, discard :128-137, readBlock :170-196, readOption :199-236,
-// readSectionHeader :240-305, skipSection :308-320, firstInterface :330-369,
-// readInterfaceDescriptor :372-436, convertTime :439-443,
-// readInterfaceStatistics :446-492, readPacketHeader :497-582,
-// readPacketOptions :584-632, ReadPacketDataWithOptions :642-675,
-// readNameResolutionBlock ngread_nrb.go:63-130, readDecryptionSecretsBlock
-// ngread_dsb.go:17-39; NewReader/readHeader read.go:64-122, ReadPacketData
-// :124-140, readPacketHeader :171-180.
+// Reference functions (pcapgo/): NewNgReader ngread.go:64-107, readBytes
+// :113-126, discard :128-137, readBlock :165-193, readOption :196-234,
+// readSectionHeader :238-312, skipSection :315-327, firstInterface :338-373,
+// readInterfaceDescriptor :376-437, convertTime :440-443,
+// readInterfaceStatistics :446-489, readPacketHeader :494-580,
+// readPacketOptions :582-625, ReadPacketDataWithOptions :636-664,
+// readNameResolutionBlock ngread_nrb.go:64-130, readDecryptionSecretsBlock
+// ngread_dsb.go:18-39; NewReader/readHeader read.go:65-119, ReadPacketData
+// :122-137, readPacketHeader :169-177.
 #include <algorithm>
 #include <condition_variable>
 #include <cstdarg>
@@ -124,6 +124,28 @@ struct NgState {  // what a rollback restores
   uint16_t link_type = 0;
   bool first_section_found = false, active_section = false;
   std::vector<std::pair<Section, std::vector<Iface>>> ended;
+  std::vector<uint64_t> ended_at;   // packets returned before each SectionEndCallback call
+  std::vector<uint64_t> ended_seq;  // ... and its place among all the reader's callbacks
+  uint64_t ncb = 0;                 // SectionEndCallback + StatisticsCallback calls so far
+};
+
+// One NgNameRecord (pcapng.go NgNameRecord; readNameResolutionBlock,
+// ngread_nrb.go:64-130): IPv4 / IPv6 addresses as their 4 / 16 bytes, EUI
+// addresses as the 24 bytes newHWAddress clones (the reader's whole scratch
+// buffer, ngread_nrb.go:56-61), and the names with their NULs trimmed.
+struct NameRec {
+  uint16_t rtype = 0;
+  uint8_t addr[24] = {0};
+  uint32_t alen = 0;
+  std::vector<std::string> names;
+};
+
+// One StatisticsCallback call (ngread.go:485-487): the interface id and the
+// statistics as the block left them, after `at` packets were returned.
+struct StatEvent {
+  uint64_t at = 0, seq = 0;
+  uint32_t iface = 0;
+  Stats stats;
 };
 
 struct OptBuf {  // NgReader.currentOption.value: backing array + length
@@ -159,6 +181,20 @@ struct gpk_capreader {
   // chunking, so a byte-range replay can tell whether its range changed any
   // reader state (gpk_replay_file_range)
   uint64_t mutations = 0;
+  // NgReader.buf, the 24-byte scratch buffer block and option headers are read
+  // into (EUI name records clone all of it); undone with a rolled-back call
+  uint8_t gobuf[24] = {0};
+  uint64_t npk = 0;  // packets returned so far (by gpk_capreader_index / _index_all)
+  // name records of the current section (NgReader.nameRecords), snapshot like opt
+  std::vector<NameRec> names, names_snap;
+  bool names_saved = false;
+  std::vector<StatEvent> stat_events;  // every StatisticsCallback call so far
+  // gpk_capreader_keep_options: the options of the packets of the last index
+  // call, as records {u16 code, u16 0, u32 len, value padded to 4}
+  bool keep_opts = false;
+  std::vector<uint8_t> opt_arena;
+  std::vector<uint64_t> opt_at;  // packet k's records: opt_arena[opt_at[k], opt_at[k+1])
+  bool pending_skip = false;     // gpk_capreader_skip_section: SkipSection first
   uint32_t typ = 0, blen = 0;  // currentBlock
   uint16_t opt_code = 0;
   // ci of the current call
@@ -191,6 +227,14 @@ struct gpk_capreader {
     pos += m;
     return p;
   }
+  // readBytes(r.buf[:m]) (ngread.go:113-126): the bytes land in NgReader.buf
+  // (partly when the stream ends first, with the error)
+  const uint8_t* read_gobuf(uint64_t m) {
+    if (m > avail() && eof) to_gobuf(0, b + pos, avail());
+    const uint8_t* p = read_view(m);
+    to_gobuf(0, p, m);
+    return p;
+  }
   void discard(uint64_t m) {  // NgReader.discard
     if (m > avail()) {
       if (!eof) throw NeedMore{};
@@ -215,20 +259,36 @@ struct gpk_capreader {
       opt_saved = true;
     }
   }
+  // name records are no state a later packet depends on (no mutation counted:
+  // a byte-range replay may split across them)
+  void touch_names() {
+    if (!names_saved) {
+      names_snap = names;
+      names_saved = true;
+    }
+  }
+  // bytes readBytes put into NgReader.buf[at, at + m)
+  void to_gobuf(uint32_t at, const uint8_t* p, uint64_t m) {
+    if (m) memcpy(gobuf + at, p, m);
+  }
 
   // ---- pcapng --------------------------------------------------------------
   void read_block() {
     if (avail() < 8) {
       if (!eof) throw NeedMore{};
       uint64_t k = avail();
+      to_gobuf(0, b + pos, k);
       pos = n;
       fail(k == 0 ? kEOF : kUnexpectedEOF);
     }
     const uint8_t* h = b + pos;
     pos += 8;
+    to_gobuf(0, h, 8);
     typ = ld32(h, be());
     if (typ == kSHB) {
+      if (avail() < 4 && eof) to_gobuf(8, b + pos, avail());
       const uint8_t* m = read_view(4);
+      to_gobuf(8, m, 4);
       bool nbe;
       if (ld32(m, true) == kByteOrderMagic)
         nbe = true;
@@ -251,7 +311,7 @@ struct gpk_capreader {
       opt_code = 0;
       return;
     }
-    const uint8_t* h = read_view(4);
+    const uint8_t* h = read_gobuf(4);
     blen -= 4;
     opt_code = ld16(h, be());
     uint16_t olen = ld16(h + 2, be());
@@ -282,11 +342,17 @@ struct gpk_capreader {
 
   void read_section_header() {
     touch();
-    if (st.active_section) st.ended.emplace_back(st.section, st.ifaces);
+    if (st.active_section) {
+      st.ended.emplace_back(st.section, st.ifaces);
+      st.ended_at.push_back(npk);
+      st.ended_seq.push_back(st.ncb++);
+    }
     st.ifaces.clear();
+    touch_names();
+    names.clear();
     st.active_section = false;
     for (;;) {  // RESTART
-      const uint8_t* h = read_view(12);
+      const uint8_t* h = read_gobuf(12);
       blen -= 12;
       uint16_t vmaj = ld16(h, be()), vmin = ld16(h + 2, be());
       if (vmaj != 1 || vmin != 0) {
@@ -354,7 +420,7 @@ struct gpk_capreader {
   }
 
   void read_interface_descriptor() {
-    const uint8_t* h = read_view(8);
+    const uint8_t* h = read_gobuf(8);
     blen -= 8;
     Iface it;
     it.link_type = ld16(h, be());
@@ -393,7 +459,7 @@ struct gpk_capreader {
     st.ifaces.push_back(std::move(it));
   }
 
-  // convertTime (ngread.go:439-443) in uint64 arithmetic. The common
+  // convertTime (ngread.go:440-443) in uint64 arithmetic. The common
   // resolutions divide by constants (multiply-shift) or shift: a 64-bit
   // hardware divide per packet would dominate the record walk.
   void convert_time(uint32_t idx, uint64_t ts, int64_t* s, uint32_t* ns) const { iface_time(st.ifaces[idx], ts, s, ns); }
@@ -422,7 +488,7 @@ struct gpk_capreader {
   }
 
   void read_interface_statistics() {
-    const uint8_t* h = read_view(12);
+    const uint8_t* h = read_gobuf(12);
     blen -= 12;
     uint32_t idx = ld32(h, be());
     uint64_t ts = (uint64_t)ld32(h + 4, be()) << 32 | ld32(h + 8, be());
@@ -447,13 +513,18 @@ struct gpk_capreader {
       }
     }
     discard(blen);
+    StatEvent ev;  // StatisticsCallback(ifaceID, *stats)
+    ev.at = npk;
+    ev.seq = st.ncb++;  // (st was saved by touch() above)
+    ev.iface = idx;
+    ev.stats = st.ifaces[idx].stats;
+    stat_events.push_back(std::move(ev));
   }
 
   void read_decryption_secrets() {
-    uint8_t h[8];
-    if (read_into(h, 8) < 8) fail(fmt("could not read DecryptionSecret Header block length: %s", kUnexpectedEOF));
+    if (read_into(gobuf, 8) < 8) fail(fmt("could not read DecryptionSecret Header block length: %s", kUnexpectedEOF));
     blen -= 8;
-    uint32_t slen = ld32(h + 4, be());
+    uint32_t slen = ld32(gobuf + 4, be());
     if (read_into(nullptr, slen) < slen)
       fail(fmt("could not read %u bytes from DecryptionSecret payload: %s", slen, kUnexpectedEOF));
     blen -= slen;
@@ -461,25 +532,30 @@ struct gpk_capreader {
 
   void read_name_resolution() {
     while (blen > 0) {
-      uint8_t h[4];
-      if (read_into(h, 4) < 4) fail(fmt("could not read NameRecord Header block length: %s", kUnexpectedEOF));
+      if (read_into(gobuf, 4) < 4) fail(fmt("could not read NameRecord Header block length: %s", kUnexpectedEOF));
       blen -= 4;
-      uint16_t rtype = ld16(h, be()), rlen = ld16(h + 2, be());
+      uint16_t rtype = ld16(gobuf, be()), rlen = ld16(gobuf + 2, be());
       int64_t length = rlen < (int64_t)blen ? (int64_t)rlen : (int64_t)blen;
       int64_t padding = length % 4 ? 4 - length % 4 : 0;
       int64_t alen;
+      NameRec rec;
+      rec.rtype = rtype;
       if (rtype == 1 || rtype == 2) {
         uint64_t m = rtype == 1 ? 4 : 16;
-        if (read_into(nullptr, m) < m)
+        if (read_into(gobuf, m) < m)
           fail(fmt("could not read %s address: could not read IP address: %s", rtype == 1 ? "IPv4" : "IPv6",
                    kUnexpectedEOF));
-        alen = (int64_t)m;
+        alen = (int64_t)m;  // netip.AddrFromSlice(r.buf[:m])
+        memcpy(rec.addr, gobuf, m);
+        rec.alen = (uint32_t)m;
       } else if (rtype == 3 || rtype == 4) {
         uint64_t m = rtype == 3 ? 6 : 8;
-        if (read_into(nullptr, m) < m)
+        if (read_into(gobuf, m) < m)
           fail(fmt("could not read %s address: could not read EUI address: %s", rtype == 3 ? "EUI-48" : "EUI-64",
                    kUnexpectedEOF));
         alen = 24;  // newHWAddress(r.buf[:]) clones the whole 24-byte buffer
+        memcpy(rec.addr, gobuf, 24);
+        rec.alen = 24;
       } else if (rtype == 0) {
         break;
       } else {
@@ -503,9 +579,13 @@ struct gpk_capreader {
           fail(fmt("could not read name: %s", kEOF));
         }
         uint64_t k = (const uint8_t*)z - (b + pos) + 1;
+        // string(bytes.Trim(bstr, "\x00")): the NUL is last, and NULs can only lead when the name is empty
+        rec.names.emplace_back((const char*)b + pos, k - 1);
         pos += k;
         length -= (int64_t)k;
       }
+      touch_names();
+      names.push_back(std::move(rec));
       discard((uint64_t)padding);
     }
     discard(blen);
@@ -516,7 +596,7 @@ struct gpk_capreader {
       for (;;) {  // FIND_PACKET
         read_block();
         if (typ == kEPB) {
-          const uint8_t* h = read_view(20);
+          const uint8_t* h = read_gobuf(20);
           blen -= 20;
           uint32_t idx = ld32(h, be());
           if (idx >= st.ifaces.size())
@@ -527,7 +607,7 @@ struct gpk_capreader {
           ci_len = ld32(h + 16, be());
           break;
         } else if (typ == kSPB) {
-          const uint8_t* h = read_view(4);
+          const uint8_t* h = read_gobuf(4);
           blen -= 4;
           ci_s = kZeroTimeSec;
           ci_ns = 0;
@@ -544,7 +624,7 @@ struct gpk_capreader {
         } else if (typ == kSHB) {
           read_section_header();
         } else if (typ == kPB) {
-          const uint8_t* h = read_view(20);
+          const uint8_t* h = read_gobuf(20);
           blen -= 20;
           uint32_t idx = ld16(h, be());
           if (idx >= st.ifaces.size())
@@ -580,6 +660,14 @@ struct gpk_capreader {
         fail(fmt("runtime error: index out of range [3] with length %u", opt.len), true);
       if ((opt_code == 4 || opt_code == 5) && opt.len < 8)  // binary.LittleEndian.Uint64: _ = b[7]
         fail(fmt("runtime error: index out of range [7] with length %u", opt.len), true);
+      if (keep_opts) {  // the option as readPacketOptions saw it (its value: the reused buffer's)
+        const size_t at = opt_arena.size(), padded = (opt.len + 3u) & ~3u;
+        opt_arena.resize(at + 8 + padded, 0);
+        uint8_t* q = opt_arena.data() + at;
+        memcpy(q, &opt_code, 2);
+        memcpy(q + 4, &opt.len, 4);
+        memcpy(q + 8, opt.back.data(), opt.len);
+      }
     }
   }
 
@@ -696,6 +784,10 @@ int gpk_capreader_index(gpk_capreader* r, const uint8_t* buf, uint64_t len, int 
   if (!r || (!buf && len) || !offsets || !caplens || !n_pkts || !consumed) return GPK_EINVAL;
   *n_pkts = 0;
   *consumed = 0;
+  if (r->keep_opts) {  // the options of this call's packets only
+    r->opt_arena.clear();
+    r->opt_at.assign(1, 0);
+  }
   if (r->open_failed) return GPK_CAP_END;  // NewReader/NewNgReader failed: no reader
   r->b = buf;
   r->n = len;
@@ -705,37 +797,78 @@ int gpk_capreader_index(gpk_capreader* r, const uint8_t* buf, uint64_t len, int 
   const bool mixed = (r->flags & GPK_NG_WANT_MIXED_LINKTYPE) != 0;
   uint64_t k = 0;
   int status = GPK_CAP_MORE;
+  // One reference call (NewNgReader, SkipSection or ReadPacketData) at a time:
+  // run() undoes everything a call changed when it needs bytes beyond buf.
+  struct Undo {
+    uint64_t start, m0;
+    size_t ev0, oa0;
+    uint8_t gb0[24];
+  };
+  auto begin = [r](Undo& u) {
+    u.start = r->pos;
+    u.m0 = r->mutations;
+    u.ev0 = r->stat_events.size();
+    u.oa0 = r->opt_arena.size();
+    memcpy(u.gb0, r->gobuf, 24);
+    r->st_saved = r->opt_saved = r->names_saved = false;
+  };
+  auto undo = [r](const Undo& u) {
+    if (r->st_saved) r->st = std::move(r->st_snap);
+    if (r->opt_saved) r->opt = std::move(r->opt_snap);
+    if (r->names_saved) r->names = std::move(r->names_snap);
+    r->stat_events.resize(u.ev0);
+    r->opt_arena.resize(u.oa0);
+    memcpy(r->gobuf, u.gb0, 24);
+    r->mutations = u.m0;
+    r->pos = u.start;
+  };
+  auto end_with = [r](const GoErr& e) {
+    r->err_text = e.text;
+    r->err_eof = e.text == kEOF;
+    r->err_panic = e.panic;
+  };
   try {
+    Undo u;
     if (!r->opened) {
-      r->st_saved = r->opt_saved = false;
+      begin(u);
       try {
         if (ng)
           r->ng_open();
         else
           r->pcap_open();
       } catch (NeedMore&) {
-        r->st = NgState();
-        r->opt = OptBuf();
-        r->mutations = 0;
-        r->pos = 0;
+        undo(u);
         throw;
       } catch (GoErr& e) {
         r->open_failed = true;
-        r->err_text = e.text;
-        r->err_eof = e.text == kEOF;
-        r->err_panic = e.panic;
+        end_with(e);
         *consumed = r->pos;
         return GPK_CAP_END;
       }
       r->opened = true;
+    }
+    if (r->pending_skip) {  // NgReader.SkipSection (ngread.go:330-335)
+      begin(u);
+      try {
+        r->skip_section();
+        r->read_section_header();
+        r->pending_skip = false;
+      } catch (NeedMore&) {
+        undo(u);
+        throw;
+      } catch (GoErr& e) {
+        r->pending_skip = false;
+        end_with(e);
+        *consumed = r->pos;
+        return GPK_CAP_END;
+      }
     }
     for (;;) {
       if (k == max_pkts) {
         status = GPK_CAP_FULL;
         break;
       }
-      const uint64_t start = r->pos, m0 = r->mutations;
-      r->st_saved = r->opt_saved = false;
+      begin(u);
       try {
         const uint64_t off = ng ? r->ng_read_packet() : r->pcap_read_packet();
         offsets[k] = off;
@@ -748,17 +881,14 @@ int gpk_capreader_index(gpk_capreader* r, const uint8_t* buf, uint64_t len, int 
           ci[k].link_type = (ng && mixed) ? (int32_t)r->st.ifaces[r->ci_iface].link_type : -1;
         }
         k++;
+        r->npk++;
+        if (r->keep_opts) r->opt_at.push_back(r->opt_arena.size());
       } catch (NeedMore&) {
-        if (r->st_saved) r->st = std::move(r->st_snap);
-        if (r->opt_saved) r->opt = std::move(r->opt_snap);
-        r->mutations = m0;
-        r->pos = start;
+        undo(u);
         status = GPK_CAP_MORE;
         break;
       } catch (GoErr& e) {
-        r->err_text = e.text;
-        r->err_eof = e.text == kEOF;
-        r->err_panic = e.panic;
+        end_with(e);
         status = GPK_CAP_END;
         break;
       }
@@ -873,6 +1003,91 @@ int gpk_capreader_interface_str(const gpk_capreader* r, int s, int i, int field,
     case GPK_IFACE_STATS_COMMENT: return put_str(it.stats.comment, buf, cap);
   }
   return GPK_EINVAL;
+}
+
+int gpk_capreader_nnames(const gpk_capreader* r) {
+  if (!r || r->format != GPK_CAP_PCAPNG) return GPK_EINVAL;
+  return (int)r->names.size();
+}
+
+int gpk_capreader_name(const gpk_capreader* r, int i, int* kind, uint8_t* addr, int* addr_len, int* nnames,
+                       char* names, size_t cap) {
+  if (!r || r->format != GPK_CAP_PCAPNG || i < 0 || i >= (int)r->names.size()) return GPK_EINVAL;
+  const NameRec& x = r->names[(size_t)i];
+  if (kind) *kind = x.rtype;
+  if (addr) memcpy(addr, x.addr, x.alen);
+  if (addr_len) *addr_len = (int)x.alen;
+  if (nnames) *nnames = (int)x.names.size();
+  size_t need = 0;
+  for (const auto& nm : x.names) {
+    if (names && need + nm.size() + 1 <= cap) {
+      memcpy(names + need, nm.data(), nm.size());
+      names[need + nm.size()] = 0;
+    }
+    need += nm.size() + 1;
+  }
+  return (int)need;
+}
+
+int gpk_capreader_nstat_events(const gpk_capreader* r) {
+  if (!r || r->format != GPK_CAP_PCAPNG) return GPK_EINVAL;
+  return (int)r->stat_events.size();
+}
+
+int gpk_capreader_stat_event(const gpk_capreader* r, int k, uint64_t* at, uint64_t* seq, int* iface,
+                             gpk_ng_interface* stats, char* comment, size_t cap) {
+  if (!r || r->format != GPK_CAP_PCAPNG || k < 0 || k >= (int)r->stat_events.size()) return GPK_EINVAL;
+  const StatEvent& e = r->stat_events[(size_t)k];
+  if (at) *at = e.at;
+  if (seq) *seq = e.seq;
+  if (iface) *iface = (int)e.iface;
+  if (stats) {
+    memset(stats, 0, sizeof(*stats));
+    stats->has_statistics = 1;
+    stats->last_update_sec = e.stats.lu_s;
+    stats->last_update_nsec = e.stats.lu_ns;
+    stats->start_time_sec = e.stats.st_s;
+    stats->start_time_nsec = e.stats.st_ns;
+    stats->end_time_sec = e.stats.et_s;
+    stats->end_time_nsec = e.stats.et_ns;
+    stats->packets_received = e.stats.received;
+    stats->packets_dropped = e.stats.dropped;
+  }
+  return put_str(e.stats.comment, comment, cap);
+}
+
+int gpk_capreader_section_end_at(const gpk_capreader* r, int s, uint64_t* at, uint64_t* seq) {
+  if (!r || r->format != GPK_CAP_PCAPNG || s < 0 || s >= (int)r->st.ended_at.size()) return GPK_EINVAL;
+  if (at) *at = r->st.ended_at[(size_t)s];
+  if (seq) *seq = r->st.ended_seq[(size_t)s];
+  return GPK_OK;
+}
+
+int gpk_capreader_skip_section(gpk_capreader* r) {
+  if (!r || r->format != GPK_CAP_PCAPNG || r->open_failed) return GPK_EINVAL;
+  r->pending_skip = true;
+  return GPK_OK;
+}
+
+int gpk_capreader_set_snaplen(gpk_capreader* r, uint32_t snaplen) {
+  if (!r || r->format != GPK_CAP_PCAP) return GPK_EINVAL;
+  r->snaplen = snaplen;
+  return GPK_OK;
+}
+
+int gpk_capreader_keep_options(gpk_capreader* r, int on) {
+  if (!r) return GPK_EINVAL;
+  r->keep_opts = on != 0;
+  r->opt_arena.clear();
+  r->opt_at.assign(1, 0);
+  return GPK_OK;
+}
+
+int gpk_capreader_packet_options(const gpk_capreader* r, uint64_t i, const uint8_t** tlv, uint64_t* bytes) {
+  if (!r || !r->keep_opts || !tlv || !bytes || i + 1 >= r->opt_at.size()) return GPK_EINVAL;
+  *tlv = r->opt_arena.data() + r->opt_at[i];
+  *bytes = r->opt_at[i + 1] - r->opt_at[i];
+  return GPK_OK;
 }
 
 }  // extern "C"
@@ -1044,11 +1259,11 @@ class Pool {
   bool stop_ = false;
 };
 
-// What ReadPacketData does on a plain EPB at b[p] (ngread.go:497-527, 642-675):
+// What ReadPacketData does on a plain EPB at b[p] (ngread.go:494-514, 642-675):
 // block header; 20-byte EPB header; interface known (else an error) and, without
 // WantMixedLinkType, of the first interface's link type (else the block is
 // skipped); data + padding; the 4 bytes left make readOption return end of
-// options at once (ngread.go:201-204); discard(4). No state changes. "Plain":
+// options at once (ngread.go:197-201); discard(4). No state changes. "Plain":
 // total length == 32 + caplen + padding (no options) and the block inside
 // b[p, end). Returns the block length, 0 for anything else.
 uint32_t plain_epb(const NgState& st, uint32_t flags, const uint8_t* b, uint64_t p, uint64_t end, uint64_t* off,
@@ -1253,6 +1468,10 @@ extern "C" int gpk_capreader_index_all(gpk_capreader* r, const uint8_t* buf, uin
             pieces.push_back({&s.v, 0, s.v.n, total});
             total += s.v.n;
             pos = s.end;
+            // what the exact reader would have left: the packets counted, and
+            // NgReader.buf holding the last block's 20-byte EPB header
+            r->npk += s.v.n;
+            if (s.v.n) r->to_gobuf(0, buf + s.v.off[s.v.n - 1] - 20, 20);
           }
         }
         if (!done) {  // the rest of the slot, exactly

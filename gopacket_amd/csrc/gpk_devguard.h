@@ -12,6 +12,7 @@
 #define GPK_DEVGUARD_H
 
 #include <hip/hip_runtime.h>
+#include <stdint.h>
 
 namespace gpk {
 
@@ -38,5 +39,8 @@ struct DeviceScope {
 // The device of a context (gpk_host.cpp), for the library's own pipelines.
 struct gpk_ctx;
 extern "C" __attribute__((visibility("hidden"))) int gpk_ctx_device(const gpk_ctx* c);
+// How many times gpk_stop was called on the context: a replay or pump takes it
+// when it starts and ends early once it has changed.
+extern "C" __attribute__((visibility("hidden"))) uint64_t gpk_ctx_stop_seq(const gpk_ctx* c);
 
 #endif  // GPK_DEVGUARD_H

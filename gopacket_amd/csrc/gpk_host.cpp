@@ -122,6 +122,7 @@ struct gpk_ctx {
   // gpk_replay_file's staging buffers, kept for the next call (gpk_walk.h)
   void* replay_cache = nullptr;
   void (*replay_cache_free)(void*) = nullptr;
+  std::atomic<uint64_t> stop_seq{0};  // gpk_stop calls so far
 };
 
 void* gpk_ctx_replay_take(gpk_ctx* c) {
@@ -166,6 +167,14 @@ int gpk_abi_version(void) { return GPK_ABI_VERSION; }
 
 int gpk_ctx_device(const gpk_ctx* c) { return c ? c->device : -1; }
 
+uint64_t gpk_ctx_stop_seq(const gpk_ctx* c) { return c ? c->stop_seq.load() : 0; }
+
+int gpk_stop(gpk_ctx* c) {
+  if (!c) return GPK_EINVAL;
+  c->stop_seq.fetch_add(1);
+  return GPK_OK;
+}
+
 const char* gpk_strerror(int status) {
   switch (status) {
     case GPK_OK: return "ok";
@@ -174,6 +183,7 @@ const char* gpk_strerror(int status) {
     case GPK_EHIP: return "HIP runtime error";
     case GPK_ENODEV: return "no such device";
     case GPK_EUNSUPP: return "unsupported configuration";
+    case GPK_STOPPED: return "stopped";
     default: return "unknown status";
   }
 }

@@ -3,8 +3,8 @@
 // host memory.
 //
 // The reference loop this replaces (examples/pcapdump, gopacket_benchmark):
-//   r, _ := pcapgo.NewNgReader(f, opts)            pcapgo/ngread.go:64-106
-//   for { data, ci, err := r.ReadPacketData()      ngread.go:636-640
+//   r, _ := pcapgo.NewNgReader(f, opts)            pcapgo/ngread.go:64-107
+//   for { data, ci, err := r.ReadPacketData()      ngread.go:629-632
 //         parser.DecodeLayers(data, &decoded)      parser.go:303-317
 //         ... VerifyChecksum / Flow.FastHash }
 //
@@ -243,6 +243,16 @@ struct Pipeline {
   void* user = nullptr;
   gpk_replay_stats* st = nullptr;
   std::string herr;
+  // gpk_stop: the context and its stop count when the call started; once it
+  // has changed no callback is made and the rest only drains
+  const gpk_ctx* ctx = nullptr;
+  uint64_t stop0 = 0;
+  bool stopped = false;
+  uint64_t delivered = 0;  // packets whose callbacks were made
+  bool stop_seen() {
+    if (!stopped && gpk_ctx_stop_seq(ctx) != stop0) stopped = true;
+    return stopped;
+  }
   // first call: the slots' and batches' buffers are allocated in the
   // background (slot 0 and the first two batches first, the rest behind
   // them while slot 0 is read); the read of a slot and the first use of a
@@ -265,13 +275,17 @@ struct Pipeline {
     if (hipEventElapsedTime(&ms, B.e0, B.done) == hipSuccess) st->gpu_s += ms * 1e-3;
     if (hipEventElapsedTime(&kms, B.k0, B.k1) == hipSuccess) st->kernel_s += kms * 1e-3;
     double t = now_s();
-    for (uint64_t i = 0; i < B.n; i++) st->packet_bytes += B.h_cap[i];
-    if (packets_cb && B.base) packets_cb(user, B.first, B.n, B.base, B.base_bytes, B.h_off, B.h_cap);
+    const bool deliver = !stop_seen();  // a batch is delivered whole or not at all
+    if (deliver) {
+      for (uint64_t i = 0; i < B.n; i++) st->packet_bytes += B.h_cap[i];
+      delivered += B.n;
+    }
+    if (deliver && packets_cb && B.base) packets_cb(user, B.first, B.n, B.base, B.base_bytes, B.h_off, B.h_cap);
     if (B.slot >= 0 && (size_t)B.slot < slot_batches.size()) slot_batches[B.slot]--;
     B.slot = -1;
     B.base = nullptr;
-    if (fields_cb && B.with_fields) fields_cb(user, B.first, B.n, B.h_fields);  // before the batch's results
-    if (cb) cb(user, B.first, B.n, B.h_rec, B.h_err, B.h_flow, B.h_ci, B.h_cap);
+    if (deliver && fields_cb && B.with_fields) fields_cb(user, B.first, B.n, B.h_fields);  // before the batch's results
+    if (deliver && cb) cb(user, B.first, B.n, B.h_rec, B.h_err, B.h_flow, B.h_ci, B.h_cap);
     st->deliver_s += now_s() - t;
     free_bats.push_back(b);
     return true;
@@ -541,6 +555,7 @@ static int plan_range(Src& src, uint32_t ng_flags, gpk_replay_range* rg, uint64_
 static int replay_file(gpk_ctx* ctx, const gpk_parser* parser, const char* path, const gpk_replay_opts* o,
                        gpk_replay_cb cb, void* user, gpk_replay_stats* stats, gpk_replay_range* rg) {
   const double t_start = now_s();
+  const uint64_t stop0 = gpk_ctx_stop_seq(ctx);  // gpk_stop calls from here on end this call
   gpk_replay_opts opt{0, 0, 256ull << 20, 4, 1ull << 20, 8, nullptr, nullptr};
   if (o) {
     opt.fields_cb = o->fields_cb;
@@ -597,7 +612,7 @@ static int replay_file(gpk_ctx* ctx, const gpk_parser* parser, const char* path,
   stats->file_bytes = src.size;
   uint8_t magic[4] = {0, 0, 0, 0};
   ssize_t mk = pread(src.fd, magic, 4, 0);
-  if (mk >= 2 && magic[0] == 0x1f && magic[1] == 0x8b) {  // read.go:74-84, ngread.go:80-95
+  if (mk >= 2 && magic[0] == 0x1f && magic[1] == 0x8b) {  // read.go:80-86, ngread.go:75-91
     if (src.size < 10) {  // gzip.NewReader: the header read hits EOF
       snprintf(stats->error, sizeof(stats->error), "unexpected EOF");
       stats->reader_status = 1;
@@ -648,6 +663,8 @@ static int replay_file(gpk_ctx* ctx, const gpk_parser* parser, const char* path,
   pl.packets_cb = opt.packets_cb;
   pl.user = user;
   pl.st = stats;
+  pl.ctx = ctx;
+  pl.stop0 = stop0;
   pl.P = opt.batch_pkts;
   const uint64_t P = pl.P;
   // device record walk buffers (pcapng only; GPK_REPLAY_HOST_WALK=1 keeps the walk on the host)
@@ -796,7 +813,7 @@ static int replay_file(gpk_ctx* ctx, const gpk_parser* parser, const char* path,
   rc = GPK_OK;
   pl.slot_batches.assign(pl.slots.size(), 0);
   fill_ahead(1);
-  for (uint64_t si = 0; !finished && good; si++) {
+  for (uint64_t si = 0; !finished && good && !pl.stop_seen(); si++) {
     Slot& S = pl.slots[si % pl.slots.size()];
     const double t_get = now_s();
     const Fill fl = S.fill.get();
@@ -986,7 +1003,7 @@ static int replay_file(gpk_ctx* ctx, const gpk_parser* parser, const char* path,
     }
     const uint64_t pos = start + used, total = G + xi.n;
     bool copied = dwalk;
-    for (uint64_t first = 0; first < total && good;) {  // batches of up to P packets
+    for (uint64_t first = 0; first < total && good && !pl.stop_seen();) {  // batches of up to P packets
       const uint64_t n = std::min<uint64_t>(P, total - first);
       const int b = pl.acquire();
       if (b < 0) {
@@ -1110,7 +1127,8 @@ static int replay_file(gpk_ctx* ctx, const gpk_parser* parser, const char* path,
       s.fill_pending = false;
     }
   const double t_fills = now_s();
-  stats->packets = packet_index;
+  stats->packets = pl.stopped ? pl.delivered : packet_index;
+  if (pl.stopped && rc == GPK_OK) rc = GPK_STOPPED;
   // allocations the call did not reach: one that failed has cost the call
   // nothing (every packet was delivered), so the call succeeds and only the
   // buffers are not kept for the next one
@@ -1121,7 +1139,7 @@ static int replay_file(gpk_ctx* ctx, const gpk_parser* parser, const char* path,
   stats->alloc_wait_s = pl.alloc_wait_ns.load() * 1e-9;
   stats->wall_s = now_s() - t_start;
   if (rg) {
-    rg->clean = good && rc == GPK_OK && clean_eof && stats->stream_bytes == src.size ? 1 : 0;
+    rg->clean = good && rc == GPK_OK && clean_eof && stats->stream_bytes == src.size ? 1 : 0;  // (not when stopped)
     // any change of the reader's state past the leading blocks (a section, an
     // interface, statistics, an option value the next block could reuse)
     rg->state_changed = gpk_capreader_mutations(rd) != hdr_mutations ? 1 : 0;

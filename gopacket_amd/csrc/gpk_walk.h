@@ -25,7 +25,7 @@ constexpr int kWalkMaxIf = 32;
 
 // One interface of the current section, as the walk needs it.
 struct WalkIface {
-  uint64_t second_mask, scale_up, scale_down, tsoff;  // convertTime (ngread.go:439-443)
+  uint64_t second_mask, scale_up, scale_down, tsoff;  // convertTime (ngread.go:440-443)
   int32_t link_type;
   uint32_t plain;  // its EPBs may be plain: known link type rule (WantMixedLinkType or the reader's)
 };

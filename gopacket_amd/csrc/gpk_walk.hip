@@ -18,7 +18,7 @@ __device__ __forceinline__ uint32_t ld32(const uint8_t* b, uint64_t p, uint32_t 
   return be ? __builtin_bswap32(v) : v;
 }
 
-// What ReadPacketData does on a plain EPB at b[p] (ngread.go:497-527,
+// What ReadPacketData does on a plain EPB at b[p] (ngread.go:494-514,
 // 642-675; host twin: gpk_capture.cpp plain_epb): block type 6, total length
 // == 32 + caplen + padding (no options), the block inside b[p, len), a known
 // interface of an allowed link type. Returns the block length, 0 otherwise.
@@ -76,7 +76,7 @@ __global__ void walk_kernel(const uint8_t* b, uint64_t p0, uint64_t len, uint64_
   out.count[k] = n;
 }
 
-// convertTime (ngread.go:439-443) + time.Unix normalisation (host twin:
+// convertTime (ngread.go:440-443) + time.Unix normalisation (host twin:
 // gpk_capreader::iface_time, unix_norm)
 __device__ void iface_time(const WalkIface& it, uint64_t ts, int64_t* s, uint32_t* ns) {
   const uint64_t m = it.second_mask;

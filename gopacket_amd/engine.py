@@ -85,6 +85,12 @@ class Context:
         """_lib.TABLES_AUTO (compact LDS tables when they fit) or TABLES_GLOBAL."""
         check(lib().gpk_ctx_set_table_mode(self.h, int(mode)))
 
+    def stop(self):
+        """gpk_stop: end the replay_file / Pump.run calls running on this
+        context (a Go caller's break out of its ReadPacketData loop); callable
+        from their callbacks or from another thread."""
+        check(lib().gpk_stop(self.h))
+
     def decode_host(self, parser, data, offsets, caplens, layouts=False, fields=False):
         """Host batch in, host results out (copies HtoD, decodes, copies DtoH).
         fields=True: gpk_decode_batch_host_fields, the results gain "fields"
@@ -206,6 +212,10 @@ class Context:
         during the call). byte_range=(begin, end): one caller's share of the
         file (gpk_replay_file_range; end 0 = the file's end); the stats then
         carry "range" (header_end, sync_begin, sync_end, clean, state_changed).
+        A callback that raises ends the call at once (gpk_stop: no further
+        callback), and the exception is raised from here; a callback, or another
+        thread, may also end it with ctx.stop(): stats["stopped"] is then True
+        and the results hold the packets delivered before it.
         Returns (results-or-None, stats dict)."""
         if packets and collect:
             raise ValueError("packets=True hands out views of the staging buffers: use collect=False and on_batch")
@@ -214,13 +224,14 @@ class Context:
 
         raised = []  # an exception inside a ctypes callback would be printed and dropped: kept for after the call
 
-        def guarded(f):  # every callback: the first exception is kept and re-raised after the C call
+        def guarded(f):  # every callback: the first exception is kept, ends the call, and is re-raised after it
             def g(*args):
                 if not raised:
                     try:
                         f(*args)
                     except BaseException as e:  # noqa: B902 (re-raised below, after the C call returns)
                         raised.append(e)
+                        lib().gpk_stop(self.h)  # no further callback: the call drains and returns
             return g
 
         @guarded
@@ -280,7 +291,7 @@ class Context:
                                              ctypes.byref(st))
         if raised:
             raise raised[0]
-        if rc != _lib.GPK_OK:
+        if rc not in (_lib.GPK_OK, _lib.GPK_STOPPED):
             err = _lib.GpkError("gpk_replay_file: %d %s %s" % (rc, st.error.decode(errors="replace"),
                                                               lib().gpk_last_hip_error().decode()))
             if rg is not None:  # where the range was cut, for the caller's redo (shard.replay_file_sharded)
@@ -289,6 +300,7 @@ class Context:
         stats = {k: getattr(st, k) for k, _ in _lib.ReplayStats._fields_}
         stats["error"] = st.error.decode(errors="replace")
         stats["kernel"] = st.kernel.decode(errors="replace")
+        stats["stopped"] = rc == _lib.GPK_STOPPED
         if rg is not None:
             stats["range"] = {k: int(getattr(rg, k)) for k, _ in _lib.ReplayRange._fields_}
         res = None

@@ -69,6 +69,7 @@ extern "C" {
 #define GPK_EHIP (-3)       /* HIP runtime error (see gpk_last_hip_error) */
 #define GPK_ENODEV (-4)     /* no gfx950 device / device ordinal out of range */
 #define GPK_EUNSUPP (-5)    /* configuration the device path does not implement */
+#define GPK_STOPPED 1       /* not an error: a replay or ring pump ended early at gpk_stop */
 
 /* ---- LayerType ids (gopacket decode.go:106-117, layers/layertypes.go) ---- */
 #define GPK_LT_ZERO 0
@@ -363,6 +364,18 @@ int gpk_ctx_destroy(gpk_ctx* ctx);
 #define GPK_TABLES_AUTO 0
 #define GPK_TABLES_GLOBAL 1
 int gpk_ctx_set_table_mode(gpk_ctx* ctx, int mode);
+/* Ends the gpk_replay_file, gpk_replay_file_range and gpk_tpacket_pump calls
+ * running on ctx early: what a Go caller does by breaking out of its
+ * ReadPacketData loop (ngread.go:629-632, afpacket.go:335-367), for the calls
+ * that push results through callbacks. Callable from inside any of their
+ * callbacks or from another thread, any number of times. Each such call checks
+ * before every batch it delivers: from the first check after gpk_stop returned
+ * it makes no further callback (a batch's packets, fields and results callbacks
+ * are made for all of it or none of it), waits for its own reads, copies and
+ * kernels, and returns GPK_STOPPED with stats.packets = the packets delivered;
+ * a range replay is then not clean. A call that starts after gpk_stop returned
+ * is not affected. */
+int gpk_stop(gpk_ctx* ctx);
 
 /* A packed, offset-indexed packet batch. Packet i is data[offsets[i] ..
  * offsets[i]+caplens[i]). In gpk_decode_batch every pointer is DEVICE memory;

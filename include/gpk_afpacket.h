@@ -7,19 +7,19 @@
  * replaces, for a Go caller binding it through cgo:
  *
  *   gpk_tp_default_opts / gpk_tp_check_opts   afpacket parseOptions + options.check
- *                                             afpacket/options.go:121-211 (defaults :105-119)
- *   gpk_tpacket_new                           afpacket.NewTPacket  afpacket.go:309-343
+ *                                             afpacket/options.go:160-211 (defaults :126-158)
+ *   gpk_tpacket_new                           afpacket.NewTPacket  afpacket.go:261-294
  *                                             (bindToInterface :155-171, setRequestedTPacketVersion
- *                                             :183-196, setVNetHdrSize :199-204, setUpRing :207-244,
- *                                             InitSocketStats :370-391)
+ *                                             :182-194, setVNetHdrSize :197-202, setUpRing :205-240,
+ *                                             InitSocketStats :378-399)
  *   gpk_tpacket_attach                        (no reference counterpart) the same reader over a ring
  *                                             the caller owns: tests, replays, the benchmark
  *   gpk_tpacket_index                         a loop of TPacket.ZeroCopyReadPacketData calls
- *                                             afpacket.go:367-399 (getTPacketHeader :469-492,
- *                                             pollForFirstPacket :494-523, releaseCurrentPacket
- *                                             :353-358) over the v1/v2/v3 headers of header.go
- *   gpk_tpacket_stats / _socket_stats         TPacket.Stats :402-407, SocketStats :395-431
- *   gpk_tpacket_set_bpf / _set_fanout         TPacket.SetBPF :336-349, SetFanout :545-553
+ *                                             afpacket.go:335-367 (getTPacketHeader :462-486,
+ *                                             pollForFirstPacket :488-516, releaseCurrentPacket
+ *                                             :316-321) over the v1/v2/v3 headers of header.go
+ *   gpk_tpacket_stats / _socket_stats         TPacket.Stats :370-375, SocketStats :402-431
+ *   gpk_tpacket_set_bpf / _set_fanout         TPacket.SetBPF :297-309, SetFanout :542-548
  *   gpk_tpacket_pump                          the capture loop: ZeroCopyReadPacketData +
  *                                             DecodingLayerParser.DecodeLayers per packet,
  *                                             pipelined through HBM
@@ -98,7 +98,7 @@ typedef struct gpk_tp_info {
 /* Run ZeroCopyReadPacketData until max packets, a wait, or an error. Packet i
  * is ring[offsets[i], +caplens[i]) when offsets[i] < ring bytes, else
  * side[offsets[i] - ring bytes, ...): packets the reference copies to insert
- * an 802.1Q header (OptAddVLANHeader, header.go:150-158) are built in the
+ * an 802.1Q header (OptAddVLANHeader, header.go:147-155) are built in the
  * caller's side buffer. wait != 0 (socket readers): poll like
  * pollForFirstPacket, with the option's poll timeout.
  *
@@ -179,7 +179,10 @@ typedef void (*gpk_tp_pump_cb)(void* user, uint64_t first_packet, uint64_t n, co
  * mirror straight from the ring (registered with HIP where it can be), the
  * side buffer follows, the decode kernel runs on the batch's index, results
  * come back in packet order through cb. Headers are deferred and released
- * once their HtoD has completed. */
+ * once their HtoD has completed. gpk_stop(ctx) (gpk.h) ends the pump early:
+ * no further callback, GPK_STOPPED, stats.packets = the packets delivered;
+ * a pump waiting on a dry ring sees it once its wait ends (a frame, or the
+ * socket's poll timeout). */
 int gpk_tpacket_pump(gpk_ctx* ctx, const gpk_parser* p, gpk_tpacket* t, const gpk_tp_pump_opts* opts,
                      gpk_tp_pump_cb cb, void* user, gpk_tp_pump_stats* stats);
 

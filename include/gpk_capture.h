@@ -8,15 +8,21 @@
  * cgo:
  *
  *   gpk_capreader_create(GPK_CAP_PCAPNG)  pcapgo.NewNgReader(r, NgReaderOptions)
- *                                         pcapgo/ngread.go:64-106; options :23-37
- *   gpk_capreader_create(GPK_CAP_PCAP)    pcapgo.NewReader(r)            pcapgo/read.go:64-122
+ *                                         pcapgo/ngread.go:64-107; options :23-37
+ *   gpk_capreader_create(GPK_CAP_PCAP)    pcapgo.NewReader(r)            pcapgo/read.go:65-119
  *   gpk_capreader_index                   a loop of ReadPacketData calls
- *                                         pcapgo/ngread.go:642-675 (ReadPacketDataWithOptions,
- *                                         reached through ReadPacketData :636-640 and the
- *                                         ZeroCopy variants :683-716), pcapgo/read.go:124-140
- *   gpk_capreader_link_type               NgReader.LinkType() ngread.go:719 / Reader.LinkType() read.go:183
- *   gpk_capreader_section_* / _interface* NgReader.SectionInfo() :724, Interface(i) :729,
- *                                         NInterfaces() :737, SectionEndCallback (:33)
+ *                                         pcapgo/ngread.go:636-664 (ReadPacketDataWithOptions,
+ *                                         reached through ReadPacketData :629-632 and the
+ *                                         ZeroCopy variants :672-717), pcapgo/read.go:122-177
+ *   gpk_capreader_packet_options          the NgPacketOptions ReadPacketDataWithOptions returns
+ *                                         (readPacketOptions ngread.go:582-625)
+ *   gpk_capreader_link_type               NgReader.LinkType() ngread.go:720 / Reader.LinkType() read.go:180
+ *   gpk_capreader_section_* / _interface* NgReader.SectionInfo() :725, Interface(i) :730,
+ *                                         NInterfaces() :738, SectionEndCallback (:32-34)
+ *   gpk_capreader_nnames / _name          NgReader.NNames() :759 / Name(i) :751
+ *   gpk_capreader_stat_event              NgReaderOptions.StatisticsCallback (:35-36)
+ *   gpk_capreader_skip_section            NgReader.SkipSection() :330-335
+ *   gpk_capreader_set_snaplen             Reader.SetSnaplen() read.go:216-218
  *   gpk_replay_file                       the C5 loop: NgReader/Reader + DecodingLayerParser
  *                                         over a whole file, pipelined through HBM
  *
@@ -24,7 +30,7 @@
  * quirks: the indexer is a restatement of pcapgo's
  * bufio-stream reader, fed in chunks. Gzip-compressed files are inflated by
  * the file layer (gpk_replay_file) before indexing, as pcapgo does
- * transparently (read.go:74-84, ngread.go:80-95).
+ * transparently (read.go:80-86, ngread.go:75-91).
  */
 #ifndef GPK_CAPTURE_H
 #define GPK_CAPTURE_H
@@ -107,12 +113,12 @@ int gpk_capreader_error(const gpk_capreader* r, char* buf, size_t cap, int* is_e
 
 /* Reader.LinkType() / NgReader.LinkType() (0 with WantMixedLinkType). */
 int gpk_capreader_link_type(const gpk_capreader* r);
-/* pcap header fields: snaplen, version, nanosecond resolution (read.go:96-121). */
+/* pcap header fields: snaplen, version, nanosecond resolution (read.go:94-117). */
 int gpk_capreader_pcap_header(const gpk_capreader* r, uint32_t* snaplen, uint16_t* major, uint16_t* minor,
                               int* nanosecond);
 
 /* pcapng sections: sections 0 .. nsections-1 ended (the SectionEndCallback
- * calls, ngread.go:241-248); section == nsections is the current one. */
+ * calls, ngread.go:239-245); section == nsections is the current one. */
 int gpk_capreader_nsections(const gpk_capreader* r);
 #define GPK_SECTION_COMMENT 0
 #define GPK_SECTION_HARDWARE 1
@@ -141,6 +147,52 @@ int gpk_capreader_interface(const gpk_capreader* r, int section, int index, gpk_
 #define GPK_IFACE_OS 4
 #define GPK_IFACE_STATS_COMMENT 5
 int gpk_capreader_interface_str(const gpk_capreader* r, int section, int index, int field, char* buf, size_t cap);
+
+/* The rest of NgReader's / Reader's interface. What the reader reports here
+ * is the state after the packets it has returned through gpk_capreader_index
+ * (and _index_all; a gpk_replay_file reader does not report it). */
+/* SectionEndCallback's timing: section s (< nsections) ended during the call
+ * that returned packet *at (or ended with an error there): *at = the packets
+ * returned before it; *seq = its place among all SectionEndCallback and
+ * StatisticsCallback calls (0, 1, ...). */
+int gpk_capreader_section_end_at(const gpk_capreader* r, int section, uint64_t* at, uint64_t* seq);
+/* StatisticsCallback(ifaceID, NgInterfaceStatistics) (ngread.go:35-36, made at
+ * :485-487 after each interface statistics block): every call so far, in
+ * order. Event k: *iface, the statistics in the statistics fields of *stats
+ * (has_statistics 1, the rest 0), its comment into buf (returns the comment's
+ * length), *at = the packets returned before it and *seq its place among all
+ * callbacks (as in gpk_capreader_section_end_at). Any pointer may be NULL. */
+int gpk_capreader_nstat_events(const gpk_capreader* r);
+int gpk_capreader_stat_event(const gpk_capreader* r, int k, uint64_t* at, uint64_t* seq, int* iface,
+                             gpk_ng_interface* stats, char* buf, size_t cap);
+/* NgReader.NNames() / Name(i) (ngread.go:751-761): the name resolution records
+ * of the current section (readNameResolutionBlock, ngread_nrb.go:64-130).
+ * *kind = the record type: 1 IPv4 / 2 IPv6 (NgIPAddress: *addr_len 4 / 16),
+ * 3 EUI-48 / 4 EUI-64 (NgEUIAddress: *addr_len 24, the reader's whole 24-byte
+ * scratch buffer, which newHWAddress clones, ngread_nrb.go:56-61); addr has
+ * room for 24 bytes. names: the record's Names, each followed by a NUL, as
+ * far as cap holds whole names; returns the bytes all of them take. */
+int gpk_capreader_nnames(const gpk_capreader* r);
+int gpk_capreader_name(const gpk_capreader* r, int i, int* kind, uint8_t* addr, int* addr_len, int* nnames,
+                       char* names, size_t cap);
+/* NgReader.SkipSection (ngread.go:330-335): the next gpk_capreader_index call
+ * first skips the rest of the current section and reads the next section
+ * header; an error there ends that call with GPK_CAP_END and no packet (the
+ * error SkipSection returns). */
+int gpk_capreader_skip_section(gpk_capreader* r);
+/* Reader.SetSnaplen (read.go:216-218), for the packets read from now on. */
+int gpk_capreader_set_snaplen(gpk_capreader* r, uint32_t snaplen);
+/* ReadPacketDataWithOptions's NgPacketOptions (ngread.go:636-664,
+ * readPacketOptions :582-625). After gpk_capreader_keep_options(r, 1) each
+ * gpk_capreader_index call keeps the options of the packets it returned:
+ * for its packet i, *tlv = *bytes bytes of records {uint16_t code; uint16_t 0;
+ * uint32_t len; len value bytes, zero-padded to a multiple of 4}, one per
+ * option readPacketOptions read, in order, each with the value the reader
+ * held for it (a zero-length option keeps the previous option's value,
+ * ngread.go:214-232); none for simple and obsolete packet blocks. Valid until
+ * the next index call (gpk_capreader_index_all's own calls included). */
+int gpk_capreader_keep_options(gpk_capreader* r, int on);
+int gpk_capreader_packet_options(const gpk_capreader* r, uint64_t i, const uint8_t** tlv, uint64_t* bytes);
 
 /* ---- whole-file replay through the GPU (BASELINE config C5) -------------- */
 /* The layer fields of one device launch's packets (gpk_replay_opts.fields_cb):
@@ -204,7 +256,10 @@ typedef void (*gpk_replay_cb)(void* user, uint64_t first_packet, uint64_t n, con
  * The reader threads, and the calling thread for the duration of the call,
  * run on the CPUs of the current device's NUMA node that the caller may use
  * (its affinity is restored on return); environment GPK_REPLAY_NUMA=0 turns
- * this off, =1 pins the reader threads only. */
+ * this off, =1 pins the reader threads only.
+ * gpk_stop(ctx) (gpk.h), from a callback or another thread, ends the call
+ * early: no further callback, GPK_STOPPED, stats.packets = the packets
+ * delivered. */
 int gpk_replay_file(gpk_ctx* ctx, const gpk_parser* p, const char* path, const gpk_replay_opts* opts,
                     gpk_replay_cb cb, void* user, gpk_replay_stats* stats);
 

@@ -7,18 +7,18 @@ never imports it.
 What it restates, as a state machine over a bytearray ring (the Go reader's
 fields are the attributes of TPacketOracle):
 
-  afpacket/options.go:105-114   defaultOpts
-  afpacket/options.go:121-211   parseOptions / options.check (error texts)
-  afpacket/afpacket.go:367-399  ZeroCopyReadPacketData (the retry loop, the
+  afpacket/options.go:149-158   defaultOpts
+  afpacket/options.go:160-211   parseOptions / options.check (error texts)
+  afpacket/afpacket.go:335-367  ZeroCopyReadPacketData (the retry loop, the
                                 "empty block" skip, Stats.Packets)
-  afpacket/afpacket.go:353-358  releaseCurrentPacket (clearStatus, offset++)
-  afpacket/afpacket.go:469-492  getTPacketHeader (ring position arithmetic)
-  afpacket/afpacket.go:494-523  pollForFirstPacket (TP_STATUS_USER check)
-  afpacket/header.go:60-127     v1/v2/v3 header layouts (tpacket_hdr, tpacket2_hdr,
+  afpacket/afpacket.go:316-321  releaseCurrentPacket (clearStatus, offset++)
+  afpacket/afpacket.go:462-486  getTPacketHeader (ring position arithmetic)
+  afpacket/afpacket.go:488-516  pollForFirstPacket (TP_STATUS_USER check)
+  afpacket/header.go:59-137     v1/v2/v3 header layouts (tpacket_hdr, tpacket2_hdr,
                                 tpacket_block_desc + tpacket_hdr_v1, tpacket3_hdr,
                                 tpacketHdrVarient1, sockaddr_ll after tpAlign(hdr))
-  afpacket/header.go:150-158    insertVlanHeader (panics below 12 bytes)
-  afpacket/header.go:160-263    get{Status,Time,Data,Length,IfaceIndex,VLAN}, next()
+  afpacket/header.go:147-155    insertVlanHeader (panics below 12 bytes)
+  afpacket/header.go:157-268    get{Status,Time,Data,Length,IfaceIndex,VLAN}, next()
   Go stdlib time.Unix(sec, nsec) normalisation
 
 Where Go would block in poll(2) the oracle stops with WAIT and resumes at the

@@ -6,7 +6,7 @@
  * as (off, len) views into the packet with cap = caplen - off: every slice on
  * this path keeps its capacity to the end of the packet buffer (reslicing
  * data[:n] keeps cap), and the packet buffer handed to DecodeLayers is taken
- * to have cap == len (what pcapgo.Reader / NgReader return, read.go:122-140).
+ * to have cap == len (what pcapgo.Reader / NgReader return, read.go:122-137).
  */
 #include "gpk_oracle.h"
 

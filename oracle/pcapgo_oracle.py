@@ -8,32 +8,37 @@ What it restates, line by line, as a byte-stream state machine (a position in
 the capture plus the reader's state, exactly what Go's bufio-backed reader
 consumes per call, so every quirk of the reference's accounting is kept):
 
-  pcapgo/read.go:64-122     NewReader / readHeader (magic, byte order, ns factor,
+  pcapgo/read.go:65-119     NewReader / readHeader (magic, byte order, ns factor,
                             version, snaplen, link type)
-  pcapgo/read.go:124-140    Reader.ReadPacketData (snaplen / length checks)
-  pcapgo/read.go:171-180    Reader.readPacketHeader (uint32 usec*factor wraps)
-  pcapgo/ngread.go:64-106   NewNgReader (gzip peek, first SHB)
-  pcapgo/ngread.go:112-143  readBytes / discard (ErrUnexpectedEOF mapping)
-  pcapgo/ngread.go:170-196  readBlock (SHB byte-order magic, u32 length)
-  pcapgo/ngread.go:199-236  readOption (the option value buffer is reused and
+  pcapgo/read.go:122-137    Reader.ReadPacketData (snaplen / length checks)
+  pcapgo/read.go:169-177    Reader.readPacketHeader (uint32 usec*factor wraps)
+  pcapgo/ngread.go:64-107   NewNgReader (gzip peek, first SHB)
+  pcapgo/ngread.go:113-137  readBytes / discard (ErrUnexpectedEOF mapping)
+  pcapgo/ngread.go:165-193  readBlock (SHB byte-order magic, u32 length)
+  pcapgo/ngread.go:196-234  readOption (the option value buffer is reused and
                             keeps stale bytes; zero-length options keep the
                             previous value)
-  pcapgo/ngread.go:240-305  readSectionHeader (version skip, section info)
-  pcapgo/ngread.go:308-327  skipSection / SkipSection
-  pcapgo/ngread.go:330-369  firstInterface
-  pcapgo/ngread.go:372-436  readInterfaceDescriptor (time scale; a resolution
+  pcapgo/ngread.go:238-312  readSectionHeader (version skip, section info)
+  pcapgo/ngread.go:315-335  skipSection / SkipSection
+  pcapgo/ngread.go:338-373  firstInterface
+  pcapgo/ngread.go:376-437  readInterfaceDescriptor (time scale; a resolution
                             exponent >= 64 panics with divide by zero)
-  pcapgo/ngread.go:439-443  convertTime (uint64 arithmetic)
-  pcapgo/ngread.go:446-492  readInterfaceStatistics
-  pcapgo/ngread.go:497-582  readPacketHeader (EPB / SPB / PB, link-type filter)
-  pcapgo/ngread.go:584-632  readPacketOptions (EPB option panics)
-  pcapgo/ngread.go:642-675  ReadPacketDataWithOptions
-  pcapgo/ngread_nrb.go:63-130  readNameResolutionBlock (EUI records count 24
-                               address bytes: newHWAddress clones r.buf[:])
-  pcapgo/ngread_dsb.go:17-39   readDecryptionSecretsBlock
+  pcapgo/ngread.go:440-443  convertTime (uint64 arithmetic)
+  pcapgo/ngread.go:446-489  readInterfaceStatistics
+  pcapgo/ngread.go:494-580  readPacketHeader (EPB / SPB / PB, link-type filter)
+  pcapgo/ngread.go:582-625  readPacketOptions (EPB option panics; the options read are
+                            kept per packet, ReadPacketDataWithOptions's opts)
+  pcapgo/ngread.go:636-664  ReadPacketDataWithOptions
+  pcapgo/ngread_nrb.go:64-130  readNameResolutionBlock (EUI records count 24
+                               address bytes: newHWAddress clones r.buf[:], so
+                               the reader's 24-byte scratch buffer is tracked
+                               through every read into it); Name(i) / NNames()
+  NgReaderOptions.StatisticsCallback / SectionEndCallback (ngread.go:32-36): the
+                            calls, with the packets returned before each
+  pcapgo/ngread_dsb.go:18-39   readDecryptionSecretsBlock
   time.Unix(sec, nsec).UTC() normalisation (Go stdlib time.Unix)
 
-Gzip input (read.go:74-84, ngread.go:80-95) is inflated before the reader sees
+Gzip input (read.go:80-86, ngread.go:75-91) is inflated before the reader sees
 it (zlib's published DEFLATE), as the product's file layer does.
 
 Output of read_all(): list of packets (offset into the inflated stream,
@@ -87,7 +92,7 @@ def unix_utc(sec, nsec):
 
 
 def inflate_if_gzip(raw):
-    """read.go:74-84 / ngread.go:80-95: transparently gunzip. Returns (bytes, error-or-None)."""
+    """read.go:80-86 / ngread.go:75-91: transparently gunzip. Returns (bytes, error-or-None)."""
     if len(raw) >= 2 and raw[0] == 0x1F and raw[1] == 0x8B:
         if len(raw) < 10:  # gzip.NewReader: the 10-byte header read hits EOF
             return b"", ERR_UNEXPECTED_EOF
@@ -119,7 +124,7 @@ class _Stream:
         self.pos = 0
 
     def read_into(self, n):
-        """NgReader.readBytes (ngread.go:112-126): (bytes, n_read, err)."""
+        """NgReader.readBytes (ngread.go:113-126): (bytes, n_read, err)."""
         avail = len(self.d) - self.pos
         k = n if n <= avail else avail
         b = self.d[self.pos:self.pos + k]
@@ -153,12 +158,13 @@ class _Stream:
 
 
 class Packet:
-    __slots__ = ("offset", "caplen", "ts_sec", "ts_nsec", "length", "iface", "ancil")
+    __slots__ = ("offset", "caplen", "ts_sec", "ts_nsec", "length", "iface", "ancil", "opts")
 
-    def __init__(self, offset, caplen, ts, length, iface, ancil):
+    def __init__(self, offset, caplen, ts, length, iface, ancil, opts=None):
         self.offset, self.caplen = offset, caplen
         self.ts_sec, self.ts_nsec = ts
         self.length, self.iface, self.ancil = length, iface, ancil
+        self.opts = opts or []  # the EPB's options as readPacketOptions read them: [(code, value)]
 
     def key(self):
         return (self.offset, self.caplen, self.ts_sec, self.ts_nsec, self.length, self.iface, self.ancil)
@@ -171,7 +177,7 @@ class Reader:
     MAGIC_NS, MAGIC_NS_BE, MAGIC_US, MAGIC_US_BE = 0xA1B23C4D, 0x4D3CB2A1, 0xA1B2C3D4, 0xD4C3B2A1
 
     def __init__(self, data):
-        """NewReader (read.go:64-70) + readHeader (read.go:72-122). Raises GoError."""
+        """NewReader (read.go:65-71) + readHeader (read.go:73-119). Raises GoError."""
         if len(data) < 2:
             raise GoError(ERR_EOF)  # br.Peek(2)
         data, gerr = inflate_if_gzip(data)
@@ -200,9 +206,12 @@ class Reader:
         self.snaplen = struct.unpack_from(self.bo + "I", buf, 16)[0]
         self.link_type = struct.unpack_from(self.bo + "I", buf, 20)[0] & 0xFFFF  # layers.LinkType is uint16
 
+    def set_snaplen(self, v):  # SetSnaplen (read.go:216-218)
+        self.snaplen = v
+
     def read_packet(self):
-        """ReadPacketData (read.go:124-140): Packet, or raises GoError."""
-        hdr, err = self.s.read_full(16)  # readPacketHeader (read.go:171-180)
+        """ReadPacketData (read.go:122-137): Packet, or raises GoError."""
+        hdr, err = self.s.read_full(16)  # readPacketHeader (read.go:169-177)
         if err:
             raise GoError(err)
         sec, usec, caplen, length = struct.unpack(self.bo + "IIII", hdr)
@@ -243,7 +252,7 @@ class NgInterface:
 
 class NgReader:
     def __init__(self, data, want_mixed=False, error_on_mismatch=False, skip_unknown_version=False):
-        """NewNgReader (ngread.go:64-106). Raises GoError."""
+        """NewNgReader (ngread.go:64-107). Raises GoError."""
         self.want_mixed, self.error_on_mismatch, self.skip_unknown = want_mixed, error_on_mismatch, skip_unknown_version
         if len(data) < 2:  # reader.r.Peek(2)
             raise GoError(ERR_UNEXPECTED_EOF if len(data) > 0 else ERR_EOF)
@@ -265,7 +274,13 @@ class NgReader:
         self.ended_sections = []  # SectionEndCallback(interfaces, sectionInfo)
         self.ci = [0, 0, (0, 0), 0, 0]  # iface, caplen, ts, length, (unused)
         self.ancil = None
-        self.n_name_records = 0
+        self.buf = bytearray(24)  # NgReader.buf: block / option headers land here; EUI names clone all of it
+        self.npk = 0  # packets returned
+        self.names = []  # nameRecords: (record type, address bytes, [names])
+        self.stat_events = []  # StatisticsCallback calls: (packets before, call number, iface, stats dict)
+        self.ended_at = []  # SectionEndCallback calls: (packets before, call number)
+        self.ncb = 0  # SectionEndCallback + StatisticsCallback calls so far
+        self.cur_opts = []
         self.n_secrets = 0
         self._read_block()
         if self.typ != SHB:
@@ -288,6 +303,18 @@ class NgReader:
             raise GoError(err)
         return b
 
+    def _rbuf(self, n, at=0):
+        """readBytes(r.buf[at:at+n]): the bytes (a short read's too) land in NgReader.buf."""
+        b, k, err = self.s.read_into(n)
+        self.buf[at:at + k] = b
+        return b, k, err
+
+    def _read_buf(self, n):
+        b, k, err = self._rbuf(n)
+        if err:
+            raise GoError(err)
+        return b
+
     def _discard(self, n):
         if self.s.discard(n):
             raise GoError(ERR_UNEXPECTED_EOF)
@@ -299,14 +326,16 @@ class NgReader:
     def _opt_reslice(self, hi):  # value[:hi] reslices up to cap (stale bytes visible)
         return bytes(self.opt_back[:hi])
 
-    # -- ngread.go:170-196 ---------------------------------------------
+    # -- ngread.go:165-193 ---------------------------------------------
     def _read_block(self):
-        b, k, err = self.s.read_into(8)
+        b, k, err = self._rbuf(8)
         if err:
             raise GoError(ERR_EOF if k == 0 else err)
         self.typ = self._u32(b, 0)
         if self.typ == SHB:
-            m = self._read(4)
+            m, k, err = self._rbuf(4, 8)
+            if err:
+                raise GoError(err)
             if struct.unpack(">I", m)[0] == BYTE_ORDER_MAGIC:
                 self.be = True
             elif struct.unpack("<I", m)[0] == BYTE_ORDER_MAGIC:
@@ -317,12 +346,12 @@ class NgReader:
             return
         self.length = (self._u32(b, 4) - 8) & M32
 
-    # -- ngread.go:199-236 ---------------------------------------------
+    # -- ngread.go:196-234 ---------------------------------------------
     def _read_option(self):
         if self.length == 4:
             self.opt_code = 0
             return
-        b = self._read(4)
+        b = self._read_buf(4)
         self.length = (self.length - 4) & M32
         self.opt_code = self._u16(b, 0)
         olen = self._u16(b, 2)
@@ -345,16 +374,18 @@ class NgReader:
                 self._discard(4 - pad)
             self.length = (self.length - olen) & M32
 
-    # -- ngread.go:240-305 ---------------------------------------------
+    # -- ngread.go:238-312 ---------------------------------------------
     def _read_section_header(self):
         if self.active_section:
             self.ended_sections.append((self.section, [i.as_dict() for i in self.ifaces]))
+            self.ended_at.append((self.npk, self.ncb))
+            self.ncb += 1
         self.ifaces = []
         self.n_secrets = 0
-        self.n_name_records = 0
+        self.names = []
         self.active_section = False
         while True:  # RESTART
-            b = self._read(12)
+            b = self._read_buf(12)
             self.length = (self.length - 12) & M32
             vmaj, vmin = self._u16(b, 0), self._u16(b, 2)
             if vmaj != 1 or vmin != 0:
@@ -391,7 +422,7 @@ class NgReader:
                 return
             self._discard(self.length)
 
-    # -- ngread.go:330-369 ---------------------------------------------
+    # -- ngread.go:338-373 ---------------------------------------------
     def _first_interface(self):
         while True:
             self._read_block()
@@ -414,9 +445,9 @@ class NgReader:
                 self._read_name_resolution()
             self._discard(self.length)
 
-    # -- ngread.go:372-436 ---------------------------------------------
+    # -- ngread.go:376-437 ---------------------------------------------
     def _read_interface_descriptor(self):
-        b = self._read(8)
+        b = self._read_buf(8)
         self.length = (self.length - 8) & M32
         it = NgInterface()
         it.link_type = self._u16(b, 0)
@@ -469,9 +500,9 @@ class NgReader:
     def _time(self, idx, ts):
         return unix_utc(*self._convert_time(idx, ts))
 
-    # -- ngread.go:446-492 ---------------------------------------------
+    # -- ngread.go:446-489 ---------------------------------------------
     def _read_interface_statistics(self):
-        b = self._read(12)
+        b = self._read_buf(12)
         self.length = (self.length - 12) & M32
         idx = self._u32(b, 0)
         ts = (self._u32(b, 4) << 32) | self._u32(b, 8)
@@ -497,10 +528,12 @@ class NgReader:
             elif c == 5:
                 st["dropped"] = self._u64(self._opt_reslice(8))
         self._discard(self.length)
+        self.stat_events.append((self.npk, self.ncb, idx, dict(st)))  # StatisticsCallback(ifaceID, *stats)
+        self.ncb += 1
 
-    # -- ngread_dsb.go:17-39 --------------------------------------------
+    # -- ngread_dsb.go:18-39 --------------------------------------------
     def _read_decryption_secrets(self):
-        b, k, err = self.s.read_into(8)
+        b, k, err = self._rbuf(8)
         if err:
             raise GoError("could not read DecryptionSecret Header block length: %s" % err)
         self.length = (self.length - 8) & M32
@@ -511,10 +544,10 @@ class NgReader:
         self.length = (self.length - slen) & M32
         self.n_secrets += 1
 
-    # -- ngread_nrb.go:63-130 -------------------------------------------
+    # -- ngread_nrb.go:64-130 -------------------------------------------
     def _read_name_resolution(self):
         while self.length > 0:
-            b, k, err = self.s.read_into(4)
+            b, k, err = self._rbuf(4)
             if err:
                 raise GoError("could not read NameRecord Header block length: %s" % err)
             self.length = (self.length - 4) & M32
@@ -522,17 +555,19 @@ class NgReader:
             length = min(rlen, self.length)
             padding = (4 - length % 4) if length % 4 else 0
             if rtype in (1, 2):
-                _, k, err = self.s.read_into(4 if rtype == 1 else 16)
+                _, k, err = self._rbuf(4 if rtype == 1 else 16)
                 if err:
                     raise GoError("could not read %s address: could not read IP address: %s"
                                   % ("IPv4" if rtype == 1 else "IPv6", err))
                 alen = 4 if rtype == 1 else 16
+                addr = bytes(self.buf[:alen])  # netip.AddrFromSlice(r.buf[:length])
             elif rtype in (3, 4):
-                _, k, err = self.s.read_into(6 if rtype == 3 else 8)
+                _, k, err = self._rbuf(6 if rtype == 3 else 8)
                 if err:
                     raise GoError("could not read %s address: could not read EUI address: %s"
                                   % ("EUI-48" if rtype == 3 else "EUI-64", err))
                 alen = 24  # newHWAddress(r.buf[:]) clones the whole 24-byte buffer
+                addr = bytes(self.buf)
             elif rtype == 0:
                 break
             else:
@@ -542,23 +577,25 @@ class NgReader:
                 continue
             self.length = (self.length - length) & M32
             length -= alen
+            names = []
             while length > 0:
                 bstr, err = self.s.read_until_nul()
                 if err:
                     raise GoError("could not read name: %s" % err)
                 length -= len(bstr)
-            self.n_name_records += 1
+                names.append(bytes(bstr).strip(b"\x00"))  # bytes.Trim(bstr, "\x00")
+            self.names.append((rtype, addr, names))
             self._discard(padding)
         self._discard(self.length)
 
-    # -- ngread.go:497-582 ---------------------------------------------
+    # -- ngread.go:494-580 ---------------------------------------------
     def _read_packet_header(self):
         while True:  # RESTART
             while True:  # FIND_PACKET
                 self._read_block()
                 t = self.typ
                 if t == EPB:
-                    b = self._read(20)
+                    b = self._read_buf(20)
                     self.length = (self.length - 20) & M32
                     idx = self._u32(b, 0)
                     if idx >= len(self.ifaces):
@@ -568,7 +605,7 @@ class NgReader:
                     self.ci = [idx, self._u32(b, 12), ts, self._u32(b, 16)]
                     break
                 elif t == SPB:
-                    b = self._read(4)
+                    b = self._read_buf(4)
                     self.length = (self.length - 4) & M32
                     length = self._u32(b, 0)
                     caplen = length
@@ -587,7 +624,7 @@ class NgReader:
                 elif t == SHB:
                     self._read_section_header()
                 elif t == PB:
-                    b = self._read(20)
+                    b = self._read_buf(20)
                     self.length = (self.length - 20) & M32
                     idx = self._u16(b, 0)
                     if idx >= len(self.ifaces):
@@ -611,7 +648,7 @@ class NgReader:
             self.ancil = self.ifaces[self.ci[0]].link_type
             return
 
-    # -- ngread.go:584-632 ---------------------------------------------
+    # -- ngread.go:582-625 ---------------------------------------------
     def _read_packet_options(self):
         while True:
             self._read_option()
@@ -623,10 +660,18 @@ class NgReader:
                 raise GoError("runtime error: index out of range [3] with length %d" % n, panic=True)
             if c in (4, 5) and n < 8:  # binary.LittleEndian.Uint64: _ = b[7]
                 raise GoError("runtime error: index out of range [7] with length %d" % n, panic=True)
+            self.cur_opts.append((c, self._opt_value()))
 
-    # -- ngread.go:642-675 ---------------------------------------------
+    # -- ngread.go:315-335 ---------------------------------------------
+    def skip_section(self):
+        """SkipSection: skipSection, then readSectionHeader. Raises GoError."""
+        self._skip_section()
+        self._read_section_header()
+
+    # -- ngread.go:636-664 ---------------------------------------------
     def read_packet(self):
-        """ReadPacketDataWithOptions: Packet, or raises GoError."""
+        """ReadPacketDataWithOptions: Packet (opts: the options read), or raises GoError."""
+        self.cur_opts = []
         self._read_packet_header()
         idx, caplen, ts, length = self.ci
         off = self.s.pos
@@ -638,7 +683,8 @@ class NgReader:
         if self.typ == EPB:
             self._read_packet_options()
         self._discard(self.length)
-        return Packet(off, caplen, ts, length, idx, self.ancil)
+        self.npk += 1
+        return Packet(off, caplen, ts, length, idx, self.ancil, self.cur_opts)
 
     def section_state(self):
         return self.section, [i.as_dict() for i in self.ifaces]

@@ -37,6 +37,7 @@ extern "C" int gpk_decode_batch_ex(gpk_ctx*, const gpk_parser*, const gpk_batch*
 }
 hipError_t gpk_pin_alloc(void**, size_t) { abort(); }
 extern "C" int gpk_ctx_device(const gpk_ctx*) { abort(); }
+extern "C" uint64_t gpk_ctx_stop_seq(const gpk_ctx*) { abort(); }
 hipError_t gpk_pin_free(void*) { abort(); }
 
 namespace {

@@ -5,6 +5,8 @@
  *
  *   gpk_threads_test <golden dir> <threads> <copies> <reps>
  *   gpk_threads_test replay <pcapng> <threads>
+ *   (the replay mode also ends replays early with gpk_stop, from a callback and
+ *   from another thread: a Go caller's break out of its ReadPacketData loop)
  *
  * The batch is <copies> shuffled copies of the golden packets of
  * tests/golden/c_abi (reference vectors, the reference's capture files,
@@ -27,6 +29,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include <hip/hip_runtime_api.h>
 
@@ -294,6 +297,104 @@ static void* replay_run(void* arg) {
   return NULL;
 }
 
+/* ---- gpk_stop: a replay ended early ---------------------------------------- */
+struct stopper {
+  gpk_ctx* ctx;
+  struct collected got;
+  int batches, stop_after, sleep_us;
+  volatile int started;
+};
+
+static void on_results_stop(void* user, uint64_t first, uint64_t n, const gpk_record* rec, const uint32_t* err,
+                            const uint64_t* flows, const gpk_capture_info* ci, const uint32_t* caplens) {
+  struct stopper* s = (struct stopper*)user;
+  on_results(&s->got, first, n, rec, err, flows, ci, caplens);
+  s->batches++;
+  __atomic_store_n(&s->started, 1, __ATOMIC_SEQ_CST);
+  if (s->batches == s->stop_after) CHECK(gpk_stop(s->ctx) == GPK_OK, "gpk_stop");
+  if (s->sleep_us) {
+    struct timespec ts = {0, (long)s->sleep_us * 1000};
+    nanosleep(&ts, NULL);
+  }
+}
+
+static struct {
+  struct stopper* s;
+  gpk_parser* p;
+  const char* path;
+  int rc;
+  gpk_replay_stats st;
+} SR;
+
+static void* stop_run(void* arg) {
+  (void)arg;
+  gpk_replay_opts o;
+  memset(&o, 0, sizeof(o));
+  o.slot_bytes = 4u << 20;
+  o.slots = 3;
+  o.batch_pkts = 2000;
+  SR.rc = gpk_replay_file(SR.s->ctx, SR.p, SR.path, &o, on_results_stop, SR.s, &SR.st);
+  return NULL;
+}
+
+static int prefix_equal(const struct collected* a, const struct collected* whole) {
+  for (uint64_t i = 0; i < a->n; i++)
+    if (i >= whole->n || memcmp(&a->rec[i], &whole->rec[i], sizeof(gpk_record)) != 0 ||
+        memcmp(&a->fl[3 * i], &whole->fl[3 * i], 24) != 0 || memcmp(&a->ci[i], &whole->ci[i], sizeof(gpk_capture_info)) != 0)
+      return 0;
+  return 1;
+}
+
+static void stop_checks(gpk_ctx* ctx, gpk_parser* p, const char* path, const struct collected* whole) {
+  /* from inside the second batch's callback */
+  struct stopper a;
+  memset(&a, 0, sizeof(a));
+  a.ctx = ctx;
+  a.stop_after = 2;
+  gpk_replay_opts o;
+  memset(&o, 0, sizeof(o));
+  o.slot_bytes = 4u << 20;
+  o.slots = 3;
+  o.batch_pkts = 1000;
+  gpk_replay_stats st;
+  int rc = gpk_replay_file(ctx, p, path, &o, on_results_stop, &a, &st);
+  CHECK(rc == GPK_STOPPED && a.batches == 2 && a.got.n == 2000 && st.packets == 2000,
+        "stop in a callback: %s, %d batches, %llu packets delivered, stats %llu", gpk_strerror(rc), a.batches,
+        (unsigned long long)a.got.n, (unsigned long long)st.packets);
+  CHECK(prefix_equal(&a.got, whole), "stop in a callback: results differ from the whole replay's");
+  /* from another thread, while the replay runs */
+  struct stopper b;
+  memset(&b, 0, sizeof(b));
+  b.ctx = ctx;
+  b.sleep_us = 20000;
+  SR.s = &b;
+  SR.p = p;
+  SR.path = path;
+  pthread_t th;
+  if (pthread_create(&th, NULL, stop_run, NULL)) {
+    CHECK(0, "pthread_create");
+    return;
+  }
+  while (!__atomic_load_n(&b.started, __ATOMIC_SEQ_CST)) {
+    struct timespec ts = {0, 100000};
+    nanosleep(&ts, NULL);
+  }
+  CHECK(gpk_stop(ctx) == GPK_OK, "gpk_stop from another thread");
+  pthread_join(th, NULL);
+  CHECK(SR.rc == GPK_STOPPED && b.got.n == SR.st.packets && b.got.n < whole->n,
+        "stop from another thread: %s, %llu delivered, stats %llu, whole %llu", gpk_strerror(SR.rc),
+        (unsigned long long)b.got.n, (unsigned long long)SR.st.packets, (unsigned long long)whole->n);
+  CHECK(prefix_equal(&b.got, whole), "stop from another thread: results differ from the whole replay's");
+  /* the next call runs to the end */
+  struct collected c;
+  memset(&c, 0, sizeof(c));
+  rc = gpk_replay_file(ctx, p, path, &o, on_results, &c, &st);
+  CHECK(rc == GPK_OK && c.n == whole->n && prefix_equal(&c, whole), "replay after a stop: %s, %llu of %llu",
+        gpk_strerror(rc), (unsigned long long)c.n, (unsigned long long)whole->n);
+  printf("stop: in a callback after 2 of %llu batches, from another thread after %llu packets, then whole again\n",
+         (unsigned long long)((whole->n + 999) / 1000), (unsigned long long)b.got.n);
+}
+
 static int replay_main(const char* path, int T) {
   if (hipGetDeviceCount(&R.ndev) != hipSuccess || R.ndev < 1) return 2;
   FILE* f = fopen(path, "rb");
@@ -317,6 +418,7 @@ static int replay_main(const char* path, int T) {
   gpk_replay_stats st;
   int rc = gpk_replay_file(ctx, p, path, &o, on_results, &whole, &st);
   CHECK(rc == GPK_OK && strcmp(st.error, "EOF") == 0, "whole replay: %s %s", gpk_strerror(rc), st.error);
+  stop_checks(ctx, p, path, &whole);
   /* the ranges, a thread and context each, at once */
   struct worker* w = (struct worker*)calloc(T, sizeof(*w));
   for (int t = 0; t < T; t++) {

@@ -24,7 +24,7 @@ def golden_bytes(name):
 
 
 def read_pcap(path):
-    """Classic pcap (pcapgo/read.go:65-178 semantics for the fixture files)."""
+    """Classic pcap (pcapgo/read.go:65-177 semantics for the fixture files)."""
     raw = open(path, "rb").read()
     magic = struct.unpack("<I", raw[:4])[0]
     if magic in (0xa1b2c3d4, 0xa1b23c4d):

@@ -220,7 +220,7 @@ def test_empty_block_retry_and_vlan_edge_cases():
 
 def test_every_header_empty_goes_round_once():
     """Every header handed over and empty (tp_len 0): the retry releases each
-    one (afpacket.go:371-385, releaseCurrentPacket hands it to the kernel at
+    one (afpacket.go:338-351, releaseCurrentPacket hands it to the kernel at
     once), so the walk comes round to a header the kernel owns and stops there
     instead of circling the ring (found by tests/asan/fuzz_host.cpp: the
     native walk committed its releases only after the step, and looped)."""

@@ -167,8 +167,45 @@ def test_pump_callback_exception_reaches_the_caller(gpu_ctx):
     def boom(first, n, *views):
         raise KeyError("consumer")
 
+    calls = []
+
+    def boom_counted(first, n, *views):
+        calls.append(first)
+        boom(first, n, *views)
+
     with pytest.raises(KeyError):
-        tp.Pump(gpu_ctx, device_parser(CONFIGS["statsassembly"]), batch_pkts=100, collect=False, on_batch=boom)
+        tp.Pump(gpu_ctx, device_parser(CONFIGS["statsassembly"]), batch_pkts=100, collect=False, on_batch=boom_counted)
+    assert calls == [0]  # the exception ended the pump (gpk_stop): no further callback
+    tp.Close()
+
+
+def test_pump_stop_from_a_callback(gpu_ctx):
+    """ctx.stop() inside the third batch's callback ends the pump: no further
+    callback, stats["stopped"], and the delivered packets are the oracle's
+    first ones."""
+    S = _lib.synth_lib()
+    bs, nb = 1 << 20, 4
+    ring = np.zeros(bs * nb, np.uint8)
+    S.gpk_synth_tpacket_v3(ring.ctypes.data, bs, nb, synth.C4_IMIX, 11, 7, 0, None)
+    opts = dict(frame_size=4096, block_size=bs, num_blocks=nb)
+    pk, exp = expect(ring.tobytes(), AO.V3, opts)
+    tp = afpacket.AttachRing(ring, afpacket.TPacketVersion3, afpacket.OptFrameSize(4096), afpacket.OptBlockSize(bs),
+                             afpacket.OptNumBlocks(nb))
+    seen = []
+
+    def stop_at_third(first, n, *views):
+        seen.append((first, n))
+        if len(seen) == 3:
+            gpu_ctx.stop()
+
+    got, st = tp.Pump(gpu_ctx, device_parser(CONFIGS["statsassembly"]), batch_pkts=50, inflight=3,
+                      on_batch=stop_at_third)
+    k = sum(n for _, n in seen)
+    assert st["stopped"] and len(seen) == 3 and st["packets"] == k < len(pk)
+    assert [f for f, _ in seen] == [0, seen[0][1], seen[0][1] + seen[1][1]]
+    data, off, cap = pktutil.pack(pk[:k])
+    ref = oracle_parser(CONFIGS["statsassembly"]).decode(data, off, cap, nthreads=8, layouts=False)
+    assert_same(got, ref, "pump stopped")
     tp.Close()
 
 

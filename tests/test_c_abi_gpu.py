@@ -87,3 +87,4 @@ def test_c_abi_threads_replay_ranges(tmp_path, threads):
     assert out.returncode == 0, out.stdout + out.stderr
     assert "all checks passed (threads replay)" in out.stdout
     assert "= 200000 of 200000, bit-exact" in out.stdout, out.stdout
+    assert "stop: in a callback after 2 of 200 batches" in out.stdout, out.stdout  # gpk_stop, C caller

@@ -11,6 +11,7 @@ import ctypes
 import gzip
 import os
 import random
+import struct
 
 import numpy as np
 import pytest
@@ -24,12 +25,23 @@ FILES = sorted([os.path.join(be, f) for be in ("le", "be") for f in os.listdir(o
 FLAG_SETS = [0, 1, 2, 4, 6, 7]
 
 
+def tlv_options(tlv):
+    """gpk_capreader_packet_options records -> [(code, value)]."""
+    out, p = [], 0
+    while p < len(tlv):
+        code, n = struct.unpack_from("<H2xI", tlv, p)
+        out.append((code, bytes(tlv[p + 8:p + 8 + n])))
+        p += 8 + ((n + 3) & ~3)
+    return out
+
+
 def native_events(stream, fmt, flags, chunk=None, max_pkts=1 << 30, errors=1, max_events=100000):
-    """Drive gpk_capreader_index like a ReadPacketData loop; returns events:
-    ("pkt", abs_offset, caplen, ts_sec, ts_nsec, length, iface, ancil) or ("err", text, panic)."""
+    """Drive gpk_capreader_index like a ReadPacketDataWithOptions loop; returns events:
+    ("pkt", abs_offset, caplen, ts_sec, ts_nsec, length, iface, ancil, options) or ("err", text, panic)."""
     L = _lib.lib()
     h = ctypes.c_void_p()
     _lib.check(L.gpk_capreader_create(ctypes.byref(h), fmt, flags))
+    _lib.check(L.gpk_capreader_keep_options(h, 1))
     ev = []
     base, have = 0, (len(stream) if chunk is None else min(len(stream), chunk))
     nerr = 0
@@ -48,8 +60,11 @@ def native_events(stream, fmt, flags, chunk=None, max_pkts=1 << 30, errors=1, ma
             for i in range(n.value):
                 r = ci[i]
                 assert int(off[i]) + int(cap[i]) <= used.value
+                tlv, nb = ctypes.c_void_p(), ctypes.c_uint64()
+                _lib.check(L.gpk_capreader_packet_options(h, i, ctypes.byref(tlv), ctypes.byref(nb)))
                 ev.append(("pkt", base + int(off[i]), int(cap[i]), int(r["ts_sec"]), int(r["ts_nsec"]),
-                           int(r["length"]), int(r["iface"]), None if int(r["link_type"]) < 0 else int(r["link_type"])))
+                           int(r["length"]), int(r["iface"]), None if int(r["link_type"]) < 0 else int(r["link_type"]),
+                           tlv_options(ctypes.string_at(tlv, nb.value) if nb.value else b"")))
             base += used.value
             if rc == _lib.CAP_END:
                 b = ctypes.create_string_buffer(512)
@@ -97,7 +112,36 @@ def native_meta(L, h, fmt):
                                        end_time=(x.end_time_sec, x.end_time_nsec), comment=s(f, sec, i, 5),
                                        received=x.packets_received, dropped=x.packets_dropped)))
         out.append((info, ifs))
-    return out
+    return dict(sections=out, **native_reader_state(L, h))
+
+
+def native_reader_state(L, h):
+    """Name records, StatisticsCallback and SectionEndCallback calls."""
+    names = []
+    for i in range(L.gpk_capreader_nnames(h)):
+        kind, alen, nn = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        addr = (ctypes.c_uint8 * 24)()
+        need = L.gpk_capreader_name(h, i, ctypes.byref(kind), addr, ctypes.byref(alen), ctypes.byref(nn), None, 0)
+        b = ctypes.create_string_buffer(max(need, 1))
+        assert L.gpk_capreader_name(h, i, None, None, None, None, b, need) == need
+        names.append((kind.value, bytes(addr)[:alen.value], b.raw[:need].split(b"\x00")[:nn.value]))
+    stats = []
+    for k in range(L.gpk_capreader_nstat_events(h)):
+        at, seq, iface, x = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_int(), _lib.NgInterface()
+        n = L.gpk_capreader_stat_event(h, k, ctypes.byref(at), ctypes.byref(seq), ctypes.byref(iface), ctypes.byref(x),
+                                       None, 0)
+        b = ctypes.create_string_buffer(n + 1)
+        L.gpk_capreader_stat_event(h, k, None, None, None, None, b, n + 1)
+        stats.append((at.value, seq.value, iface.value,
+                      dict(last_update=(x.last_update_sec, x.last_update_nsec),
+                           start_time=(x.start_time_sec, x.start_time_nsec), end_time=(x.end_time_sec, x.end_time_nsec),
+                           comment=b.raw[:n], received=x.packets_received, dropped=x.packets_dropped)))
+    ends = []
+    for sec in range(L.gpk_capreader_nsections(h)):
+        at, seq = ctypes.c_uint64(), ctypes.c_uint64()
+        _lib.check(L.gpk_capreader_section_end_at(h, sec, ctypes.byref(at), ctypes.byref(seq)))
+        ends.append((at.value, seq.value))
+    return dict(names=names, stat_events=stats, section_ends=ends)
 
 
 def oracle_events(stream, fmt, flags, errors=1, max_events=100000):
@@ -111,7 +155,7 @@ def oracle_events(stream, fmt, flags, errors=1, max_events=100000):
     while len(ev) < max_events:
         try:
             p = r.read_packet()
-            ev.append(("pkt",) + p.key())
+            ev.append(("pkt",) + p.key() + (list(p.opts),))
         except PO.GoError as e:
             ev.append(("err", e.text, e.panic))
             nerr += 1
@@ -119,8 +163,17 @@ def oracle_events(stream, fmt, flags, errors=1, max_events=100000):
                 break
     meta = None
     if fmt == _lib.CAP_PCAPNG:
-        meta = list(r.ended_sections) + [r.section_state()]
+        meta = oracle_meta(r)
     return ev, meta
+
+
+def oracle_meta(r):
+    return dict(sections=list(r.ended_sections) + [r.section_state()], **oracle_reader_state(r))
+
+
+def oracle_reader_state(r):
+    return dict(names=[(t, a, list(n)) for t, a, n in r.names], stat_events=list(r.stat_events),
+                section_ends=list(r.ended_at))
 
 
 def compare(stream, fmt, flags, chunk=None, errors=1):
@@ -321,8 +374,9 @@ def test_python_mirror_gzip_and_batches():
         pcapgo.NewNgReader(b"")
 
 
-def index_all_events(stream, flags, threads, chunk=None):
-    """gpk_capreader_index_all over the stream (whole or in chunks), as events."""
+def index_all_events(stream, flags, threads, chunk=None, state=False):
+    """gpk_capreader_index_all over the stream (whole or in chunks), as events
+    (state=True: and the reader's name records and callback calls after it)."""
     L = _lib.lib()
     h = ctypes.c_void_p()
     _lib.check(L.gpk_capreader_create(ctypes.byref(h), _lib.CAP_PCAPNG, flags))
@@ -357,9 +411,10 @@ def index_all_events(stream, flags, threads, chunk=None):
                 break
             assert not eof
             have = len(stream) if chunk is None else min(len(stream), have + chunk)
+        st = native_reader_state(L, h)
     finally:
         L.gpk_capreader_destroy(h)
-    return ev
+    return (ev, st) if state else ev
 
 
 def big_capture(n=60000, seed=3):
@@ -384,13 +439,37 @@ def test_parallel_walk_equals_sequential():
     fake = b"".join(pcapgen.epb(bytes([7]) * 40, ts=5) for _ in range(6))
     v.insert(15000, pcapgen.epb(bytes(3) + fake + bytes(5)))
     variants["mixed"] = v
+    # name records after long plain runs (EUI records clone the reader's scratch
+    # buffer: the last block header the speculative walk skipped over) and
+    # statistics blocks (StatisticsCallback's packet count after those runs)
+    w = list(blocks)
+    for at in (9000, 33000, 52000):
+        w.insert(at, pcapgen.nrb([(1, b"\x0a\x00\x00\x01" + b"v4\x00"), (2, bytes(range(16)) + b"v6\x00x\x00")]))
+        w.insert(at + 1, pcapgen.isb(1, at, options=pcapgen.opt(4, struct.pack("<Q", at)) + pcapgen.end_opt()))
+    # an EUI record desynchronises the rest of the stream as in Go: the last block
+    w.append(pcapgen.nrb([(1, b"\x0a\x00\x00\x02" + b"w\x00"), (3, bytes(range(6)) + b"eui48\x00")]))
+    variants["names"] = w
     for name, bl in variants.items():
         data = head + b"".join(bl)
         for flags in (0, 1, 2):
-            want, _ = native_events(data, _lib.CAP_PCAPNG, flags, errors=1, max_events=10 ** 7)
+            want, meta = native_events(data, _lib.CAP_PCAPNG, flags, errors=1, max_events=10 ** 7)
+            want = [e[:8] if e[0] == "pkt" else e for e in want]  # (index_all keeps no options)
+            wstate = {k: meta[k] for k in ("names", "stat_events", "section_ends")}
             for threads in (1, 3, 8):
-                assert index_all_events(data, flags, threads) == want, (name, flags, threads)
-            assert index_all_events(data, flags, 8, chunk=(5 << 20) + 13) == want, (name, flags)
+                assert index_all_events(data, flags, threads, state=True) == (want, wstate), (name, flags, threads)
+            assert index_all_events(data, flags, 8, chunk=(5 << 20) + 13, state=True) == (want, wstate), (name, flags)
+        if name == "names":
+            # an EUI record clones the reader's whole scratch buffer: its first 6 bytes,
+            # the NRB block length's high half, then the ts-low / caplen / length words
+            # the last EPB header before the block left there (a plain run the
+            # speculative walk took); the reference's 24-byte address length then
+            # desynchronises the rest of the block, as in Go (ngread_nrb.go:56-61,108)
+            nm = wstate["names"]
+            assert nm[:2] == [(1, b"\x0a\x00\x00\x01", [b"v4"]), (2, bytes(range(16)), [b"v6", b"x"])]
+            assert len(nm) == 8 and nm[6] == (1, b"\x0a\x00\x00\x02", [b"w"]) and nm[7][0] == 3
+            prev = blocks[-1]
+            assert nm[7][1][:6] == bytes(range(6)) and nm[7][1][8:20] == prev[16:28] and nm[7][1][20:] == bytes(4)
+            assert [e[0] for e in wstate["stat_events"]] == [9000, 33000 - 2, 52000 - 4]  # packets before each
 
 
 def pcapgen_payload(block):

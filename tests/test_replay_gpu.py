@@ -153,11 +153,11 @@ def test_replay_device_walk_corrupt(gpu_ctx, tmp_path, seed):
     byte of a block length, interface id, capture length, original length,
     trailer, packet bytes. The device walk must stop at every block that is not
     a plain EPB and leave it to the host reader, which desynchronises or fails
-    exactly as Go's reader does (ngread.go:494-585); packets, capture info and
+    exactly as Go's reader does (ngread.go:494-580); packets, capture info and
     the reader's error then match the reader oracle. One record longer than
     the staging carry region ends the call with GPK_EUNSUPP by design: the
     flips keep block lengths small, but Go reads options past a short block
-    (ngread.go:199-236), so a shrunk capture length can make the following
+    (ngread.go:196-234), so a shrunk capture length can make the following
     megabytes one record's options. Small slots may refuse such a file; the
     default slots must match the oracle."""
     from gopacket_amd import _lib
@@ -188,7 +188,7 @@ def test_replay_device_walk_corrupt(gpu_ctx, tmp_path, seed):
 def test_replay_pcap_corrupt(gpu_ctx, tmp_path, seed):
     """Classic pcap with byte flips in record headers (timestamps, capture
     length, original length), both byte orders, micro- and nanosecond files:
-    Reader.ReadPacketData's checks (read.go:124-178: capture length over the
+    Reader.ReadPacketData's checks (read.go:122-177: capture length over the
     snap length or over the original length) end the stream where Go's do,
     and every packet before matches the reader and decode oracles."""
     import struct
@@ -319,10 +319,76 @@ def test_replay_callback_exception_reaches_the_caller(gpu_ctx, capture):
     def boom(first, n, *views):
         raise ValueError("consumer failed at packet %d" % first)
 
+    calls = []
+
+    def boom_counted(first, n, *views):
+        calls.append(first)
+        boom(first, n, *views)
+
     with pytest.raises(ValueError, match="consumer failed at packet 0"):
-        gpu_ctx.replay_file(device_parser(CONFIGS["statsassembly"]), path, collect=False, on_batch=boom,
+        gpu_ctx.replay_file(device_parser(CONFIGS["statsassembly"]), path, collect=False, on_batch=boom_counted,
                             slot_bytes=1 << 20, slots=2, batch_pkts=5000)
+    assert calls == [0]  # the exception ended the call (gpk_stop): no further callback
     check(gpu_ctx, path, raw, slot_bytes=1 << 20, slots=2, batch_pkts=5000)
+
+
+@pytest.mark.parametrize("packets", [False, True])
+def test_replay_stop_from_a_callback(gpu_ctx, capture, packets):
+    """ctx.stop() (gpk_stop) inside the second batch's callback: a Go caller's
+    break out of its ReadPacketData loop. No further callback, GPK_STOPPED
+    (stats["stopped"]), stats["packets"] = the packets delivered, and those
+    results are the whole-file replay's first packets; the next call on the
+    context runs to the end."""
+    path, raw = capture
+    res, pk = packets_and_expect(raw)
+    firsts = []
+
+    def stop_at_second(first, n, rec, err, fl, ci, cap, *rest):
+        firsts.append((first, n))
+        if len(firsts) == 2:
+            gpu_ctx.stop()
+
+    got, st = gpu_ctx.replay_file(device_parser(CONFIGS["statsassembly"]), path, collect=not packets,
+                                  on_batch=stop_at_second, packets=packets, slot_bytes=1 << 18, slots=3,
+                                  batch_pkts=700)
+    k = sum(n for _, n in firsts)  # (a launch holds at most 700 packets, fewer at a staging slot's end)
+    assert st["stopped"] and len(firsts) == 2 and firsts[1][0] == firsts[0][1] and st["packets"] == k
+    full, st2 = gpu_ctx.replay_file(device_parser(CONFIGS["statsassembly"]), path, slot_bytes=1 << 18, slots=3,
+                                    batch_pkts=700)
+    assert not st2["stopped"] and st2["packets"] == len(pk)
+    if not packets:
+        for key in ("records", "ci", "caplens"):
+            assert np.array_equal(got[key], full[key][:k]), key
+        assert np.array_equal(got["err_args"], full["err_args"][:2 * k])
+        assert np.array_equal(got["flows"].reshape(3, -1), full["flows"].reshape(3, -1)[:, :k])
+
+
+def test_replay_stop_from_another_thread(gpu_ctx, capture):
+    """gpk_stop from a thread other than the replay's: the replay ends early
+    with every delivered batch whole."""
+    import threading
+    import time
+    path, raw = capture
+    started, seen = threading.Event(), []
+
+    def slow(first, n, *views):
+        seen.append((first, n))
+        started.set()
+        time.sleep(0.02)
+
+    out = {}
+    t = threading.Thread(target=lambda: out.update(r=gpu_ctx.replay_file(
+        device_parser(CONFIGS["statsassembly"]), path, collect=False, on_batch=slow, slot_bytes=1 << 18, slots=3,
+        batch_pkts=300)))
+    t.start()
+    assert started.wait(60)
+    gpu_ctx.stop()
+    t.join(120)
+    assert not t.is_alive()
+    _, st = out["r"]
+    total = len(packets_and_expect(raw)[1])
+    assert st["stopped"] and st["packets"] == sum(n for _, n in seen) < total
+    assert [f for f, _ in seen] == list(np.cumsum([0] + [n for _, n in seen])[:-1])
 
 
 def test_replay_packets_and_hydrate(gpu_ctx, capture):

@@ -111,7 +111,7 @@ def test_range_default_opts_and_fields(gpu_ctx, imix):
 def test_range_option_blocks_are_state(gpu_ctx, tmp_path):
     """An EPB with options and an interface statistics block change reader
     state a later block can read (NgReader reuses one option buffer: a
-    zero-length option keeps the previous value, ngread.go:215-219), so the
+    zero-length option keeps the previous value, ngread.go:214-219), so the
     range holding either is not exact for the ranges after it; a name record
     changes nothing. Three files, one of each, split 2 ways with the block in
     the first half."""

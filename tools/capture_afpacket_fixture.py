@@ -4,7 +4,7 @@ store them as fixtures (tests/golden/afpacket/): the ring bytes exactly as the
 Linux kernel laid them out, plus the datagrams that were sent.
 
 These pin the header layouts the ring walker and its oracle assume
-(afpacket/header.go:60-127) to what the kernel actually writes. Needs
+(afpacket/header.go:59-137) to what the kernel actually writes. Needs
 CAP_NET_RAW (root in this container); plain Python sockets, no product code.
 
     python tools/capture_afpacket_fixture.py
