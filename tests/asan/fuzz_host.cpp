@@ -165,6 +165,30 @@ void metadata(gpk_capreader* rd) {
       g_sink += gpk_capreader_interface(rd, sec, i, &itf);
       for (int f = -1; f <= 6; f++) g_sink += gpk_capreader_interface_str(rd, sec, i, f, s, sizeof(s));
     }
+    uint64_t at = 0, seq = 0;
+    g_sink += gpk_capreader_section_end_at(rd, sec, &at, &seq) + at + seq;
+  }
+  // name records, statistics callbacks (every index, a few out of range)
+  const int nn = gpk_capreader_nnames(rd);
+  for (int i = -1; i <= nn; i++) {
+    int kind = 0, alen = 0, nnames = 0;
+    uint8_t addr[24];
+    const int need = gpk_capreader_name(rd, i, &kind, addr, &alen, &nnames, nullptr, 0);
+    if (need >= 0) {
+      CHECK(alen == 4 || alen == 16 || alen == 24);
+      std::vector<char> names((size_t)need + 1);
+      CHECK(gpk_capreader_name(rd, i, nullptr, nullptr, nullptr, nullptr, names.data(), (size_t)need) == need);
+      CHECK(gpk_capreader_name(rd, i, nullptr, nullptr, nullptr, nullptr, names.data(), (size_t)need / 2) == need);
+      g_sink += touch(addr, (uint64_t)alen) + (uint64_t)nnames;
+    }
+  }
+  const int ne = gpk_capreader_nstat_events(rd);
+  for (int k = -1; k <= ne; k++) {
+    uint64_t at = 0, seq = 0;
+    int iface = 0;
+    gpk_ng_interface st;
+    g_sink += gpk_capreader_stat_event(rd, k, &at, &seq, &iface, &st, s, sizeof(s)) + at + seq;
+    g_sink += gpk_capreader_stat_event(rd, k, nullptr, nullptr, nullptr, nullptr, s, 1);
   }
 }
 
@@ -172,8 +196,12 @@ void run_capture(const std::vector<uint8_t>& file, int fmt, Rng& r) {
   const uint32_t flags = (uint32_t)r.below(8);
   gpk_capreader* rd = nullptr;
   CHECK(gpk_capreader_create(&rd, fmt, flags) == GPK_OK);
+  const bool opts = r.chance(0.7);  // ReadPacketDataWithOptions: the options kept per packet
+  CHECK(gpk_capreader_keep_options(rd, opts ? 1 : 0) == GPK_OK);
+  if (fmt == GPK_CAP_PCAP && r.chance(0.3)) CHECK(gpk_capreader_set_snaplen(rd, (uint32_t)r.next()) == GPK_OK);
   uint64_t pos = 0, chunk = 1 + r.below(std::max<uint64_t>(1, file.size())), calls = 0, ends = 0;
   while (calls++ < 4096) {
+    if (fmt == GPK_CAP_PCAPNG && r.chance(0.02)) g_sink += (uint64_t)gpk_capreader_skip_section(rd);
     const uint64_t avail = std::min<uint64_t>(file.size() - pos, chunk);
     const int eof = pos + avail == file.size();
     Exact in(file.data() + pos, avail);
@@ -189,7 +217,21 @@ void run_capture(const std::vector<uint8_t>& file, int fmt, Rng& r) {
     for (uint64_t i = 0; i < n; i++) {
       CHECK(off[i] + cap[i] <= used);
       g_sink += touch(in.data() + off[i], cap[i]);
+      const uint8_t* tlv = nullptr;
+      uint64_t nb = 0;
+      if (opts) {
+        CHECK(gpk_capreader_packet_options(rd, i, &tlv, &nb) == GPK_OK);
+        for (uint64_t q = 0; q < nb;) {  // well-formed records, inside the bytes given
+          uint32_t len = 0;
+          CHECK(q + 8 <= nb);
+          memcpy(&len, tlv + q + 4, 4);
+          q += 8 + ((len + 3ull) & ~3ull);
+          CHECK(q <= nb);
+        }
+        g_sink += touch(tlv, nb);
+      }
     }
+    if (opts) CHECK(gpk_capreader_packet_options(rd, n, nullptr, nullptr) == GPK_EINVAL);
     pos += used;
     if (rc == GPK_CAP_END) {
       metadata(rd);
