@@ -93,6 +93,7 @@ EXPORTS = (
     "gpk_tpacket_ring", "gpk_tpacket_index", "gpk_tpacket_defer", "gpk_tpacket_set_threads", "gpk_tpacket_release_seq", "gpk_tpacket_release",
     "gpk_tpacket_take_new_headers", "gpk_tpacket_geometry", "gpk_tpacket_error", "gpk_tpacket_stats",
     "gpk_tpacket_socket_stats", "gpk_tpacket_set_bpf", "gpk_tpacket_set_fanout", "gpk_tpacket_pump",
+    "gpk_tpacket_set_ebpf", "gpk_tpacket_set_promiscuous", "gpk_tpacket_write", "gpk_tpacket_init_socket_stats",
     # include/gpk_flows.h
     "gpk_grouper_create", "gpk_grouper_destroy", "gpk_group_batch", "gpk_pack_batch", "gpk_decode_group_batch",
     # include/gpk_bpf.h
@@ -329,6 +330,10 @@ def lib():
         "gpk_tpacket_socket_stats": ([vp, P(u32), P(u32), P(u32)], c_int),
         "gpk_tpacket_set_bpf": ([vp, vp, u32], c_int),
         "gpk_tpacket_set_fanout": ([vp, c_int, ctypes.c_uint16], c_int),
+        "gpk_tpacket_set_ebpf": ([vp, ctypes.c_int32], c_int),
+        "gpk_tpacket_set_promiscuous": ([vp, c_int], c_int),
+        "gpk_tpacket_write": ([vp, vp, ctypes.c_uint64], c_int),
+        "gpk_tpacket_init_socket_stats": ([vp], c_int),
         "gpk_tpacket_pump": ([vp, vp, vp, P(PumpOpts), PUMP_CB, vp, P(PumpStats)], c_int),
         "gpk_grouper_create": ([P(vp), c_int, u64], c_int),
         "gpk_grouper_destroy": ([vp], c_int),

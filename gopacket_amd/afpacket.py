@@ -10,6 +10,8 @@ Mirrors the reference's afpacket package for the ingest side of the path
   TPacket.ReadPacketData() / ReadPacketDataTo afpacket.go:438-460
   TPacket.Stats() / SocketStats()             afpacket.go:370-431
   TPacket.SetBPF / SetFanout / Close          afpacket.go:297-309,542-548,243-254
+  TPacket.SetEBPF / SetPromiscuous            afpacket.go:312-314,552-564
+  TPacket.WritePacketData / InitSocketStats   afpacket.go:567-570,378-399
 
 plus what the reference has no counterpart for:
 
@@ -223,6 +225,19 @@ class TPacket:
 
     def SetFanout(self, t, id_):
         _lib.check(_lib.lib().gpk_tpacket_set_fanout(self.h, int(t), int(id_)))
+
+    def SetEBPF(self, prog_fd):  # afpacket.go:312-314
+        _lib.check(_lib.lib().gpk_tpacket_set_ebpf(self.h, int(prog_fd)))
+
+    def SetPromiscuous(self, on):  # afpacket.go:552-564
+        _lib.check(_lib.lib().gpk_tpacket_set_promiscuous(self.h, 1 if on else 0))
+
+    def WritePacketData(self, pkt):  # afpacket.go:567-570
+        b = bytes(pkt)
+        _lib.check(_lib.lib().gpk_tpacket_write(self.h, b, len(b)))
+
+    def InitSocketStats(self):  # afpacket.go:378-399
+        _lib.check(_lib.lib().gpk_tpacket_init_socket_stats(self.h))
 
     def Pump(self, ctx, parser, batch_pkts=0, max_packets=0, wait=False, inflight=0, collect=True, on_batch=None,
              fields=False, packets=False):

@@ -168,6 +168,7 @@ struct gpk_tpacket {
   int version = GPK_TPACKET_V3;
   gpk_tp_opts o{};
   int fd = -1;
+  int ifindex = 0;  // the interface bound to (0: every interface), for SetPromiscuous
   bool mapped = false;
   uint64_t hdr_bytes = 0, nhdr = 0;
   GoState s;
@@ -792,6 +793,7 @@ int gpk_tpacket_new(gpk_tpacket** out, const gpk_tp_opts* o, char* err, size_t c
   t->version = version;
   t->o = oc;
   t->fd = fd;
+  t->ifindex = ifindex;
   t->mapped = true;
   init_geometry(t);
   *out = t;
@@ -999,6 +1001,36 @@ int gpk_tpacket_set_fanout(gpk_tpacket* t, int type, uint16_t id) {
   if (!t || t->fd < 0) return GPK_EINVAL;
   int arg = (type << 16) | id;
   return setsockopt(t->fd, SOL_PACKET, PACKET_FANOUT, &arg, sizeof(arg)) == 0 ? GPK_OK : GPK_EINVAL;
+}
+
+int gpk_tpacket_set_ebpf(gpk_tpacket* t, int32_t prog_fd) {  // SetEBPF (afpacket.go:312-314)
+  if (!t || t->fd < 0) return GPK_EINVAL;
+  return setsockopt(t->fd, SOL_SOCKET, SO_ATTACH_BPF, &prog_fd, sizeof(prog_fd)) == 0 ? GPK_OK : GPK_EINVAL;
+}
+
+int gpk_tpacket_set_promiscuous(gpk_tpacket* t, int on) {  // SetPromiscuous (afpacket.go:552-564)
+  if (!t || t->fd < 0) return GPK_EINVAL;
+  struct packet_mreq mr;
+  memset(&mr, 0, sizeof(mr));
+  mr.mr_ifindex = t->ifindex;
+  mr.mr_type = PACKET_MR_PROMISC;
+  return setsockopt(t->fd, SOL_PACKET, on ? PACKET_ADD_MEMBERSHIP : PACKET_DROP_MEMBERSHIP, &mr, sizeof(mr)) == 0
+             ? GPK_OK
+             : GPK_EINVAL;
+}
+
+int gpk_tpacket_write(gpk_tpacket* t, const void* pkt, uint64_t n) {  // WritePacketData (afpacket.go:567-570)
+  if (!t || t->fd < 0 || (!pkt && n)) return GPK_EINVAL;
+  return write(t->fd, pkt, (size_t)n) >= 0 ? GPK_OK : GPK_EINVAL;
+}
+
+int gpk_tpacket_init_socket_stats(gpk_tpacket* t) {  // InitSocketStats (afpacket.go:378-399)
+  if (!t || t->fd < 0) return GPK_EINVAL;
+  struct tpacket_stats_v3 st{};
+  socklen_t sl = t->version == GPK_TPACKET_V3 ? sizeof(struct tpacket_stats_v3) : sizeof(struct tpacket_stats);
+  if (getsockopt(t->fd, SOL_PACKET, PACKET_STATISTICS, &st, &sl) < 0) return GPK_EINVAL;
+  t->ss_packets = t->ss_drops = t->ss_freeze = 0;
+  return GPK_OK;
 }
 
 }  // extern "C"

@@ -20,6 +20,9 @@
  *                                             :316-321) over the v1/v2/v3 headers of header.go
  *   gpk_tpacket_stats / _socket_stats         TPacket.Stats :370-375, SocketStats :402-431
  *   gpk_tpacket_set_bpf / _set_fanout         TPacket.SetBPF :297-309, SetFanout :542-548
+ *   gpk_tpacket_set_ebpf / _set_promiscuous   TPacket.SetEBPF :312-314, SetPromiscuous :552-564
+ *   gpk_tpacket_write                         TPacket.WritePacketData :567-570
+ *   gpk_tpacket_init_socket_stats             TPacket.InitSocketStats :378-399
  *   gpk_tpacket_pump                          the capture loop: ZeroCopyReadPacketData +
  *                                             DecodingLayerParser.DecodeLayers per packet,
  *                                             pipelined through HBM
@@ -135,6 +138,15 @@ int gpk_tpacket_socket_stats(gpk_tpacket* t, uint32_t* packets, uint32_t* drops,
 /* SetBPF with classic BPF instructions {code u16, jt u8, jf u8, k u32}; n = 0 detaches. */
 int gpk_tpacket_set_bpf(gpk_tpacket* t, const void* insns, uint32_t n);
 int gpk_tpacket_set_fanout(gpk_tpacket* t, int type, uint16_t id);
+/* SetEBPF: attach the eBPF program prog_fd (SO_ATTACH_BPF). SetPromiscuous:
+ * PACKET_MR_PROMISC membership on the bound interface (on != 0 adds, 0 drops).
+ * WritePacketData: write the frame to the socket (transmit). InitSocketStats:
+ * read and clear the kernel's counters and the accumulated ones. Socket
+ * readers only (GPK_EINVAL on an attached ring or when the kernel refuses). */
+int gpk_tpacket_set_ebpf(gpk_tpacket* t, int32_t prog_fd);
+int gpk_tpacket_set_promiscuous(gpk_tpacket* t, int on);
+int gpk_tpacket_write(gpk_tpacket* t, const void* pkt, uint64_t n);
+int gpk_tpacket_init_socket_stats(gpk_tpacket* t);
 
 /* ---- the capture loop through the GPU ------------------------------------ */
 /* Per batch, before its gpk_tp_pump_cb: the layer fields of its n packets

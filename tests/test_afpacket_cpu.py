@@ -365,6 +365,49 @@ def test_live_loopback_capture(version):
     tp.Close()
 
 
+@pytest.mark.skipif(not _can_capture(), reason="AF_PACKET sockets need CAP_NET_RAW")
+def test_live_write_promiscuous_ebpf_socket_stats():
+    """WritePacketData (afpacket.go:567-570) transmits a frame on lo that a second
+    TPacket captures byte for byte; SetPromiscuous (:552-564) on and off;
+    SetEBPF (:312-314) with no program is refused by the kernel; InitSocketStats
+    (:378-399) clears the accumulated socket counters. An attached ring has no
+    socket: every one of them is refused."""
+    rx = afpacket.NewTPacket(afpacket.OptInterface("lo"), afpacket.OptTPacketVersion(afpacket.TPacketVersion3),
+                             afpacket.OptFrameSize(2048), afpacket.OptBlockSize(1 << 16), afpacket.OptNumBlocks(8),
+                             afpacket.OptBlockTimeout(5_000_000), afpacket.OptPollTimeout(2_000_000_000))
+    tx = afpacket.NewTPacket(afpacket.OptInterface("lo"), afpacket.OptTPacketVersion(afpacket.TPacketVersion2),
+                             afpacket.OptFrameSize(2048), afpacket.OptBlockSize(1 << 16), afpacket.OptNumBlocks(2))
+    try:
+        rx.SetPromiscuous(True)
+        rx.SetPromiscuous(False)
+        frames = [b"\x02" * 6 + b"\x04" * 6 + b"\x88\xb5" + bytes([i]) * (46 + 13 * i) for i in range(6)]
+        for f in frames:
+            tx.WritePacketData(f)
+        got = []
+        while len(got) < len(frames):
+            d, ci = rx.ReadPacketData()
+            if d[12:14] == b"\x88\xb5" and d not in got:
+                got.append(d)
+        assert got == frames
+        before = rx.SocketStats()[1].Packets()  # (a V3 socket: the SocketStatsV3 half)
+        assert before >= len(frames)
+        rx.InitSocketStats()
+        assert rx.SocketStats()[1].Packets() < before  # the accumulated count starts again
+        with pytest.raises(_lib.GpkError):
+            rx.SetEBPF(-1)
+    finally:
+        rx.Close()
+        tx.Close()
+    ring = np.zeros(1 << 16, np.uint8)
+    tp = afpacket.AttachRing(ring, afpacket.TPacketVersion3, afpacket.OptFrameSize(4096),
+                             afpacket.OptBlockSize(1 << 16), afpacket.OptNumBlocks(1))
+    for call in (lambda: tp.SetPromiscuous(True), lambda: tp.WritePacketData(b"x"), lambda: tp.SetEBPF(3),
+                 tp.InitSocketStats):
+        with pytest.raises(_lib.GpkError):
+            call()
+    tp.Close()
+
+
 @pytest.mark.parametrize("vlan", [False, True])
 def test_parallel_prewalk_equals_sequential_walk(vlan):
     """Calls of >= 4096 packets take V3 blocks from the parallel pre-walk; the
