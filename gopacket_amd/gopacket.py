@@ -2,7 +2,8 @@
 
 Mirrors (reference file:line):
   LayerType / LayerTypeZero.. (layertype.go:20-111, decode.go:106-117)
-  Endpoint, Flow, NewFlow, FastHash (flows.go:27-224)
+  Endpoint, Flow, NewFlow, NewEndpoint, FlowFromEndpoints, LessThan, FastHash,
+  RegisterEndpointType / EndpointType names (flows.go:27-236, layers/endpoints.go:17-49)
   ChecksumVerificationResult (checksum.go:14-21)
   Payload, Fragment DecodingLayers (base.go:40-124)
   DecodingLayerParser, NewDecodingLayerParser, DecodeLayers, AddDecodingLayer,
@@ -96,7 +97,6 @@ class ChecksumVerificationResult:
     Actual: int = 0
 
 
-EndpointInvalid, EndpointIPv4, EndpointIPv6, EndpointMAC, EndpointTCPPort, EndpointUDPPort = 0, 1, 2, 3, 4, 5
 MaxEndpointSize = 16
 _FNV_BASIS = 14695981039346656037
 _FNV_PRIME = 1099511628211
@@ -110,19 +110,86 @@ def _fnv(b):
     return h
 
 
+def _go_bytes(b):  # fmt's %v of a []byte / [N]byte: "[1 2 3]"
+    return "[" + " ".join(str(x) for x in b) + "]"
+
+
+def _ip_string(b):
+    """net.IP.String (Go): dotted for 4 bytes and IPv4-mapped 16, RFC 5952 for IPv6."""
+    import ipaddress
+    if len(b) == 0:
+        return "<nil>"
+    if len(b) == 4:
+        return str(ipaddress.IPv4Address(bytes(b)))
+    if len(b) == 16:
+        if b[:10] == bytes(10) and b[10:12] == b"\xff\xff":
+            return str(ipaddress.IPv4Address(bytes(b[12:])))
+        return ipaddress.IPv6Address(bytes(b)).compressed
+    return "?" + bytes(b).hex()
+
+
+@dataclass
+class EndpointTypeMetadata:  # flows.go:99-106
+    Name: str
+    Formatter: object = None  # bytes -> str
+
+
+_endpoint_types = {}
+
+
+class EndpointType(int):
+    """flows.go:108-131: registered types print their name, others their number."""
+
+    def String(self):
+        m = _endpoint_types.get(int(self))
+        return m.Name if m is not None else str(int(self))
+
+    __str__ = String
+
+
+def RegisterEndpointType(num, meta):
+    """flows.go:117-124 (panics on a number already in use)."""
+    if num in _endpoint_types:
+        raise GoPanic("Endpoint type number already in use")
+    _endpoint_types[num] = meta
+    return EndpointType(num)
+
+
+def _port(b):
+    if len(b) < 2:  # binary.BigEndian.Uint16: _ = b[1]
+        raise GoPanic("runtime error: index out of range [1] with length %d" % len(b))
+    return str(struct.unpack(">H", bytes(b[:2]))[0])
+
+
+EndpointInvalid = RegisterEndpointType(0, EndpointTypeMetadata("invalid", _go_bytes))  # flows.go:228-230
+# layers/endpoints.go:21-48
+EndpointIPv4 = RegisterEndpointType(1, EndpointTypeMetadata("IPv4", _ip_string))
+EndpointIPv6 = RegisterEndpointType(2, EndpointTypeMetadata("IPv6", _ip_string))
+EndpointMAC = RegisterEndpointType(3, EndpointTypeMetadata("MAC", lambda b: ":".join("%02x" % x for x in b)))
+EndpointTCPPort = RegisterEndpointType(4, EndpointTypeMetadata("TCP", _port))
+EndpointUDPPort = RegisterEndpointType(5, EndpointTypeMetadata("UDP", _port))
+EndpointSCTPPort = RegisterEndpointType(6, EndpointTypeMetadata("SCTP", _port))
+EndpointRUDPPort = RegisterEndpointType(7, EndpointTypeMetadata("RUDP", lambda b: str(b[0])))
+EndpointUDPLitePort = RegisterEndpointType(8, EndpointTypeMetadata("UDPLite", _port))
+EndpointPPP = RegisterEndpointType(9, EndpointTypeMetadata("PPP", lambda b: "point"))
+
+
 class Endpoint:
-    """flows.go:32-97"""
+    """flows.go:32-97, 133-138"""
 
     def __init__(self, typ, raw):
         if len(raw) > MaxEndpointSize:
             raise GoPanic("raw byte length greater than MaxEndpointSize")
-        self.typ, self.raw = typ, bytes(raw)
+        self.typ, self.raw = EndpointType(typ), bytes(raw)
 
     def EndpointType(self):
         return self.typ
 
     def Raw(self):
         return self.raw
+
+    def LessThan(self, b):  # flows.go:53-55
+        return self.typ < b.typ or (self.typ == b.typ and self.raw < b.raw)
 
     def FastHash(self):
         return ((_fnv(self.raw) ^ self.typ) * _FNV_PRIME) & _M64
@@ -134,16 +201,17 @@ class Endpoint:
         return hash((self.typ, self.raw))
 
     def String(self):
-        if self.typ in (EndpointIPv4, EndpointIPv6):
-            import ipaddress
-            return str(ipaddress.ip_address(self.raw))
-        if self.typ == EndpointMAC:
-            return ":".join("%02x" % b for b in self.raw)
-        if self.typ in (EndpointTCPPort, EndpointUDPPort):
-            return str(struct.unpack(">H", self.raw)[0])
-        return "%d:%s" % (self.typ, list(self.raw))
+        m = _endpoint_types.get(int(self.typ))
+        if m is not None and m.Formatter is not None:
+            return m.Formatter(self.raw)
+        return "%s:%s" % (self.typ.String(), _go_bytes(self.raw.ljust(MaxEndpointSize, b"\x00")))  # %v of the [16]byte
 
     __str__ = String
+
+
+def NewEndpoint(typ, raw):
+    """flows.go:89-97"""
+    return Endpoint(typ, raw)
 
 
 class Flow:
@@ -153,7 +221,7 @@ class Flow:
     def __init__(self, typ, src, dst, fast_hash=None):
         if len(src) > MaxEndpointSize or len(dst) > MaxEndpointSize:
             raise GoPanic("flow raw byte length greater than MaxEndpointSize")
-        self.typ, self.src, self.dst = typ, bytes(src), bytes(dst)
+        self.typ, self.src, self.dst = EndpointType(typ), bytes(src), bytes(dst)
         self._hash = fast_hash
 
     def FastHash(self):
@@ -190,6 +258,17 @@ class Flow:
 
 def NewFlow(t, src, dst):
     return Flow(t, src, dst)
+
+
+def FlowFromEndpoints(src, dst):
+    """flows.go:151-157: (Flow, None), or (the zero Flow, error) for mismatched types."""
+    if src.typ != dst.typ:
+        return Flow(0, b"", b""), GoError("Mismatched endpoint types: %s->%s" % (src.typ.String(), dst.typ.String()))
+    return Flow(src.typ, src.raw, dst.raw), None
+
+
+InvalidEndpoint = NewEndpoint(EndpointInvalid, b"")  # flows.go:233
+InvalidFlow = NewFlow(EndpointInvalid, b"", b"")      # flows.go:236
 
 
 # ---- Payload / Fragment ----------------------------------------------------

@@ -23,7 +23,9 @@ from typing import List, Optional
 
 from . import _lib
 from .gopacket import (ChecksumVerificationResult, Flow, LayerClass, LayerType, NewFlow, EndpointIPv4, EndpointIPv6,
-                       EndpointMAC, EndpointTCPPort, EndpointUDPPort, LayerTypeFragment, LayerTypePayload)
+                       EndpointMAC, EndpointTCPPort, EndpointUDPPort, EndpointSCTPPort, EndpointRUDPPort,
+                       EndpointUDPLitePort, EndpointPPP, InvalidEndpoint, NewEndpoint, LayerTypeFragment,
+                       LayerTypePayload)
 
 _REG = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "registry_gen.json")))
 
@@ -766,3 +768,54 @@ class UDP(BaseLayer, _Checksummed):
 
 
 __all__ = [n for n in dir() if not n.startswith("_")]
+
+
+# ---- endpoints (layers/endpoints.go:51-99) --------------------------------------
+
+
+def _to4(ip):  # net.IP.To4
+    if len(ip) == 4:
+        return ip
+    if len(ip) == 16 and ip[:10] == bytes(10) and ip[10:12] == b"\xff\xff":
+        return ip[12:]
+    return None
+
+
+def NewIPEndpoint(ip):
+    """An IPv4 endpoint for a 4-byte or IPv4-mapped address, IPv6 for another
+    16-byte one, InvalidEndpoint otherwise (ip: bytes or an ipaddress object)."""
+    b = ip.packed if hasattr(ip, "packed") else bytes(ip)
+    v4 = _to4(b)
+    if v4 is not None:
+        return NewEndpoint(EndpointIPv4, v4)
+    if len(b) == 16:
+        return NewEndpoint(EndpointIPv6, b)
+    return InvalidEndpoint
+
+
+def NewMACEndpoint(mac):
+    return NewEndpoint(EndpointMAC, bytes(mac))
+
+
+def _port_endpoint(t, p):
+    return NewEndpoint(t, bytes([(p >> 8) & 0xFF, p & 0xFF]))
+
+
+def NewTCPPortEndpoint(p):
+    return _port_endpoint(EndpointTCPPort, int(p))
+
+
+def NewUDPPortEndpoint(p):
+    return _port_endpoint(EndpointUDPPort, int(p))
+
+
+def NewSCTPPortEndpoint(p):
+    return _port_endpoint(EndpointSCTPPort, int(p))
+
+
+def NewRUDPPortEndpoint(p):
+    return NewEndpoint(EndpointRUDPPort, bytes([int(p) & 0xFF]))
+
+
+def NewUDPLitePortEndpoint(p):
+    return _port_endpoint(EndpointUDPLitePort, int(p))
