@@ -4,7 +4,9 @@ Mirrors (reference file:line):
   LayerType / LayerTypeZero.. (layertype.go:20-111, decode.go:106-117)
   Endpoint, Flow, NewFlow, NewEndpoint, FlowFromEndpoints, LessThan, FastHash,
   RegisterEndpointType / EndpointType names (flows.go:27-236, layers/endpoints.go:17-49)
-  ChecksumVerificationResult (checksum.go:14-21)
+  ChecksumVerificationResult, ComputeChecksum, FoldChecksum (checksum.go:14-58)
+  RegisterLayerType / OverrideLayerType / LayerTypeMetadata (layertype.go:22-83)
+  LayerClassSlice / LayerClassMap / NewLayerClass (layerclass.go:9-107)
   Payload, Fragment DecodingLayers (base.go:40-124)
   DecodingLayerParser, NewDecodingLayerParser, DecodeLayers, AddDecodingLayer,
   UnsupportedLayerType, DecodingLayerParserOptions (parser.go:182-351)
@@ -27,15 +29,49 @@ _LT_NAMES = {int(k): v for k, v in _REG["layer_type_names"].items()}
 
 
 class LayerType(int):
-    """gopacket.LayerType (layertype.go:20); String() per layertype.go:101-111."""
+    """gopacket.LayerType (layertype.go:20); String() per layertype.go:101-111;
+    a LayerType is a LayerClass of itself (layerclass.go:21-29)."""
 
     def String(self):
-        return _LT_NAMES.get(int(self), str(int(self)))
+        s = _LT_NAMES.get(int(self), "")
+        return s if s else str(int(self))
 
     __str__ = String
 
     def __repr__(self):
         return "LayerType(%s)" % self.String()
+
+    def Contains(self, a):
+        return int(self) == int(a)
+
+    def LayerTypes(self):
+        return [self]
+
+
+@dataclass
+class LayerTypeMetadata:  # layertype.go:22-29 (Decoder: the NewPacket path, outside the hot path)
+    Name: str
+    Decoder: object = None
+
+
+DecodersByLayerName = {}  # layertype.go:39
+_LT_IN_USE = set(_LT_NAMES)
+
+
+def RegisterLayerType(num, meta):
+    """layertype.go:53-64: a new layer type (panics when the number is taken).
+    Its name is what String(), UnsupportedLayerType and the decoded lists print."""
+    if int(num) in _LT_IN_USE:
+        raise GoPanic("Layer type already exists")
+    return OverrideLayerType(num, meta)
+
+
+def OverrideLayerType(num, meta):
+    """layertype.go:69-83"""
+    _LT_IN_USE.add(int(num))
+    _LT_NAMES[int(num)] = meta.Name
+    DecodersByLayerName[meta.Name] = meta.Decoder
+    return LayerType(num)
 
 
 class LayerClass(list):
@@ -47,6 +83,45 @@ class LayerClass(list):
 
     def LayerTypes(self):
         return list(self)
+
+
+class LayerClassSlice(list):
+    """layerclass.go:31-67: a []bool indexed by LayerType."""
+
+    def Contains(self, t):
+        return 0 <= int(t) < len(self) and bool(self[int(t)])
+
+    def LayerTypes(self):
+        return [LayerType(i) for i, v in enumerate(self) if v]
+
+
+class LayerClassMap(dict):
+    """layerclass.go:69-94: a map[LayerType]bool."""
+
+    def Contains(self, t):
+        return bool(self.get(int(t), False))
+
+    def LayerTypes(self):
+        return [LayerType(t) for t in self]
+
+
+def NewLayerClassSlice(types):
+    m = max([0] + [int(t) for t in types])
+    s = LayerClassSlice([False] * (m + 1))
+    for t in types:
+        s[int(t)] = True
+    return s
+
+
+def NewLayerClassMap(types):
+    return LayerClassMap({int(t): True for t in types})
+
+
+def NewLayerClass(types):
+    """layerclass.go:98-107: a map when any type exceeds maxLayerType (2000), else a slice."""
+    if any(int(t) > 2000 for t in types):
+        return NewLayerClassMap(types)
+    return NewLayerClassSlice(types)
 
 
 LayerTypeZero = LayerType(0)
@@ -95,6 +170,26 @@ class ChecksumVerificationResult:
     Valid: bool = False
     Correct: int = 0
     Actual: int = 0
+
+
+def ComputeChecksum(data, csum=0):
+    """checksum.go:35-50: RFC 1071 sum of big-endian 16-bit words (an odd last
+    byte as the high byte) added to csum, in uint32 arithmetic (it wraps)."""
+    b = np.frombuffer(bytes(data), np.uint8)
+    n = len(b) & ~1
+    w = b[:n].reshape(-1, 2).astype(np.uint64)
+    total = int(csum) + int((w[:, 0] << 8).sum() + w[:, 1].sum())
+    if len(b) & 1:
+        total += int(b[-1]) << 8
+    return total & 0xFFFFFFFF
+
+
+def FoldChecksum(csum):
+    """checksum.go:53-58"""
+    csum &= 0xFFFFFFFF
+    while csum > 0xFFFF:
+        csum = (csum >> 16) + (csum & 0xFFFF)
+    return ~csum & 0xFFFF
 
 
 MaxEndpointSize = 16
