@@ -566,11 +566,12 @@ class _LayersDecoder:
     raises GoPanic. `decoded` is truncated and refilled, except when `first`
     has no decoder (returned at once, layers_decoder.go:12-16)."""
 
-    def __init__(self, dlc, first, df):
+    def __init__(self, dlc, first, df, overrides=None):
         self.dlc, self.first, self.df = dlc, first, df
         self._p = DecodingLayerParser(first)
         self._p.SetDecodingLayerContainer(dlc)
         self._p.IgnorePanic = True  # panics raise (GoPanic) instead of becoming errors
+        self._p._overrides = overrides
 
     def __call__(self, data, decoded):
         if not self.dlc.Decoder(self.first)[1]:
@@ -602,6 +603,7 @@ class DecodingLayerParser:
         self.IgnoreUnsupported = False
         self.Truncated = False
         self._ctx = ctx
+        self._overrides = None  # next-layer table entries of this parser alone (DecodeFromBytes)
         dlc = DecodingLayerMap()  # NewDecodingLayerParser's default container (parser.go:226)
         for d in decoders:
             dlc = dlc.Put(d)
@@ -625,6 +627,8 @@ class DecodingLayerParser:
         from .engine import ParserConfig
         from . import layers
         ed = layers._registry_edits()  # EthernetTypeMetadata / IPProtocolMetadata edits, Register*PortLayerType
+        for k, v in (self._overrides or {}).items():
+            ed[k] = list(ed[k]) + list(v)
         key = (tuple(sorted(self._decoders)), self.IgnorePanic, self.IgnoreUnsupported, outputs,
                tuple((k, tuple(v)) for k, v in sorted(ed.items())))
         if self._cfg is None or self._cfg[0] != key:

@@ -214,6 +214,24 @@ def _be32(b, o):
     return struct.unpack_from(">I", b, o)[0]
 
 
+_NO_DECODER = 1999  # a LayerType no device parser has a decoder for
+
+
+def _tables_into(own):
+    """(value, LayerType) entries that send every next-layer lookup landing on
+    one of the types in `own` to a type without a decoder instead."""
+    def enum(t):
+        vals = set(t._default) | set(t._edits)
+        return [(v, _NO_DECODER) for v in sorted(vals) if int(t[v].LayerType) in own]
+
+    def ports(switch, override, lookup):
+        return [(p, _NO_DECODER) for p in sorted(set(switch) | set(override)) if int(lookup(p)) in own]
+
+    return dict(ethertype=enum(EthernetTypeMetadata), ipprotocol=enum(IPProtocolMetadata),
+                tcp_port=ports(_TCP_SWITCH, _tcp_override, TCPPortLayerType),
+                udp_port=ports(_UDP_SWITCH, _udp_override, UDPPortLayerType))
+
+
 class BaseLayer:
     Contents: bytes = b""
     Payload: bytes = b""
@@ -223,6 +241,20 @@ class BaseLayer:
 
     def LayerPayload(self):
         return self.Payload
+
+    def DecodeFromBytes(self, data, df):
+        """The DecodingLayer method (ethernet.go:42-55, dot1q.go:28-41,
+        ip4.go:178-271, ip6.go:221-278, 437-461, tcp.go:292-313, udp.go:30-43),
+        on the device: one packet through a parser holding only this layer,
+        whose next-layer tables lead nowhere back into it, so exactly this one
+        header is decoded. Returns the decoder's error (None on success); a
+        truncated header calls df.SetTruncated(); a decoder panic raises
+        GoPanic, as it propagates out of DecodeFromBytes in Go."""
+        from .gopacket import DecodingLayerArray, _LayersDecoder
+        types = self.CanDecode().LayerTypes()
+        dec = _LayersDecoder(DecodingLayerArray().Put(self), types[0], df, _tables_into({int(t) for t in types}))
+        _, err = dec(bytes(data), [])
+        return err
 
 
 # ---- layers/ethernet.go:22-63 ------------------------------------------------

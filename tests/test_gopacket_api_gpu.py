@@ -210,3 +210,78 @@ def test_register_port_layer_type_on_device(gp):
         assert decoded == [L.LayerTypeEthernet, L.LayerTypeIPv4, L.LayerTypeTCP] and eth.NextLayerType() == 20
     finally:
         L._reset_registry()
+
+
+class _Feedback:  # a gopacket.DecodeFeedback that records SetTruncated
+    def __init__(self):
+        self.truncated = False
+
+    def SetTruncated(self):
+        self.truncated = True
+
+
+def test_decode_from_bytes_one_layer(gp):
+    """DecodingLayer.DecodeFromBytes called directly on each struct (the
+    interface parser.go:42-60 names): on the device, exactly one header, its
+    fields as a full DecodeLayers of the packet sets them."""
+    gopacket, L, _ = gp
+    pkt = pktutil.golden_bytes("simple_tcp")
+    full = [L.Ethernet(), L.IPv4(), L.TCP()]
+    assert _parser(gp, L.LayerTypeEthernet, *full, gopacket.Payload()).DecodeLayers(pkt, []) is None
+    eth, ip4, tcp = L.Ethernet(), L.IPv4(), L.TCP()
+    assert eth.DecodeFromBytes(pkt, gopacket.NilDecodeFeedback) is None
+    assert (eth.SrcMAC, eth.DstMAC, eth.EthernetType) == (full[0].SrcMAC, full[0].DstMAC, full[0].EthernetType)
+    assert eth.NextLayerType() == L.LayerTypeIPv4 and eth.LayerPayload() == pkt[14:]
+    assert ip4.DecodeFromBytes(pkt[14:], gopacket.NilDecodeFeedback) is None
+    assert (ip4.SrcIP, ip4.DstIP, ip4.Length, ip4.Checksum) == (full[1].SrcIP, full[1].DstIP, full[1].Length,
+                                                                full[1].Checksum)
+    assert tcp.DecodeFromBytes(pkt[34:], gopacket.NilDecodeFeedback) is None
+    assert (tcp.SrcPort, tcp.DstPort, tcp.Seq, tcp.Window) == (full[2].SrcPort, full[2].DstPort, full[2].Seq,
+                                                              full[2].Window)
+    assert tcp.LayerPayload() == pkt[66:]
+
+
+def test_decode_from_bytes_stops_at_its_own_header(gp):
+    """A parser of one struct would decode QinQ's inner tag, IP-in-IP's inner
+    header, the next IPv6 extension header into the same struct; DecodeFromBytes
+    decodes the first one only."""
+    gopacket, L, _ = gp
+    inner = struct.pack(">HH", (5 << 13) | 300, 0x0800)
+    d = L.Dot1Q()
+    assert d.DecodeFromBytes(struct.pack(">HH", 100, 0x8100) + inner + bytes(20), gopacket.NilDecodeFeedback) is None
+    assert (d.VLANIdentifier, d.Type, d.LayerPayload()[:4]) == (100, 0x8100, inner)
+    ipip = bytes.fromhex("4500003c000000004004") + bytes(2) + bytes([10, 0, 0, 1, 10, 0, 0, 2])
+    inner4 = bytes.fromhex("45000028000000004006") + bytes(2) + bytes([192, 168, 0, 1, 192, 168, 0, 2])
+    ip = L.IPv4()
+    assert ip.DecodeFromBytes(ipip + inner4 + bytes(20), gopacket.NilDecodeFeedback) is None
+    assert (ip.Protocol, ip.SrcIP, ip.DstIP) == (4, bytes([10, 0, 0, 1]), bytes([10, 0, 0, 2]))
+    sk = L.IPv6ExtensionSkipper()
+    hbh = bytes([60, 0]) + bytes(6)        # HopByHop, next: Destination options
+    dst = bytes([6, 0]) + bytes(6)         # Destination options, next: TCP
+    assert sk.DecodeFromBytes(hbh + dst + bytes(20), gopacket.NilDecodeFeedback) is None
+    assert sk.NextLayerType() == L.LayerTypeIPv6Destination and sk.LayerPayload() == dst + bytes(20)
+
+
+def test_decode_from_bytes_errors_and_truncation(gp):
+    """Errors come back as the decoder's error value; a truncated header calls
+    the DecodeFeedback's SetTruncated (ip4.go:178-271, tcp.go:292-313)."""
+    gopacket, L, _ = gp
+    from oracle import oracle as O
+    pkt = pktutil.golden_bytes("simple_tcp")
+    for layer, data, kind in ((L.IPv4(), pkt[14:30], "IPV4"), (L.TCP(), pkt[34:50], "TCP"),
+                              (L.IPv4(), bytes([0x42]) + pkt[15:34], "IPV4"), (L.Ethernet(), pkt[:10], "ETHERNET")):
+        fb = _Feedback()
+        err = layer.DecodeFromBytes(data, fb)
+        assert err is not None, (kind, data.hex())
+        want = _oracle_error(O, layer, kind, data)
+        assert err.Error() == want[0] and fb.truncated == want[1], (kind, err.Error(), want)
+
+
+def _oracle_error(O, layer, kind, data):
+    """The error text and Truncated of a one-decoder parser in the oracle."""
+    p = O.OracleParser(int(layer.CanDecode().LayerTypes()[0]), [kind])
+    arr = np.frombuffer(data + bytes(16), np.uint8)
+    res = p.decode(arr, np.array([0], np.uint64), np.array([len(data)], np.uint32), nthreads=1, layouts=False)
+    st = int(res["records"][0]["status"])
+    ea = res["err_args"]
+    return p.error_string(st & 0x7F, int(ea[0]), int(ea[1])), bool(st & 0x80)
