@@ -335,11 +335,30 @@ class Dot1Q(BaseLayer):
         return EthernetTypeLayerType(self.Type)
 
 
+IPv4EvilBit, IPv4DontFragment, IPv4MoreFragments = 1 << 2, 1 << 1, 1 << 0
+
+
+class IPv4Flag(int):
+    """ip4.go:22-40"""
+
+    def String(self):
+        names = [n for bit, n in ((IPv4EvilBit, "Evil"), (IPv4DontFragment, "DF"), (IPv4MoreFragments, "MF"))
+                 if self & bit]
+        return "|".join(names)
+
+    __str__ = String
+
+
 @dataclass
 class IPv4Option:
     OptionType: int = 0
     OptionLength: int = 0
     OptionData: Optional[bytes] = None
+
+    def String(self):  # ip4.go:73-75: "IPv4Option(%v:%v)"
+        return "IPv4Option(%d:[%s])" % (self.OptionType, " ".join(str(b) for b in (self.OptionData or b"")))
+
+    __str__ = String
 
 
 class _Checksummed:
@@ -399,7 +418,7 @@ class IPv4(BaseLayer, _Checksummed):
         self.Version = d[0] >> 4
         self.TOS = d[1]
         self.Id = _be16(d, 4)
-        self.Flags = ff >> 13
+        self.Flags = IPv4Flag(ff >> 13)
         self.FragOffset = ff & 0x1FFF
         self.TTL = d[8]
         self.Protocol = d[9]
@@ -412,7 +431,7 @@ class IPv4(BaseLayer, _Checksummed):
         self.Version, self.IHL, self.TOS = int(f["ip4_version"]), int(f["ip4_ihl"]), int(f["ip4_tos"])
         self.Length, self.Id = int(f["ip4_length"]), int(f["ip4_id"])
         ff = int(f["ip4_flags_frag"])
-        self.Flags, self.FragOffset = ff >> 13, ff & 0x1FFF
+        self.Flags, self.FragOffset = IPv4Flag(ff >> 13), ff & 0x1FFF
         self.TTL, self.Protocol, self.Checksum = int(f["ip4_ttl"]), int(f["ip4_protocol"]), int(f["ip4_checksum"])
         self.SrcIP, self.DstIP = bytes(f["ip4_src"]), bytes(f["ip4_dst"])
         hl = self.IHL * 4
@@ -430,6 +449,27 @@ class IPv4(BaseLayer, _Checksummed):
 
     def NetworkFlow(self):
         return NewFlow(EndpointIPv4, self.SrcIP, self.DstIP)
+
+    def AddressTo4(self):
+        """ip4.go:295-321: both addresses in their 4-byte form, or the error."""
+        from .gopacket import GoError
+
+        def check(a):
+            c = _to4(bytes(a))
+            if c is not None:
+                return c, None
+            if len(a) == 16:
+                return None, "address is IPv6"
+            return None, "wrong length of %d bytes instead of 4" % len(a)
+
+        src, e = check(self.SrcIP)
+        if e:
+            return GoError("Invalid source IPv4 address (%s)" % e)
+        dst, e = check(self.DstIP)
+        if e:
+            return GoError("Invalid destination IPv4 address (%s)" % e)
+        self.SrcIP, self.DstIP = src, dst
+        return None
 
 
 @dataclass
@@ -650,14 +690,230 @@ class IPv6ExtensionSkipper(BaseLayer):
 
 TCPOptionKindEndList, TCPOptionKindNop, TCPOptionKindMSS, TCPOptionKindTimestamps = 0, 1, 2, 8
 TCPOptionKindMultipathTCP = 30
+_TCP_OPTION_NAMES = {0: "EndList", 1: "NOP", 2: "MSS", 3: "WindowScale", 4: "SACKPermitted", 5: "SACK", 6: "Echo",
+                     7: "EchoReply", 8: "Timestamps", 9: "PartialOrderConnectionPermitted",
+                     10: "PartialOrderServiceProfile", 11: "CC", 12: "CCNew", 13: "CCEcho", 14: "AltChecksum",
+                     15: "AltChecksumData", 30: "MultipathTCP"}  # tcp.go:62-101
+
+
+def TCPOptionKindString(k):
+    return _TCP_OPTION_NAMES.get(int(k), "Unknown(%d)" % int(k))
+
+
+# ---- layers/multipathtcp.go: MPTCP option subtypes and their structs -----------
+(MPTCPSubtypeMPCAPABLE, MPTCPSubtypeMPJOIN, MPTCPSubtypeDSS, MPTCPSubtypeADDADDR, MPTCPSubtypeREMOVEADDR,
+ MPTCPSubtypeMPPRIO, MPTCPSubtypeMPFAIL, MPTCPSubtypeMPFASTCLOSE, MPTCPSubtypeMPTCPRST) = range(9)
+_MPTCP_NAMES = ["MP_CAPABLE", "MP_JOIN", "DSS", "ADD_ADDR", "REMOVE_ADDR", "MP_PRIO", "MP_FAIL", "MP_FASTCLOSE",
+                "MP_TCPRST"]
+
+
+def MPTCPSubtypeString(k):
+    return _MPTCP_NAMES[k] if 0 <= int(k) < len(_MPTCP_NAMES) else "Unknown(%d)" % int(k)
+
+
+@dataclass
+class MPCapable:
+    Version: int = 0
+    A: bool = False
+    B: bool = False
+    C: bool = False
+    D: bool = False
+    E: bool = False
+    F: bool = False
+    G: bool = False
+    H: bool = False
+    SendKey: Optional[bytes] = None
+    ReceivKey: Optional[bytes] = None
+    DataLength: int = 0
+    Checksum: int = 0
+
+
+@dataclass
+class MPJoin:
+    Backup: bool = False
+    AddrID: int = 0
+    ReceivToken: int = 0
+    SendRandNum: int = 0
+    SendHMAC: Optional[bytes] = None
+
+
+@dataclass
+class Dss:
+    F: bool = False
+    m: bool = False
+    M: bool = False
+    a: bool = False
+    A: bool = False
+    DataAck: Optional[bytes] = None
+    DSN: Optional[bytes] = None
+    SSN: int = 0
+    DataLength: int = 0
+    Checksum: int = 0
+
+
+@dataclass
+class AddAddr:
+    IPVer: int = 0
+    E: bool = False
+    AddrID: int = 0
+    Address: Optional[bytes] = None
+    Port: int = 0
+    SendHMAC: Optional[bytes] = None
+
+
+@dataclass
+class RemAddr:
+    AddrIDs: Optional[list] = None
+
+
+@dataclass
+class MPPrio:
+    Backup: bool = False
+    AddrID: int = 0
+
+
+@dataclass
+class MPFail:
+    DSN: int = 0
+
+
+@dataclass
+class MPFClose:
+    ReceivKey: Optional[bytes] = None
+
+
+@dataclass
+class MPTcpRst:
+    U: bool = False
+    V: bool = False
+    W: bool = False
+    T: bool = False
+    Reason: int = 0
 
 
 @dataclass
 class TCPOption:
+    """tcp.go:103-117"""
     OptionType: int = 0
     OptionLength: int = 0
     OptionData: Optional[bytes] = None
     OptionMultipath: int = 0
+    OptionMPTCPMpCapable: Optional[MPCapable] = None
+    OptionMPTCPDss: Optional[Dss] = None
+    OptionMPTCPMpJoin: Optional[MPJoin] = None
+    OptionMPTCPMpPrio: Optional[MPPrio] = None
+    OptionMPTCPAddAddr: Optional[AddAddr] = None
+    OptionMTCPRemAddr: Optional[RemAddr] = None
+    OptionMTCPMPFastClose: Optional[MPFClose] = None
+    OptionMPTCPMPTcpRst: Optional[MPTcpRst] = None
+    OptionMTCPMPFail: Optional[MPFail] = None
+
+    def String(self):
+        """tcp.go:120-184"""
+        d = self.OptionData or b""
+        hd = (" 0x" + d.hex()) if d else ""
+        k = TCPOptionKindString(self.OptionType)
+        if self.OptionType == TCPOptionKindMSS and len(d) >= 2:
+            return "TCPOption(%s:%d%s)" % (k, _be16(d, 0), hd)
+        if self.OptionType == TCPOptionKindTimestamps and len(d) == 8:
+            return "TCPOption(%s:%d/%d%s)" % (k, _be32(d, 0), _be32(d, 4), hd)
+        if self.OptionType == TCPOptionKindMultipathTCP:
+            st, n, gb = self.OptionMultipath, MPTCPSubtypeString(self.OptionMultipath), lambda b: str(b).lower()
+            if st == MPTCPSubtypeMPCAPABLE:
+                return "MPTCPOption(%s Version %d)" % (n, self.OptionMPTCPMpCapable.Version)
+            if st == MPTCPSubtypeMPJOIN:
+                j = self.OptionMPTCPMpJoin
+                return "MPTCPOption(%s Backup %s;Address ID %d)" % (n, gb(j.Backup), j.AddrID)
+            if st in (MPTCPSubtypeDSS, MPTCPSubtypeMPFASTCLOSE, MPTCPSubtypeMPFAIL):
+                return "MPTCPOption(%s)" % n
+            if st == MPTCPSubtypeMPPRIO:
+                q = self.OptionMPTCPMpPrio
+                return "MPTCPOption(%s Backup %s;Address ID %d)" % (n, gb(q.Backup), q.AddrID)
+            if st == MPTCPSubtypeADDADDR:
+                a = self.OptionMPTCPAddAddr
+                from .gopacket import _ip_string
+                return "MPTCPOption(%s Address ID %d;Address %s;Port %d)" % (n, a.AddrID, _ip_string(a.Address or b""),
+                                                                           a.Port)
+            if st == MPTCPSubtypeREMOVEADDR:
+                return "MPTCPOption(%s Address ID [%s])" % (n, " ".join(str(x) for x in self.OptionMTCPRemAddr.AddrIDs))
+            if st == MPTCPSubtypeMPTCPRST:
+                r = self.OptionMPTCPMPTcpRst
+                return "MPTCPOption(%s Transient %s; Reason %d)" % (n, gb(r.T), r.Reason)
+        return "TCPOption(%s:%s)" % (k, hd)
+
+    __str__ = String
+
+
+def _mptcp_option(o, d):
+    """The MPTCP option struct tcp.go:346-527 builds from the option at d[0]
+    (d: the rest of the options area; the packet decoded without error, so its
+    lengths are ones the reference accepts)."""
+    L, st = o.OptionLength, o.OptionMultipath
+    b16 = lambda a: _be16(d, a)  # noqa: E731
+    b32 = lambda a: _be32(d, a)  # noqa: E731
+    if st == MPTCPSubtypeMPCAPABLE:
+        f = d[3]
+        c = MPCapable(d[2] & 0x0F, *(bool(f & (0x80 >> i)) for i in range(8)))
+        if L >= 12:
+            c.SendKey = bytes(d[4:12])
+        if L >= 20:
+            c.ReceivKey = bytes(d[12:20])
+        if L >= 22:
+            c.DataLength = b16(20)
+        if L == 24:
+            c.Checksum = b16(22)
+        o.OptionMPTCPMpCapable = c
+    elif st == MPTCPSubtypeMPJOIN:
+        if L == 12:
+            o.OptionMPTCPMpJoin = MPJoin(bool(d[2] & 1), d[3], b32(4), b32(8))
+        elif L == 16:
+            o.OptionMPTCPMpJoin = MPJoin(bool(d[2] & 1), d[3], SendHMAC=bytes(d[4:12]), SendRandNum=b32(12))
+        elif L == 24:
+            o.OptionMPTCPMpJoin = MPJoin(SendHMAC=bytes(d[4:24]))
+    elif st == MPTCPSubtypeDSS:
+        f = d[3]
+        x = Dss(bool(f & 0x10), bool(f & 0x08), bool(f & 0x04), bool(f & 0x02), bool(f & 0x01))
+        k = 4
+        if x.A:
+            n = 8 if x.a else 4
+            x.DataAck, k = bytes(d[k:k + n]), k + n
+        if x.M:
+            n = 8 if x.m else 4
+            x.DSN, k = bytes(d[k:k + n]), k + n
+            x.SSN, k = b32(k), k + 4
+            x.DataLength, k = b16(k), k + 2
+            if (L - k) & 0xFF == 2:
+                x.Checksum = b16(k)
+        o.OptionMPTCPDss = x
+    elif st == MPTCPSubtypeADDADDR:
+        n = L
+        if d[2] & 0x0F > 1:
+            a = AddAddr(IPVer=d[2] & 0x0F, AddrID=d[3])
+        else:
+            a = AddAddr(E=bool(d[2] & 1), AddrID=d[3])
+            if not a.E:
+                a.SendHMAC = bytes(d[L - 8:])  # to the end of the options area, as Go's data[L-8:]
+                n = (n - 8) & 0xFF
+        if n in (8, 10):
+            a.Address = bytes(d[4:8])
+        elif n in (20, 22):
+            a.Address = bytes(d[4:20])
+        if n == 10:
+            a.Port = b16(8)
+        elif n == 22:
+            a.Port = b16(20)
+        o.OptionMPTCPAddAddr = a
+    elif st == MPTCPSubtypeREMOVEADDR:
+        o.OptionMTCPRemAddr = RemAddr(list(d[3:3 + (L - 3)]))
+    elif st == MPTCPSubtypeMPPRIO:
+        o.OptionMPTCPMpPrio = MPPrio(bool(d[2] & 1), d[3] if L == 4 else 0)
+    elif st == MPTCPSubtypeMPFAIL:
+        o.OptionMTCPMPFail = MPFail(struct.unpack(">Q", bytes(d[4:12]))[0])
+    elif st == MPTCPSubtypeMPFASTCLOSE:
+        o.OptionMTCPMPFastClose = MPFClose(bytes(d[4:12]))
+    elif st == MPTCPSubtypeMPTCPRST:
+        o.OptionMPTCPMPTcpRst = MPTcpRst(bool(d[2] & 8), bool(d[2] & 4), bool(d[2] & 2), bool(d[2] & 1), d[3])
+    return o
 
 
 # ---- layers/tcp.go:19-551 ----------------------------------------------------
@@ -705,7 +961,7 @@ class TCP(BaseLayer, _Checksummed):
                 o = TCPOption(1, 1)
             elif t == TCPOptionKindMultipathTCP:
                 self.Multipath = True
-                o = TCPOption(t, opts[1], None, opts[2] >> 4)
+                o = _mptcp_option(TCPOption(t, opts[1], None, opts[2] >> 4), opts)
             else:
                 o = TCPOption(t, opts[1], opts[2:opts[1]])
             self.Options.append(o)
@@ -752,7 +1008,7 @@ def TCPOptionsFromMap(pkt, start, hlen, opt_map):
             opts.append(TCPOption(1, 1))
         elif t == TCPOptionKindMultipathTCP:
             mp = True
-            opts.append(TCPOption(t, pkt[b + 1], None, pkt[b + 2] >> 4))
+            opts.append(_mptcp_option(TCPOption(t, pkt[b + 1], None, pkt[b + 2] >> 4), pkt[b:start + hlen]))
         else:
             opts.append(TCPOption(t, pkt[b + 1], pkt[b + 2:b + pkt[b + 1]]))
     return opts, padding, mp

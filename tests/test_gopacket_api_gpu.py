@@ -285,3 +285,18 @@ def _oracle_error(O, layer, kind, data):
     st = int(res["records"][0]["status"])
     ea = res["err_args"]
     return p.error_string(st & 0x7F, int(ea[0]), int(ea[1])), bool(st & 0x80)
+
+
+def test_tcp_options_golden(gp):
+    """layers/tcp_test.go:88-163 TestPacketTCPOptionDecode / TestPacketMPTCPOptionDecode
+    through DecodeLayers: the Options list, the MP_CAPABLE struct included."""
+    gopacket, L, _ = gp
+    for name, want in (("tcp_option_mss_eol", [L.TCPOption(2, 4, bytes([32, 0])), L.TCPOption(0, 1)]),
+                       ("mptcp_capable", [L.TCPOption(2, 4, bytes([32, 0])),
+                                          L.TCPOption(30, 4, None, 0, OptionMPTCPMpCapable=L.MPCapable(Version=1)),
+                                          L.TCPOption(0, 1)])):
+        tcp = L.TCP()
+        err = _parser(gp, L.LayerTypeEthernet, L.Ethernet(), L.IPv4(), tcp, gopacket.Payload()).DecodeLayers(
+            pktutil.golden_bytes(name), [])
+        assert err is None and tcp.Options == want, (name, tcp.Options)
+        assert tcp.Padding == b"" or tcp.Padding == bytes(len(tcp.Padding))
