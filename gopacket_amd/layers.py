@@ -80,11 +80,13 @@ _ETHERTYPE_NAMES = {v: n for v, lt, n in _REG["ethertype"]}
 
 
 def IPProtocolString(p):
-    return IPProtocolMetadata[p].Name
+    """IPProtocol.String() (enums_generated.go:135-143)"""
+    return IPProtocolMetadata._name(int(p))
 
 
 def EthernetTypeString(t):
-    return EthernetTypeMetadata[t].Name
+    """EthernetType.String() (enums_generated.go:65-73)"""
+    return EthernetTypeMetadata._name(int(t))
 
 
 # ---- next-layer tables (layers/enums.go:294-390, ports.go:54-183) -----------
@@ -98,13 +100,29 @@ def EthernetTypeString(t):
 
 
 class EnumMetadata:
-    """enums.go EnumMetadata: the LayerType a value decodes as, and its name."""
+    """enums.go EnumMetadata: the decoder, the name and the LayerType of a
+    value. Go's EthernetType / IPProtocol LayerType() and String() read an
+    entry only when its DecodeWith is set (enums_generated.go:65-84,
+    135-154): an entry written without one decodes as nothing (LayerType 0)
+    and prints as unknown, whatever its LayerType and Name say."""
 
-    def __init__(self, LayerType=0, Name=""):
-        self.LayerType, self.Name = LayerType, Name
+    def __init__(self, LayerType=0, Name="", DecodeWith=None):
+        self.LayerType, self.Name, self.DecodeWith = LayerType, Name, DecodeWith
 
     def __repr__(self):
-        return "EnumMetadata(LayerType=%d, Name=%r)" % (int(self.LayerType), self.Name)
+        return "EnumMetadata(LayerType=%d, Name=%r, DecodeWith=%r)" % (int(self.LayerType), self.Name,
+                                                                       self.DecodeWith)
+
+
+class _GoDecoder:
+    """The DecodeWith of an entry initActualTypeData registered (enums.go:310-353):
+    a decoder of the reference's NewPacket path, which the hot path never calls."""
+
+    def __init__(self, name):
+        self.name = name
+
+    def __repr__(self):
+        return "decode%s" % self.name
 
 
 class _EnumTable:
@@ -116,6 +134,17 @@ class _EnumTable:
         self._default = {v: (LayerType(lt), name) for v, lt, name in rows}
         self._n, self._unknown, self._edits = n, unknown, {}
 
+    def _effective(self, v):
+        """What Go's LayerType() returns for v (0 without a DecodeWith)."""
+        m = self._edits.get(v)
+        if m is None:
+            return int(self._default.get(v, (0, ""))[0])
+        return int(m.LayerType) if m.DecodeWith is not None else 0
+
+    def _name(self, v):
+        m = self[v]
+        return m.Name if m.DecodeWith is not None else self._unknown
+
     def _check(self, v):
         v = int(v)
         if not 0 <= v < self._n:
@@ -125,19 +154,23 @@ class _EnumTable:
     def __getitem__(self, v):
         v = self._check(v)
         if v not in self._edits:
-            lt, name = self._default.get(v, (LayerType(0), self._unknown))
-            self._edits[v] = EnumMetadata(lt, name)
+            if v in self._default:
+                lt, name = self._default[v]
+                self._edits[v] = EnumMetadata(lt, name, _GoDecoder(name))
+            else:  # the zero EnumMetadata: no decoder
+                self._edits[v] = EnumMetadata(LayerType(0), "", None)
         return self._edits[v]
 
     def __setitem__(self, v, meta):
         self._edits[self._check(v)] = meta
 
     def _changed(self):
-        """(value, LayerType) of every entry whose LayerType differs from the default."""
+        """(value, LayerType) of every entry whose effective LayerType differs from the default."""
         out = []
-        for v, m in sorted(self._edits.items()):
-            if int(m.LayerType) != int(self._default.get(v, (0, ""))[0]):
-                out.append((v, int(m.LayerType)))
+        for v in sorted(self._edits):
+            lt = self._effective(v)
+            if lt != int(self._default.get(v, (0, ""))[0]):
+                out.append((v, lt))
         return out
 
 
@@ -162,13 +195,13 @@ def RegisterUDPPortLayerType(port, layerType):
 
 
 def EthernetTypeLayerType(t):
-    """EthernetType.LayerType() (enums_generated.go:76-86)."""
-    return LayerType(EthernetTypeMetadata[t].LayerType)
+    """EthernetType.LayerType() (enums_generated.go:76-84)."""
+    return LayerType(EthernetTypeMetadata._effective(EthernetTypeMetadata._check(t)))
 
 
 def IPProtocolLayerType(p):
-    """IPProtocol.LayerType() (enums_generated.go:146-156)."""
-    return LayerType(IPProtocolMetadata[p].LayerType)
+    """IPProtocol.LayerType() (enums_generated.go:146-154)."""
+    return LayerType(IPProtocolMetadata._effective(IPProtocolMetadata._check(p)))
 
 
 def TCPPortLayerType(port):
@@ -222,7 +255,7 @@ def _tables_into(own):
     one of the types in `own` to a type without a decoder instead."""
     def enum(t):
         vals = set(t._default) | set(t._edits)
-        return [(v, _NO_DECODER) for v in sorted(vals) if int(t[v].LayerType) in own]
+        return [(v, _NO_DECODER) for v in sorted(vals) if t._effective(v) in own]
 
     def ports(switch, override, lookup):
         return [(p, _NO_DECODER) for p in sorted(set(switch) | set(override)) if int(lookup(p)) in own]

@@ -35,8 +35,9 @@ def test_tables_after_init():
 
 def test_registry_edits_reach_parser_config():
     L.RegisterTCPPortLayerType(8080, L.LayerTypeDNS)
-    L.EthernetTypeMetadata[0x88B5] = L.EnumMetadata(LayerType=L.LayerTypeIPv4, Name="Local experimental")
-    L.IPProtocolMetadata[253] = L.EnumMetadata(LayerType=L.LayerTypeUDP, Name="Experimental")
+    L.EthernetTypeMetadata[0x88B5] = L.EnumMetadata(LayerType=L.LayerTypeIPv4, Name="Local experimental",
+                                                    DecodeWith="myDecoder")
+    L.IPProtocolMetadata[253] = L.EnumMetadata(LayerType=L.LayerTypeUDP, Name="Experimental", DecodeWith="myDecoder")
     assert L.TCPPortLayerType(8080) == L.LayerTypeDNS and L.EthernetTypeLayerType(0x88B5) == L.LayerTypeIPv4
     assert L.EthernetTypeString(0x88B5) == "Local experimental"
     ed = L._registry_edits()
@@ -49,9 +50,25 @@ def test_registry_edits_reach_parser_config():
     cfg2 = p._config()
     assert cfg2 is not cfg  # an edit rebuilds the device parser
     assert p._config() is cfg2  # ... once
-    L.IPProtocolMetadata[254].LayerType = L.LayerTypeTCP  # Go's in-place form
-    assert L._registry_edits()["ipprotocol"] == [(253, 45), (254, 44)] and p._config() is not cfg2
-    assert L.IPProtocolString(254) == "UnknownIPProtocol"
+    # Go's in-place form: an unregistered entry has no DecodeWith, so its LayerType()
+    # stays 0 and nothing changes (enums_generated.go:146-154); a registered one does
+    L.IPProtocolMetadata[254].LayerType = L.LayerTypeTCP
+    assert L.IPProtocolLayerType(254) == 0 and L.IPProtocolString(254) == "UnknownIPProtocol"
+    assert L._registry_edits()["ipprotocol"] == [(253, 45)] and p._config() is cfg2
+    L.IPProtocolMetadata[17].LayerType = L.LayerTypeTCP
+    assert L.IPProtocolLayerType(17) == L.LayerTypeTCP and L.IPProtocolString(17) == "UDP"
+    assert L._registry_edits()["ipprotocol"] == [(17, 44), (253, 45)] and p._config() is not cfg2
+
+
+def test_edit_without_decoder_decodes_as_nothing():
+    """An EnumMetadata written without DecodeWith: LayerType() 0 and an unknown
+    name, as Go's (enums_generated.go:65-84), so the device's table is not changed."""
+    L.EthernetTypeMetadata[0x88B5] = L.EnumMetadata(LayerType=L.LayerTypeIPv4, Name="Local experimental")
+    assert L.EthernetTypeLayerType(0x88B5) == 0 and L.EthernetTypeString(0x88B5) == "UnknownEthernetType"
+    assert L._registry_edits()["ethertype"] == []
+    L.EthernetTypeMetadata[0x0800] = L.EnumMetadata(LayerType=L.LayerTypeIPv4, Name="IPv4")  # no decoder now
+    assert L.EthernetTypeLayerType(0x0800) == 0 and L._registry_edits()["ethertype"] == [(0x0800, 0)]
+    assert L.EthernetTypeMetadata[0x1234].Name == "" and L.EthernetTypeMetadata[0x0800].DecodeWith is None
 
 
 @pytest.mark.parametrize("form", [G.DecodingLayerMap, G.DecodingLayerSparse, G.DecodingLayerArray])

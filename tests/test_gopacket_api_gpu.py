@@ -205,9 +205,14 @@ def test_register_port_layer_type_on_device(gp):
         assert tcp.NextLayerType() == L.LayerTypeDNS
         odd = pkt[:12] + b"\x88\xb5" + pkt[14:]
         assert p.DecodeLayers(odd, decoded) is None and decoded == [L.LayerTypeEthernet]  # unknown: success (P1)
-        L.EthernetTypeMetadata[0x88B5] = L.EnumMetadata(LayerType=L.LayerTypeIPv4, Name="Local experimental")
+        L.EthernetTypeMetadata[0x88B5] = L.EnumMetadata(LayerType=L.LayerTypeIPv4, Name="Local experimental",
+                                                        DecodeWith="myDecoder")
         assert p.DecodeLayers(odd, decoded) == gopacket.UnsupportedLayerType(L.LayerTypeDNS)
         assert decoded == [L.LayerTypeEthernet, L.LayerTypeIPv4, L.LayerTypeTCP] and eth.NextLayerType() == 20
+        # an entry written without DecodeWith decodes as nothing (enums_generated.go:76-84): LayerTypeZero ends it
+        L.EthernetTypeMetadata[0x0800] = L.EnumMetadata(LayerType=L.LayerTypeIPv4, Name="IPv4")
+        assert p.DecodeLayers(pkt, decoded) is None and decoded == [L.LayerTypeEthernet]
+        assert eth.NextLayerType() == 0
     finally:
         L._reset_registry()
 
