@@ -396,6 +396,29 @@ class IPv4Option:
 
 class _Checksummed:
     _csum = None  # (error, ChecksumVerificationResult) set from the device record
+    _pseudoheader = None  # tcpipchecksum.pseudoheader (TCP, UDP)
+
+    def SetNetworkLayerForChecksum(self, l):
+        """tcpip.go:75-85 (TCP and UDP): the IPv4 or IPv6 layer whose addresses
+        the pseudo-header of ComputeChecksum uses."""
+        from .gopacket import GoError
+        if not hasattr(l, "_pseudoheader_checksum"):
+            return GoError("cannot use layer type %s for tcp checksum network layer" % l.LayerType().String())
+        self._pseudoheader = l
+        return None
+
+    def _compute_checksum(self, header_and_payload, proto):
+        """tcpipchecksum.computeChecksum (tcpip.go:44-62): (uint32 sum, error)."""
+        from .gopacket import ComputeChecksum, GoError
+        if self._pseudoheader is None:
+            return 0, GoError("TCP/IP layer 4 checksum cannot be computed without network layer... "
+                              "call SetNetworkLayerForChecksum to set which layer to use")
+        n = len(header_and_payload)
+        csum, err = self._pseudoheader._pseudoheader_checksum()
+        if err is not None:
+            return 0, err
+        csum += proto + (n & 0xFFFF) + (n >> 16)
+        return ComputeChecksum(header_and_payload, csum & 0xFFFFFFFF), None
 
     def VerifyChecksum(self):
         """The device's checksum verification of this layer (see DecodingLayerParser)."""
@@ -504,6 +527,14 @@ class IPv4(BaseLayer, _Checksummed):
         self.SrcIP, self.DstIP = src, dst
         return None
 
+    def _pseudoheader_checksum(self):  # tcpip.go:19-28
+        err = self.AddressTo4()
+        if err is not None:
+            return 0, err
+        s_, d_ = self.SrcIP, self.DstIP
+        csum = ((s_[0] + s_[2]) << 8) + s_[1] + s_[3] + ((d_[0] + d_[2]) << 8) + d_[1] + d_[3]
+        return csum, None
+
 
 @dataclass
 class IPv6HopByHopOption:
@@ -597,6 +628,24 @@ class IPv6(BaseLayer, _Checksummed):
 
     def NetworkFlow(self):
         return NewFlow(EndpointIPv6, self.SrcIP, self.DstIP)
+
+    def AddressTo16(self):
+        """ip6.go:742-761: an error unless both addresses are 16 bytes."""
+        from .gopacket import GoError
+        for which, a in (("source", self.SrcIP), ("destination", self.DstIP)):
+            if len(a) != 16:
+                e = "address is IPv4" if len(a) == 4 else "wrong length of %d bytes instead of 16" % len(a)
+                return GoError("Invalid %s IPv6 address (%s)" % (which, e))
+        return None
+
+    def _pseudoheader_checksum(self):  # tcpip.go:30-42
+        err = self.AddressTo16()
+        if err is not None:
+            return 0, err
+        csum = 0
+        for i in range(0, 16, 2):
+            csum += (self.SrcIP[i] << 8) + self.SrcIP[i + 1] + (self.DstIP[i] << 8) + self.DstIP[i + 1]
+        return csum & 0xFFFFFFFF, None
 
 
 def _map_bits(opt_map):
@@ -1024,6 +1073,13 @@ class TCP(BaseLayer, _Checksummed):
 
     def TransportFlow(self):
         return NewFlow(EndpointTCPPort, self.sPort, self.dPort)
+
+    def ComputeChecksum(self):
+        """tcp.go:251-257: (uint16, error) over Contents + Payload as they are
+        (the header's own Checksum field included: 0 for a correct segment)."""
+        from .gopacket import FoldChecksum
+        csum, err = self._compute_checksum(bytes(self.Contents) + bytes(self.Payload), 6)
+        return (0, err) if err is not None else (FoldChecksum(csum), None)
 
 
 def TCPOptionsFromMap(pkt, start, hlen, opt_map):

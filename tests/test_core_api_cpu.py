@@ -115,3 +115,30 @@ def test_mptcp_option_structs():
     r = opt(4, 8, bytes([0x8B, 5])).OptionMPTCPMPTcpRst
     assert (r.U, r.V, r.W, r.T, r.Reason) == (True, False, True, True, 5)
     assert str(L.TCPOption(30, 4, None, 8, OptionMPTCPMPTcpRst=r)) == "MPTCPOption(MP_TCPRST Transient true; Reason 5)"
+
+
+def test_tcp_compute_checksum_and_network_layer():
+    """tcp.go:251-257 ComputeChecksum over tcpip.go:19-85's pseudo-header:
+    0 over a correct segment, the checksum itself with the field zeroed
+    (simple_tcp's 0x9a8f, decode_test.go:386-492); the errors without a
+    network layer or with a non-IP one; IPv6.AddressTo16 (ip6.go:742-761)."""
+    from gopacket_amd import layers as L
+    pkt = pktutil.golden_bytes("simple_tcp")
+    ip4, tcp = L.IPv4(), L.TCP()
+    ip4._hydrate(pkt[14:])
+    tcp._hydrate(pkt[34:34 + ip4.Length - 20])
+    csum, err = tcp.ComputeChecksum()
+    assert csum == 0 and err.Error().startswith("TCP/IP layer 4 checksum cannot be computed without network layer")
+    assert tcp.SetNetworkLayerForChecksum(L.Ethernet()).Error() == \
+        "cannot use layer type Ethernet for tcp checksum network layer"
+    assert tcp.SetNetworkLayerForChecksum(ip4) is None
+    assert tcp.ComputeChecksum() == (0, None)
+    tcp.Contents = tcp.Contents[:16] + b"\x00\x00" + tcp.Contents[18:]
+    assert tcp.ComputeChecksum() == (0x9a8f, None)
+    ip6 = L.IPv6()
+    ip6.SrcIP, ip6.DstIP = bytes(16), b"\x01\x02\x03\x04"
+    assert ip6.AddressTo16().Error() == "Invalid destination IPv6 address (address is IPv4)"
+    assert tcp.SetNetworkLayerForChecksum(ip6) is None
+    assert tcp.ComputeChecksum()[1].Error() == "Invalid destination IPv6 address (address is IPv4)"
+    ip6.DstIP = bytes(15) + b"\x01"
+    assert ip6.AddressTo16() is None and tcp.ComputeChecksum()[1] is None
