@@ -276,8 +276,8 @@ class BaseLayer:
         return self.Payload
 
     def DecodeFromBytes(self, data, df):
-        """The DecodingLayer method (ethernet.go:42-55, dot1q.go:28-41,
-        ip4.go:178-271, ip6.go:221-278, 437-461, tcp.go:292-313, udp.go:30-43),
+        """The DecodingLayer method (ethernet.go:42-63, dot1q.go:30-41,
+        ip4.go:178-271, ip6.go:221-278, 443-451, tcp.go:291-551, udp.go:30-56),
         on the device: one packet through a parser holding only this layer,
         whose next-layer tables lead nowhere back into it, so exactly this one
         header is decoded. Returns the decoder's error (None on success); a
