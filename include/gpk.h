@@ -38,6 +38,9 @@
  *                                          dot1q.go:28-41, ip4.go:178-271, ip6.go:221-278,
  *                                          tcp.go:292-313, udp.go:30-43), from the layouts of a
  *                                          decode: the fields a consumer reads after DecodeLayers
+ *   gpk_stop                               a break out of the ReadPacketData loop (ngread.go:629-632,
+ *                                          afpacket.go:335-367) for the calls that push results
+ *                                          through callbacks (gpk_replay_file, gpk_tpacket_pump)
  *   gpk_format_error                       the error values DecodeLayers returns
  *                                          (UnsupportedLayerType parser.go:321-327, panicToError
  *                                          :329-333, and every fmt.Errorf/errors.New site of
