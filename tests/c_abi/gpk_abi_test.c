@@ -400,9 +400,93 @@ static int replay_checks(int nfiles, char** files) {
   return 0;
 }
 
+/* ---- the capture reader's interface beyond ReadPacketData, from C ---------- *
+ * What a cgo binding of pcapgo.NgReader does: index a file in one call, then
+ * read the options of its packets (ReadPacketDataWithOptions), the name
+ * records (Name / NNames) and the statistics callbacks. Pinned by the
+ * reference's tests: ngread_test.go:2028-2100 (tests/epb.pcapng's options) and
+ * ngread_nrb_test.go:50-79 (tests/le/test016.pcapng's name records). */
+static unsigned char* slurp_file(const char* dir, const char* name, size_t* len) {
+  char path[1024];
+  snprintf(path, sizeof(path), "%s/%s", dir, name);
+  FILE* f = fopen(path, "rb");
+  if (!f) return NULL;
+  fseek(f, 0, SEEK_END);
+  long n = ftell(f);
+  fseek(f, 0, SEEK_SET);
+  unsigned char* b = (unsigned char*)malloc((size_t)n + 1);
+  if (fread(b, 1, (size_t)n, f) != (size_t)n) n = 0;
+  fclose(f);
+  *len = (size_t)n;
+  return b;
+}
+
+static int capture_checks(const char* dir) {
+  size_t len = 0;
+  unsigned char* raw = slurp_file(dir, "epb.pcapng", &len);
+  CHECK(raw && len > 0, "epb.pcapng");
+  if (!raw) return 1;
+  gpk_capreader* r = NULL;
+  CHECK(gpk_capreader_create(&r, GPK_CAP_PCAPNG, 0) == GPK_OK, "create");
+  CHECK(gpk_capreader_keep_options(r, 1) == GPK_OK, "keep_options");
+  uint64_t off[8], n = 0, used = 0;
+  uint32_t cap[8];
+  int rc = gpk_capreader_index(r, raw, len, 1, off, cap, NULL, 8, &n, &used);
+  CHECK(rc == GPK_CAP_END && n >= 1, "index epb.pcapng: %d, %llu packets", rc, (unsigned long long)n);
+  const uint8_t* tlv = NULL;
+  uint64_t nb = 0;
+  CHECK(gpk_capreader_packet_options(r, 0, &tlv, &nb) == GPK_OK, "packet_options");
+  /* the option codes in order: 2 comments, flags, 2 hashes, drop count, packet id, queue, 2 verdicts */
+  const uint16_t want[] = {1, 1, 2, 3, 3, 4, 5, 6, 7, 7};
+  int k = 0, good = 1;
+  uint64_t packet_id = 0;
+  for (uint64_t q = 0; q + 8 <= nb; k++) {
+    uint16_t code;
+    uint32_t olen;
+    memcpy(&code, tlv + q, 2);
+    memcpy(&olen, tlv + q + 4, 4);
+    if (k >= 10 || code != want[k]) good = 0;
+    if (code == 5 && olen >= 8) memcpy(&packet_id, tlv + q + 8, 8); /* little-endian, as the reference reads it */
+    if (k == 0 && (olen != 17 || memcmp(tlv + q + 8, "this is a comment", 17) != 0)) good = 0;
+    q += 8 + ((olen + 3u) & ~3u);
+  }
+  CHECK(good && k == 10, "epb.pcapng options: %d records", k);
+  CHECK(packet_id == 0x1234567890abcdefull, "PacketID %llx", (unsigned long long)packet_id);
+  gpk_capreader_destroy(r);
+  free(raw);
+
+  raw = slurp_file(dir, "le/test016.pcapng", &len);
+  CHECK(raw && len > 0, "le/test016.pcapng");
+  if (!raw) return 1;
+  CHECK(gpk_capreader_create(&r, GPK_CAP_PCAPNG, GPK_NG_SKIP_UNKNOWN_VERSION) == GPK_OK, "create");
+  /* read to io.EOF, past other errors (readNgNRB, ngread_nrb_test.go:11-47) */
+  uint64_t pos = 0;
+  for (int calls = 0; calls < 100; calls++) {
+    rc = gpk_capreader_index(r, raw + pos, len - pos, 1, off, cap, NULL, 8, &n, &used);
+    pos += used;
+    int is_eof = 0;
+    if (rc == GPK_CAP_END) {
+      gpk_capreader_error(r, NULL, 0, &is_eof, NULL);
+      if (is_eof) break;
+    }
+  }
+  CHECK(gpk_capreader_nnames(r) == 10, "test016: %d name records", gpk_capreader_nnames(r));
+  int kind = 0, alen = 0, nn = 0;
+  uint8_t addr[24];
+  char names[256];
+  gpk_capreader_name(r, 2, &kind, addr, &alen, &nn, names, sizeof(names));
+  CHECK(kind == 1 && alen == 4 && addr[0] == 10 && addr[1] == 1 && addr[2] == 2 && addr[3] == 3,
+        "test016 record 2: kind %d, %d address bytes", kind, alen);
+  gpk_capreader_name(r, 6, &kind, addr, &alen, &nn, names, sizeof(names));
+  CHECK(nn >= 1 && strcmp(names, "qux.example.com") == 0, "test016 record 6: %s", names);
+  gpk_capreader_destroy(r);
+  free(raw);
+  return 0;
+}
+
 int main(int argc, char** argv) {
   if (argc < 3) {
-    fprintf(stderr, "usage: %s host|decode <golden dir> | replay <capture>...\n", argv[0]);
+    fprintf(stderr, "usage: %s host|decode <golden dir> | capture <pcapgo golden dir> | replay <capture>...\n", argv[0]);
     return 2;
   }
   host_checks();
@@ -411,6 +495,9 @@ int main(int argc, char** argv) {
     if (rc) return rc;
   } else if (strcmp(argv[1], "replay") == 0) {
     int rc = replay_checks(argc - 2, argv + 2);
+    if (rc) return rc;
+  } else if (strcmp(argv[1], "capture") == 0) {
+    int rc = capture_checks(argv[2]);
     if (rc) return rc;
   }
   if (failures) {

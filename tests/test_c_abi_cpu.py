@@ -20,3 +20,14 @@ def test_c_abi_host_mode():
                          text=True, timeout=120)
     assert out.returncode == 0, out.stdout + out.stderr
     assert "all checks passed" in out.stdout
+
+
+def test_c_abi_capture_reader_interface():
+    """The capture reader's interface beyond ReadPacketData from C, as a cgo
+    binding uses it: EPB options (ngread_test.go:2028-2100) and name records
+    (ngread_nrb_test.go:50-79) of the reference's own capture files."""
+    exe = build_c_abi_test()
+    out = subprocess.run([exe, "capture", os.path.join(ROOT, "tests", "golden", "pcapgo")], capture_output=True,
+                         text=True, timeout=120)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert "all checks passed (capture)" in out.stdout
