@@ -1324,7 +1324,9 @@ def main():
     ap.add_argument("--no-narrow", action="store_true",
                     help="skip the narrow-record timing beside each config (it launches the same kernel symbols: "
                          "keep it out of kernel traces that average by name)")
-    ap.add_argument("--pcie", action="store_true", help="also time the host-buffer path (PCIe-inclusive)")
+    ap.add_argument("--pcie", action="store_true", default=True,
+                    help="time the host-buffer path too (PCIe-inclusive, N=1; on by default)")
+    ap.add_argument("--no-pcie", dest="pcie", action="store_false", help="skip the PCIe-inclusive row")
     ap.add_argument("--c5", type=float, default=10.0, metavar="GIB",
                     help="config C5: replay a GIB-GiB pcapng end to end (gpk_replay_file); 0 = skip")
     ap.add_argument("--afpacket", type=int, default=0, metavar="MPKTS",
