@@ -649,8 +649,8 @@ def c5_cpu(path, threads, nbytes=256 << 20):
                 raise RuntimeError("c5_cpu: gpk_capreader_index_all returned %d with %d packets" % (rc, x.n))
             walk.append(time.perf_counter() - t0)
             n = x.n
-            off = np.ctypeslib.as_array(ctypes.cast(x.offsets, ctypes.POINTER(ctypes.c_uint64)), (n,)).copy()
-            cap = np.ctypeslib.as_array(ctypes.cast(x.caplens, ctypes.POINTER(ctypes.c_uint32)), (n,)).copy()
+            off = _lib.host_view(x.offsets, n, np.uint64).copy()
+            cap = _lib.host_view(x.caplens, n, np.uint32).copy()
             L.gpk_capindex_free(ctypes.byref(x))
             L.gpk_capreader_destroy(h)
         w = min(walk)

@@ -362,6 +362,27 @@ def check(rc):
     return rc
 
 
+class _Mem:
+    __slots__ = ("__array_interface__",)
+
+
+def host_view(ptr, count, dtype):
+    """A numpy array of `count` elements of `dtype` over library-owned host
+    memory at `ptr` (an int or ctypes pointer), without copying. Built from the
+    array interface rather than np.ctypeslib.as_array: that creates a ctypes
+    array type per distinct length, which ctypes caches for the life of the
+    process (about 4.5 KB each), so callbacks that see batches of varying size
+    grew the process without bound."""
+    dt = np.dtype(dtype)
+    if ptr is not None and not isinstance(ptr, int):  # a ctypes pointer or c_void_p
+        ptr = ctypes.cast(ptr, ctypes.c_void_p).value
+    m = _Mem()
+    m.__array_interface__ = {"data": (int(ptr or 0), False), "shape": (int(count),), "version": 3,
+                             "typestr": dt.str if dt.fields is None else "|V%d" % dt.itemsize}
+    a = np.asarray(m)
+    return a if dt.fields is None else a.view(dt)
+
+
 _synth = None
 
 

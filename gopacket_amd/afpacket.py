@@ -149,7 +149,7 @@ class TPacket:
         ring, nbytes, ver, fd = ctypes.c_void_p(), ctypes.c_uint64(), ctypes.c_int(), ctypes.c_int()
         L.gpk_tpacket_ring(self.h, ctypes.byref(ring), ctypes.byref(nbytes), ctypes.byref(ver), ctypes.byref(fd))
         self.ring_ptr, self.ring_bytes, self.version, self.fd = ring.value, nbytes.value, ver.value, fd.value
-        self.ring = np.ctypeslib.as_array(ctypes.cast(ring, ctypes.POINTER(ctypes.c_uint8)), (self.ring_bytes,))
+        self.ring = _lib.host_view(ring, self.ring_bytes, np.uint8)
         self._side = np.zeros(1 << 20, np.uint8)
 
     def _error(self):
@@ -273,15 +273,11 @@ class TPacket:
         @guarded
         def pcb(user, first, n, data, cap):
             if n:
-                got_packets[:] = [(first, n, (
-                    np.ctypeslib.as_array(ctypes.cast(data, ctypes.POINTER(ctypes.c_uint64)), (n,)),
-                    np.ctypeslib.as_array(ctypes.cast(cap, ctypes.POINTER(ctypes.c_uint32)), (n,))))]
+                got_packets[:] = [(first, n, (_lib.host_view(data, n, np.uint64), _lib.host_view(cap, n, np.uint32)))]
 
         @guarded
         def fcb(user, first, n, f):
-            got_fields[:] = [(first, n, np.ctypeslib.as_array(ctypes.cast(f, ctypes.POINTER(ctypes.c_uint8)),
-                                                               (n * 128,)).view(_lib.FIELDS_DTYPE)
-                              if n else np.zeros(0, _lib.FIELDS_DTYPE))]
+            got_fields[:] = [(first, n, _lib.host_view(f, n, _lib.FIELDS_DTYPE) if n else np.zeros(0, _lib.FIELDS_DTYPE))]
 
         def cb(*args):
             guarded(_cb)(*args)
@@ -289,13 +285,9 @@ class TPacket:
         def _cb(user, first, n, rec, err, fl, ci, cap):
             if not n:
                 return
-            views = (np.ctypeslib.as_array(ctypes.cast(rec, ctypes.POINTER(ctypes.c_uint8)), (n * 16,)).view(
-                         _lib.RECORD_DTYPE),
-                     np.ctypeslib.as_array(ctypes.cast(err, ctypes.POINTER(ctypes.c_uint32)), (2 * n,)),
-                     np.ctypeslib.as_array(ctypes.cast(fl, ctypes.POINTER(ctypes.c_uint64)), (3 * n,)),
-                     np.ctypeslib.as_array(ctypes.cast(ci, ctypes.POINTER(ctypes.c_uint8)), (n * 24,)).view(
-                         _lib.TPINFO_DTYPE),
-                     np.ctypeslib.as_array(ctypes.cast(cap, ctypes.POINTER(ctypes.c_uint32)), (n,)))
+            views = (_lib.host_view(rec, n, _lib.RECORD_DTYPE), _lib.host_view(err, 2 * n, np.uint32),
+                     _lib.host_view(fl, 3 * n, np.uint64), _lib.host_view(ci, n, _lib.TPINFO_DTYPE),
+                     _lib.host_view(cap, n, np.uint32))
             if fields:  # the library calls fields_cb for the same packets right before this
                 if not got_fields or got_fields[0][:2] != (first, n):
                     raise RuntimeError("no layer fields delivered for packets %d..%d" % (first, first + n))

@@ -238,17 +238,15 @@ class Context:
         def pcb(user, first, n, base, nbytes, off, cap):
             if not n:
                 return
-            o = np.ctypeslib.as_array(ctypes.cast(off, ctypes.POINTER(ctypes.c_uint64)), (n,))
-            c = np.ctypeslib.as_array(ctypes.cast(cap, ctypes.POINTER(ctypes.c_uint32)), (n,))
-            data = np.ctypeslib.as_array(ctypes.cast(base, ctypes.POINTER(ctypes.c_uint8)), (max(nbytes, 1),))
+            o = _lib.host_view(off, n, np.uint64)
+            c = _lib.host_view(cap, n, np.uint32)
+            data = _lib.host_view(base, max(nbytes, 1), np.uint8)
             got_packets[:] = [(first, n, (data, o, c))]
         got_fields = []  # the current launch's fields (fields_cb runs right before cb)
 
         @guarded
         def fcb(user, first, n, f):
-            got_fields[:] = [(first, n, np.ctypeslib.as_array(ctypes.cast(f, ctypes.POINTER(ctypes.c_uint8)),
-                                                               (n * 128,)).view(_lib.FIELDS_DTYPE)
-                              if n else np.zeros(0, _lib.FIELDS_DTYPE))]
+            got_fields[:] = [(first, n, _lib.host_view(f, n, _lib.FIELDS_DTYPE) if n else np.zeros(0, _lib.FIELDS_DTYPE))]
 
         def cb(*args):
             guarded(_cb)(*args)
@@ -256,13 +254,9 @@ class Context:
         def _cb(user, first, n, rec, err, fl, ci, cap):
             if not n:
                 return
-            views = (np.ctypeslib.as_array(ctypes.cast(rec, ctypes.POINTER(ctypes.c_uint8)), (n * 16,)).view(
-                         _lib.RECORD_DTYPE),
-                     np.ctypeslib.as_array(ctypes.cast(err, ctypes.POINTER(ctypes.c_uint32)), (2 * n,)),
-                     np.ctypeslib.as_array(ctypes.cast(fl, ctypes.POINTER(ctypes.c_uint64)), (3 * n,)),
-                     np.ctypeslib.as_array(ctypes.cast(ci, ctypes.POINTER(ctypes.c_uint8)), (n * 24,)).view(
-                         _lib.CAPINFO_DTYPE),
-                     np.ctypeslib.as_array(ctypes.cast(cap, ctypes.POINTER(ctypes.c_uint32)), (n,)))
+            views = (_lib.host_view(rec, n, _lib.RECORD_DTYPE), _lib.host_view(err, 2 * n, np.uint32),
+                     _lib.host_view(fl, 3 * n, np.uint64), _lib.host_view(ci, n, _lib.CAPINFO_DTYPE),
+                     _lib.host_view(cap, n, np.uint32))
             if fields:  # the library calls fields_cb for the same packets right before this
                 if not got_fields or got_fields[0][:2] != (first, n):
                     raise RuntimeError("no layer fields delivered for packets %d..%d" % (first, first + n))

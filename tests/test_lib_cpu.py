@@ -83,3 +83,33 @@ def test_gopacket_api_objects():
     e = gopacket.Endpoint(gopacket.EndpointTCPPort, bytes([0, 80]))
     assert e.String() == "80"
     assert gopacket.UnsupportedLayerType(107).Error() == "No decoder for layer type DNS"
+
+
+def _rss_mib():
+    for line in open("/proc/self/status"):
+        if line.startswith("VmRSS:"):
+            return int(line.split()[1]) / 1024
+    return 0.0
+
+
+def test_host_view_is_a_view_and_does_not_grow_the_process():
+    """The replay and pump callbacks see library memory through _lib.host_view.
+    Its arrays alias the memory (same address, writes visible), carry the
+    record dtypes, and making them for 20 000 distinct lengths costs no memory
+    (np.ctypeslib.as_array caches a ctypes array type per length: about 90 MB
+    here, without bound in a long capture)."""
+    import numpy as np
+    buf = np.arange(1 << 20, dtype=np.uint8)
+    p = buf.ctypes.data
+    v = _lib.host_view(p, 4096, np.uint32)
+    assert v.ctypes.data == p and np.array_equal(v, buf[:16384].view(np.uint32))
+    v[0] = 0xDEADBEEF
+    assert buf[:4].view(np.uint32)[0] == 0xDEADBEEF
+    r = _lib.host_view(ctypes.cast(p, ctypes.POINTER(ctypes.c_uint8)), 100, _lib.RECORD_DTYPE)
+    assert r.dtype == _lib.RECORD_DTYPE and r.ctypes.data == p and r.tobytes() == buf[:1600].tobytes()
+    assert _lib.host_view(p, 10, _lib.CAPINFO_DTYPE).tobytes() == buf[:240].tobytes()
+    r0 = _rss_mib()
+    for n in range(1000, 21000):
+        _lib.host_view(p, n, _lib.RECORD_DTYPE)
+        _lib.host_view(p, 3 * n, np.uint64)
+    assert _rss_mib() - r0 < 16
