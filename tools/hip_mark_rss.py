@@ -40,6 +40,26 @@ def main(n=int(os.environ.get("ITERS", "50000"))):
                 hip.hipStreamSynchronize(agg)
         hip.hipDeviceSynchronize()
         print("%d iterations %-16s rss %+.1f MiB" % (n, variant, rss_mib() - r0), flush=True)
+    # the replay's slot pattern: three streams in turn, each copy waiting for the previous slot's
+    # "sent" event on another stream, then recording its own; the consumer synchronizes each slot
+    ss = [mk_stream() for _ in range(3)]
+    es = [mk_event() for _ in range(3)]
+    dbuf, hbuf = ctypes.c_void_p(), ctypes.c_void_p()
+    assert hip.hipMalloc(ctypes.byref(dbuf), ctypes.c_size_t(1 << 20)) == 0
+    assert hip.hipHostMalloc(ctypes.byref(hbuf), ctypes.c_size_t(1 << 20), 0) == 0
+    for variant in ("copy-chain", "copy-chain", "copy-nowait"):
+        r0 = rss_mib()
+        m = n // 5
+        for i in range(m):
+            k = i % 3
+            if variant == "copy-chain":
+                hip.hipStreamWaitEvent(ss[k], es[(k + 2) % 3], 0)
+            hip.hipMemcpyAsync(dbuf, hbuf, ctypes.c_size_t(1 << 16), 1, ss[k])
+            hip.hipEventRecord(es[k], ss[k])
+            hip.hipStreamSynchronize(ss[(k + 2) % 3])
+        hip.hipDeviceSynchronize()
+        print("%d iterations %-16s rss %+.1f MiB (%.2f KB per iteration)" % (
+            m, variant, rss_mib() - r0, (rss_mib() - r0) * 1024 / m), flush=True)
 
 
 if __name__ == "__main__":
