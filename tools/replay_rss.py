@@ -50,10 +50,19 @@ def main(reps=int(os.environ.get("REPS", "60"))):
             raw()
         gc.collect()
         if os.environ.get("ONLY_RAW") == "1":
+            class MallInfo2(ctypes.Structure):
+                _fields_ = [(f, ctypes.c_size_t) for f in ("arena", "ordblks", "smblks", "hblks", "hblkhd", "usmblks",
+                                                            "fsmblks", "uordblks", "fordblks", "keepcost")]
+            libc = ctypes.CDLL("libc.so.6")
+            libc.mallinfo2.restype = MallInfo2
+            m0 = libc.mallinfo2()
             r0, calls[0] = rss_mib(), 0
             for _ in range(reps):
                 raw()
             gc.collect()
+            m1 = libc.mallinfo2()
+            print("malloc (main arena) in use %+.1f MiB, mmapped blocks %+.1f MiB (%+d)" % (
+                (m1.uordblks - m0.uordblks) / 2**20, (m1.hblkhd - m0.hblkhd) / 2**20, m1.hblks - m0.hblks), flush=True)
             print("%s: %d calls, %d batches: rss %+.1f MiB, %.2f KB per call, %.2f KB per batch" % (
                 shape, reps, calls[0], rss_mib() - r0, (rss_mib() - r0) * 1024 / reps,
                 (rss_mib() - r0) * 1024 / max(calls[0], 1)), flush=True)
