@@ -957,8 +957,10 @@ static int replay_file(gpk_ctx* ctx, const gpk_parser* parser, const char* path,
         st = gpk_capreader_index_all(rd, S.host + base_off + pos, L - pos, eof ? 1 : 0, walk_threads, &xi, &used);
         if (st >= 0) {
           for (uint64_t i = 0; i < xi.n; i++) xi.offsets[i] += pos;
-          if (xi.n) chunks.push_back({G, xi});
+          const uint64_t first = G;
           G += xi.n;
+          if (xi.n) chunks.push_back({first, xi});
+          else gpk_capindex_free(&xi);  // an empty index still holds its arrays (~1.8 MB leaked per slot before)
           xi = gpk_capindex{};
         }
       } else {
@@ -993,6 +995,7 @@ static int replay_file(gpk_ctx* ctx, const gpk_parser* parser, const char* path,
     stats->index_s += now_s() - t_ix;
     const double t_walked = now_s();
     if (st < 0) {
+      gpk_capindex_free(&xi);
       rc = st;
       finished = true;
       break;
