@@ -424,3 +424,37 @@ def test_replay_packets_and_hydrate(gpu_ctx, capture):
     assert st["packets"] == len(pk) == sum(seen)
     with pytest.raises(ValueError):
         gpu_ctx.replay_file(device_parser(CONFIGS["statsassembly"]), path, packets=True)
+
+
+def test_replay_device_walk_holds_no_heap(gpu_ctx, tmp_path):
+    """Every staging slot's tail goes through the host reader after the device
+    walk; its index, empty or not, is freed (an empty one leaked ~1.8 MB per
+    slot before round 6's fix). 12 replays of ~50 slots each must leave glibc's
+    heap in use where it was (mallinfo2), within a few MB."""
+    import ctypes
+    from gopacket_amd import _lib
+
+    class MallInfo2(ctypes.Structure):
+        _fields_ = [(f, ctypes.c_size_t) for f in ("arena", "ordblks", "smblks", "hblks", "hblkhd", "usmblks",
+                                                    "fsmblks", "uordblks", "fordblks", "keepcost")]
+
+    libc = ctypes.CDLL("libc.so.6")
+    if not hasattr(libc, "mallinfo2"):
+        pytest.skip("glibc without mallinfo2")
+    libc.mallinfo2.restype = MallInfo2
+    path = str(tmp_path / "c4.pcapng")
+    n = 500_000
+    assert _lib.synth_lib().gpk_synth_write_pcapng(path.encode(), 4, 0, n, 8) > 0
+    parser = device_parser(CONFIGS["statsassembly"])
+    shape = dict(slot_bytes=4 << 20, slots=3, batch_pkts=1 << 16)
+
+    def run():
+        _, st = gpu_ctx.replay_file(parser, path, collect=False, on_batch=lambda *a: None, **shape)
+        assert st["packets"] == n and st["error"] == "EOF" and st["device_walk_packets"] > 0, st
+        return st["slots"]
+
+    run()
+    h0 = libc.mallinfo2().uordblks
+    slots = sum(run() for _ in range(12))
+    grown = (libc.mallinfo2().uordblks - h0) / 2**20
+    assert slots >= 400 and grown < 16, (slots, grown)
